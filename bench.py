@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident SSTable decode (BASELINE.json config 2).
+
+One step = one hg_decode_dev_async over a 1 GiB SSTable already in HBM
+(8,134,407 records of 16 B big-endian counter keys / 100 B random values,
+seed 2, built on the device): boundary discovery + one span per record.
+With --gpus N (launched by torch.distributed.run) every rank decodes its own
+table on its own GPU: weak scaling, no collectives on the data path (the only
+collectives are the timing barrier and the max-over-ranks reduction).
+
+Prints ONE JSON line (rank 0).  `roofline` prices the decode kernel against
+HBM: algorithmic bytes = L + 16 n (read the table once, write 16-byte spans),
+divided by the launch time measured with HIP events on the stream the kernel
+runs on.  `cpu_baseline` times the oracle (the C restatement of the
+reference's Rust decode, with its per-record ownership pattern) on one host
+core over the same bytes.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GIB = float(1 << 30)
+CFG2 = dict(n=8_134_407, k=16, v=100, seed=2)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse(argv=None):
+    p = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--cpu-sample-mb", type=int, default=256,
+                   help="bytes of the same table the CPU baseline decodes (0 = skip)")
+    p.add_argument("--no-encode", action="store_true", help="skip the config-3 encode leg")
+    return p.parse_args(argv)
+
+
+def dist_env():
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def max_over_ranks(value, world, device=None):
+    """Max of a float across ranks (identity when world == 1)."""
+    if world == 1:
+        return value
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(world, device=None):
+    if world > 1:
+        import torch.distributed as dist
+        if device is not None and device.type == "cuda":
+            dist.barrier(device_ids=[device.index])
+        else:
+            dist.barrier()
+
+
+def load_traffic(kernel):
+    """HBM bytes per launch from the committed PMC summary, if collected."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path, encoding="utf-8") as f:
+            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def time_async(torch, fn, steps, warmup, world, device):
+    """Run fn() warmup+steps times; returns (wall_s_max_over_ranks, per-launch ms list)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize(device)
+    stream = torch.cuda.current_stream(device)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    barrier(world, device)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for s, e in ev:
+        s.record(stream)
+        fn()
+        e.record(stream)
+    torch.cuda.synchronize(device)
+    barrier(world, device)
+    wall = time.perf_counter() - t0
+    launch_ms = [s.elapsed_time(e) for s, e in ev]
+    return max_over_ranks(wall, world, device), launch_ms
+
+
+def cpu_baseline(sst_dev, n_records, sample_mb):
+    """Oracle (C restatement of src/format.rs:50-77, owned buffers) on 1 core."""
+    if sample_mb <= 0:
+        return None
+    from oracle import oracle
+    rec = 16 + CFG2["k"] + CFG2["v"]
+    nrec = min(n_records, (sample_mb << 20) // rec)
+    host = sst_dev[: nrec * rec].cpu().numpy()
+    n, secs = oracle.bench_decode_owned(host)
+    assert n == nrec, (n, nrec)
+    return {"value": round(host.size / secs / GIB, 4), "unit": "GiB/s", "cores": 1,
+            "kind": "port",
+            "sample": f"first {nrec} records ({host.size} B) of the same table, "
+                      f"hgo_bench_decode_owned, {secs:.2f} s"}
+
+
+def main(argv=None):
+    args = parse(argv)
+    rank, world, local = dist_env()
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+
+    from horreum_amd import synth
+    from horreum_amd.engine import Engine
+
+    eng = Engine(local)
+    n, k, v = CFG2["n"], CFG2["k"], CFG2["v"]
+    sst = synth.fixed_sst(n, k, v, seed=CFG2["seed"] + 1000 * rank, device=device)
+    L = sst.numel()
+    eng.reserve(L, 0)
+    spans = eng.empty(n * 16)
+    res = eng.empty(64)
+
+    def step():
+        eng.decode_dev_async(sst, L, spans, n, res)
+
+    wall, launch_ms = time_async(torch, step, args.steps, args.warmup, world, device)
+
+    # correctness of what was timed (outside the timed region)
+    r = res[:24].cpu().numpy()
+    nrec = int(r[:8].view("<u8")[0])
+    kind = int(r[8:12].view("<i4")[0])
+    sp = spans[: n * 16].view(torch.int64).view(n, 2)
+    idx = torch.arange(n, device=device, dtype=torch.int64)
+    ok = (nrec == n and kind == 0 and torch.equal(sp[:, 0], idx * (16 + k + v))
+          and bool((sp[:, 1] == (k | (v << 32))).all()))
+
+    ms_step = wall / args.steps * 1e3
+    value = world * L / (wall / args.steps) / GIB
+    mean_launch_ms = sum(launch_ms) / len(launch_ms)
+    alg_bytes = L + 16 * n
+    achieved = alg_bytes / (mean_launch_ms * 1e-3) / 1e9
+    traffic = load_traffic("decode_kernel")
+
+    extra = {}
+    if not args.no_encode:
+        extra["encode_cfg3"] = encode_leg(torch, eng, device, args, world, rank)
+
+    cpu = cpu_baseline(sst, n, args.cpu_sample_mb) if (rank == 0 and world == 1) else None
+    if rank == 0:
+        line = {
+            "metric": "GiB/s SSTable bytes encoded+decoded, device-resident, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (device Philox, seed 2 + 1000*rank)",
+            "config": {"workload": "cfg2 single-SSTable decode (BASELINE configs[1])",
+                       "records_per_gpu": n, "sst_bytes_per_gpu": L, "key_bytes": k,
+                       "value_bytes": v, "decode_chunk": 16384,
+                       "parallelism": f"table-per-gpu x{world}, no collectives"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "kernel": "decode_kernel (+1 MB status memset in the same launch window)",
+                         "alg_bytes_per_launch": alg_bytes,
+                         "mean_launch_ms": round(mean_launch_ms, 5)},
+            "cpu_baseline": cpu,
+            "parity": {"spans_checked": bool(ok), "n_records": nrec, "kind": kind},
+            "extra": extra,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return 0 if ok else 1
+
+
+def encode_leg(torch, eng, device, args, world, rank):
+    """BASELINE config 3: 10 M pairs (32 B / 256 B) -> 3.04 GB of SSTable bytes."""
+    from horreum_amd import synth
+    n, k, v = 10_000_000, 32, 256
+    arena, pairs = synth.fixed_arena(n, k, v, seed=3 + 1000 * rank, device=device)
+    total = n * (16 + k + v)
+    out = eng.empty(total)
+    res = eng.empty(64)
+    eng.reserve(0, n)
+
+    def step():
+        eng.encode_dev_async(arena, pairs, n, out, total, None, 0, None, res)
+
+    steps = max(1, args.steps // 2)
+    wall, launch_ms = time_async(torch, step, steps, max(1, args.warmup // 2), world, device)
+    r = res[:16].cpu().numpy()
+    out_len = int(r[:8].view("<u8")[0])
+    rr = out.view(n, 16 + k + v)
+    ok = out_len == total and torch.equal(rr[:, 16:], arena.view(n, k + v))
+    mean_ms = sum(launch_ms) / len(launch_ms)
+    alg = n * (k + v) + 24 * n + total  # read payload + descriptors, write table
+    del arena, pairs, out
+    torch.cuda.empty_cache()
+    return {"value": round(world * total / (wall / steps) / GIB, 3), "unit": "GiB/s",
+            "ms_per_step": round(wall / steps * 1e3, 4), "records": n, "out_bytes": total,
+            "roofline_frac": round(alg / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "achieved_GBs": round(alg / (mean_ms * 1e-3) / 1e9, 2), "parity_ok": bool(ok)}
+
+
+if __name__ == "__main__":
+    sys.exit(main())

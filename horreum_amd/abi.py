@@ -1,0 +1,122 @@
+"""ctypes binding of include/horreum_gpu.h (libhorreum_gpu.so).
+
+Loading is strict: there is no CPU fallback anywhere in the product path.  If
+the shared library is missing or cannot be loaded, importing the engine raises
+HorreumGpuError with the build command.
+"""
+import ctypes
+import enum
+import os
+import re
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libhorreum_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "horreum_gpu.h")
+
+
+class HorreumGpuError(RuntimeError):
+    """A C-ABI call failed (status code + message)."""
+
+    def __init__(self, status, msg=""):
+        self.status = int(status)
+        super().__init__(f"{msg}: {status_string(self.status)} ({self.status})" if msg
+                         else f"{status_string(self.status)} ({self.status})")
+
+
+class Status(enum.IntEnum):
+    OK = 0
+    TRUNCATED_HEADER = 1
+    TRUNCATED_BODY = 2
+    LEN_OVERFLOW = 3
+    SPAN_RANGE = 4
+    CAPACITY = 5
+    INVALID_ARG = -1
+    HIP = -2
+    TOO_LARGE = -3
+    INTERNAL = -4
+    EMPTY_MERGE = -5
+
+
+# ---- struct layouts (must match include/horreum_gpu.h) -------------------------
+SPAN_DTYPE = np.dtype([("off", "<u8"), ("klen", "<u4"), ("vlen", "<u4")])
+PAIR_DTYPE = np.dtype([("key_off", "<u8"), ("val_off", "<u8"), ("klen", "<u4"), ("vlen", "<u4")])
+BLOCK_DTYPE = np.dtype([("first_rec", "<u8"), ("position", "<u8"), ("length", "<u8")])
+DECODE_RESULT_DTYPE = np.dtype([("n_records", "<u8"), ("kind", "<i4"), ("reserved", "<u4"),
+                                ("err_offset", "<u8")])
+ENCODE_RESULT_DTYPE = np.dtype([("out_len", "<u8"), ("kind", "<i4"), ("reserved", "<u4")])
+
+
+class HgErr(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int32), ("reserved", ctypes.c_uint32),
+                ("offset", ctypes.c_uint64)]
+
+
+def header_exports(path=HEADER_PATH):
+    """Function names declared in include/horreum_gpu.h."""
+    text = open(path, encoding="utf-8").read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hg_[a-z_0-9]+)\s*\(", text)))
+
+
+_u8p = ctypes.c_void_p
+_vp = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+_PROTOS = {
+    "hg_abi_version": (ctypes.c_int, []),
+    "hg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "hg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    "hg_ctx_destroy": (ctypes.c_int, [_vp]),
+    "hg_ctx_set_stream": (ctypes.c_int, [_vp, _vp]),
+    "hg_ctx_stream": (_vp, [_vp]),
+    "hg_ctx_synchronize": (ctypes.c_int, [_vp]),
+    "hg_ctx_reserve": (ctypes.c_int, [_vp, _u64, _u64]),
+    "hg_decode_dev": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, ctypes.POINTER(_u64),
+                                     ctypes.POINTER(HgErr)]),
+    "hg_decode_dev_async": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, _vp]),
+    "hg_decode_host": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, ctypes.POINTER(_u64),
+                                      ctypes.POINTER(HgErr)]),
+    "hg_encode_dev": (ctypes.c_int, [_vp, _u8p, _vp, _u64, _u8p, _u64, _vp, _u32, _vp,
+                                     ctypes.POINTER(_u64)]),
+    "hg_encode_dev_async": (ctypes.c_int, [_vp, _u8p, _vp, _u64, _u8p, _u64, _vp, _u32, _vp,
+                                           _vp]),
+    "hg_encode_host": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, _u8p, _u64, _vp, _u32, _vp,
+                                      ctypes.POINTER(_u64)]),
+    "hg_block_count": (_u64, [_u64, _u32]),
+}
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    """Load libhorreum_gpu.so once; raise HorreumGpuError if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HorreumGpuError(Status.HIP, f"{path} not built (run: make -C horreum_amd/csrc)")
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as e:  # pragma: no cover - environment specific
+        raise HorreumGpuError(Status.HIP, f"cannot load {path}: {e}") from e
+    for name, (res, args) in _PROTOS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def status_string(status):
+    try:
+        return load_library().hg_status_string(int(status)).decode()
+    except HorreumGpuError:
+        return Status(status).name if status in Status._value2member_map_ else "unknown"
+
+
+def check(status, what=""):
+    if status != 0:
+        raise HorreumGpuError(status, what)
+    return status

@@ -1,0 +1,99 @@
+// hg_device.hpp — device helpers shared by the decode and encode kernels
+// (gfx950 / CDNA4: 64-lane waves, 160 KiB LDS per CU).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/horreum_gpu.h"
+
+namespace hgk {
+
+constexpr uint64_t V40 = (1ull << 40) - 1;  // 40-bit positions/counts in status words
+
+// Status word: [63:62] flag | [61:40] aux (22 bits) | [39:0] value (40 bits).
+// Every word a look-back reads is written whole by ONE 8-byte agent-scope
+// atomic store (a granule, cdna_hip_programming.md G16 R2), so a reader sees
+// either the old or the new word, never a torn one.
+__device__ __forceinline__ unsigned long long pack_status(uint32_t flag, uint32_t aux,
+                                                          uint64_t val) {
+    return ((unsigned long long)flag << 62) |
+           ((unsigned long long)(aux & 0x3FFFFFu) << 40) | (val & V40);
+}
+__device__ __forceinline__ uint32_t st_flag(unsigned long long w) { return (uint32_t)(w >> 62); }
+__device__ __forceinline__ uint32_t st_aux(unsigned long long w) {
+    return (uint32_t)(w >> 40) & 0x3FFFFFu;
+}
+__device__ __forceinline__ uint64_t st_val(unsigned long long w) { return w & V40; }
+
+__device__ __forceinline__ unsigned long long ld_agent(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Per-byte zero mask of 16 bytes held as 4 dwords: bit i set <=> byte i == 0.
+__device__ __forceinline__ uint32_t zmask4(uint32_t x) {
+    uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // byte MSB set <=> byte != 0
+    uint32_t z = ~t & 0x80808080u;
+    return ((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u);
+}
+__device__ __forceinline__ uint32_t zmask16(uint4 v) {
+    return zmask4(v.x) | (zmask4(v.y) << 4) | (zmask4(v.z) << 8) | (zmask4(v.w) << 12);
+}
+
+// Unaligned little-endian u64 pair (klen, vlen) at byte offset p of an
+// 8-byte-aligned LDS buffer; reads 24 bytes from p & ~7.
+__device__ __forceinline__ void lds_header(const uint8_t* lds, uint32_t p, uint64_t& k,
+                                           uint64_t& v) {
+    const uint64_t* w = reinterpret_cast<const uint64_t*>(lds + (p & ~7u));
+    uint64_t w0 = w[0], w1 = w[1], w2 = w[2];
+    uint32_t s = (p & 7u) * 8u;
+    if (s) {
+        k = (w0 >> s) | (w1 << (64u - s));
+        v = (w1 >> s) | (w2 << (64u - s));
+    } else {
+        k = w0;
+        v = w1;
+    }
+}
+
+// Wave-level inclusive scan (64 lanes).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_sum(T x) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+    return x;
+}
+
+// Block-wide exclusive scan over NW waves; s_tmp needs NW words.
+template <uint32_t NW>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_tmp,
+                                                    uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint32_t inc = wave_incl_scan(v);
+    if (lane == 63) s_tmp[wid] = inc;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < NW; ++w) {
+        uint32_t t = s_tmp[w];
+        pre += (w < wid) ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + inc - v;
+}
+
+}  // namespace hgk

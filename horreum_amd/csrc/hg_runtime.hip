@@ -1,0 +1,380 @@
+// hg_runtime.hip — host runtime behind include/horreum_gpu.h: contexts
+// (device + stream + workspace), argument checking, sync/async entry points
+// and the pinned host staging pipeline.  Kernels: hg_decode.hip,
+// hg_encode.hip.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <algorithm>
+#include <new>
+
+#include "../../include/horreum_gpu.h"
+
+extern "C" int hgk_decode_launch(const uint8_t*, uint64_t, hg_span*, uint64_t, hg_decode_result*,
+                                 unsigned long long*, hipStream_t);
+extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t);
+extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
+                                 uint64_t*, uint32_t, hg_block*, hg_encode_result*,
+                                 unsigned long long*, hipStream_t);
+extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t);
+
+namespace {
+
+constexpr uint64_t kMaxLen = 1ull << 40;  // 40-bit positions in decode statuses
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace
+
+struct hg_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    DevBuf ws;        // decode statuses / encode tile statuses
+    DevBuf recoff;    // encode record offsets when blocks are wanted w/o rec_off
+    DevBuf results;   // hg_decode_result + hg_encode_result
+    PinBuf hres;      // pinned mirror of `results`
+    // host-path staging (device side)
+    DevBuf d_in, d_out, d_aux;
+    PinBuf h_stage[2];
+};
+
+namespace {
+
+int set_dev(hg_ctx* c) { return hipSetDevice(c->device) == hipSuccess ? HG_OK : HG_ERR_HIP; }
+
+// Grow a device buffer; only ever called outside stream-ordered hot loops
+// (hg_ctx_reserve pre-sizes everything the bench touches).
+int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes) return HG_OK;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return HG_ERR_HIP;
+    if (b.p) hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    size_t want = std::max(bytes, (size_t)256);
+    if (hipMalloc(&b.p, want) != hipSuccess) return HG_ERR_HIP;
+    b.bytes = want;
+    return HG_OK;
+}
+
+int ensure_pin(PinBuf& b, size_t bytes) {
+    if (b.bytes >= bytes) return HG_OK;
+    if (b.p) hipHostFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) return HG_ERR_HIP;
+    b.bytes = bytes;
+    return HG_OK;
+}
+
+hg_decode_result* dres(hg_ctx* c) { return reinterpret_cast<hg_decode_result*>(c->results.p); }
+hg_encode_result* eres(hg_ctx* c) {
+    return reinterpret_cast<hg_encode_result*>(reinterpret_cast<char*>(c->results.p) + 64);
+}
+
+}  // namespace
+
+extern "C" {
+
+int hg_abi_version(void) { return HG_ABI_VERSION; }
+
+const char* hg_status_string(int s) {
+    switch (s) {
+        case HG_OK: return "ok";
+        case HG_ERR_TRUNCATED_HEADER: return "truncated record header (UnexpectedEof)";
+        case HG_ERR_TRUNCATED_BODY: return "truncated record body (UnexpectedEof)";
+        case HG_ERR_LEN_OVERFLOW: return "key_len + value_len overflows u64";
+        case HG_ERR_SPAN_RANGE: return "key or value length >= 2^32 (span limit)";
+        case HG_ERR_CAPACITY: return "output buffer too small";
+        case HG_ERR_INVALID_ARG: return "invalid argument";
+        case HG_ERR_HIP: return "HIP runtime error";
+        case HG_ERR_TOO_LARGE: return "input too large (>= 2^40 bytes)";
+        case HG_ERR_INTERNAL: return "internal error (device spin timeout)";
+        case HG_ERR_EMPTY_MERGE: return "merge of zero records";
+        default: return "unknown status";
+    }
+}
+
+int hg_ctx_create(int device, hg_ctx** out) {
+    if (!out) return HG_ERR_INVALID_ARG;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev)
+        return HG_ERR_INVALID_ARG;
+    hg_ctx* c = new (std::nothrow) hg_ctx();
+    if (!c) return HG_ERR_INTERNAL;
+    c->device = device;
+    if (set_dev(c) != HG_OK || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return HG_ERR_HIP;
+    }
+    c->stream = c->own;
+    if (ensure(c, c->results, 256) != HG_OK || ensure_pin(c->hres, 256) != HG_OK) {
+        hg_ctx_destroy(c);
+        return HG_ERR_HIP;
+    }
+    *out = c;
+    return HG_OK;
+}
+
+int hg_ctx_destroy(hg_ctx* c) {
+    if (!c) return HG_ERR_INVALID_ARG;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux})
+        if (b->p) hipFree(b->p);
+    for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1]})
+        if (b->p) hipHostFree(b->p);
+    if (c->own) hipStreamDestroy(c->own);
+    delete c;
+    return HG_OK;
+}
+
+int hg_ctx_set_stream(hg_ctx* c, void* s) {
+    if (!c) return HG_ERR_INVALID_ARG;
+    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+    return HG_OK;
+}
+
+void* hg_ctx_stream(hg_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) : nullptr; }
+
+int hg_ctx_synchronize(hg_ctx* c) {
+    if (!c) return HG_ERR_INVALID_ARG;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+int hg_ctx_reserve(hg_ctx* c, uint64_t max_sst_bytes, uint64_t max_pairs) {
+    if (!c) return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    size_t need = std::max(hgk_decode_workspace_bytes(max_sst_bytes),
+                           hgk_encode_workspace_bytes(max_pairs));
+    int r = ensure(c, c->ws, need);
+    if (r == HG_OK && max_pairs) r = ensure(c, c->recoff, max_pairs * sizeof(uint64_t));
+    return r;
+}
+
+uint64_t hg_block_count(uint64_t n, uint32_t stride) {
+    return stride ? (n + stride - 1) / stride : 0;
+}
+
+// ---- decode ------------------------------------------------------------------
+int hg_decode_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
+                        uint64_t cap, hg_decode_result* d_result) {
+    if (!c || !d_result || (len && !d_sst) || (cap && !d_spans)) return HG_ERR_INVALID_ARG;
+    if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (len == 0)  // empty file: zero records (src/format.rs:54 loop never runs)
+        return hipMemsetAsync(d_result, 0, sizeof(hg_decode_result), c->stream) == hipSuccess
+                   ? HG_OK
+                   : HG_ERR_HIP;
+    int r = ensure(c, c->ws, hgk_decode_workspace_bytes(len));
+    if (r != HG_OK) return r;
+    return hgk_decode_launch(d_sst, len, d_spans, cap, d_result,
+                             reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+}
+
+static int finish_decode(const hg_decode_result& res, uint64_t cap, uint64_t* n_out,
+                         hg_err* err) {
+    if (n_out) *n_out = res.n_records;
+    if (err) {
+        err->kind = res.kind;
+        err->reserved = 0;
+        err->offset = res.err_offset;
+    }
+    if (res.kind != HG_OK) return res.kind;
+    return res.n_records > cap ? HG_ERR_CAPACITY : HG_OK;
+}
+
+int hg_decode_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t cap,
+                  uint64_t* n_out, hg_err* err) {
+    int r = hg_decode_dev_async(c, d_sst, len, d_spans, cap, c ? dres(c) : nullptr);
+    if (r != HG_OK) return r;
+    if (hipMemcpyAsync(c->hres.p, dres(c), sizeof(hg_decode_result), hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return HG_ERR_HIP;
+    return finish_decode(*reinterpret_cast<hg_decode_result*>(c->hres.p), cap, n_out, err);
+}
+
+// Host bytes in, host spans out.  The file is pushed through two pinned
+// staging buffers (CPU memcpy of piece i+1 overlaps the DMA of piece i), the
+// decode runs on the device copy, and the spans come back the same way.
+static constexpr size_t kStage = 64ull << 20;
+
+static int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
+        return HG_ERR_HIP;
+    hipEvent_t ev[2];
+    hipEventCreateWithFlags(&ev[0], hipEventDisableTiming);
+    hipEventCreateWithFlags(&ev[1], hipEventDisableTiming);
+    bool used[2] = {false, false};
+    int rc = HG_OK;
+    for (size_t off = 0, i = 0; off < bytes; off += kStage, ++i) {
+        const size_t n = std::min(kStage, bytes - off);
+        const int b = (int)(i & 1);
+        if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
+        memcpy(c->h_stage[b].p, static_cast<const char*>(src) + off, n);
+        if (hipMemcpyAsync(static_cast<char*>(dst) + off, c->h_stage[b].p, n,
+                           hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+            hipEventRecord(ev[b], c->stream) != hipSuccess) {
+            rc = HG_ERR_HIP;
+            break;
+        }
+        used[b] = true;
+    }
+    hipStreamSynchronize(c->stream);
+    hipEventDestroy(ev[0]);
+    hipEventDestroy(ev[1]);
+    return rc;
+}
+
+static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
+        return HG_ERR_HIP;
+    hipEvent_t ev[2];
+    hipEventCreateWithFlags(&ev[0], hipEventDisableTiming);
+    hipEventCreateWithFlags(&ev[1], hipEventDisableTiming);
+    size_t pend_off[2] = {0, 0}, pend_n[2] = {0, 0};
+    bool used[2] = {false, false};
+    int rc = HG_OK;
+    size_t i = 0;
+    for (size_t off = 0; off < bytes; off += kStage, ++i) {
+        const size_t n = std::min(kStage, bytes - off);
+        const int b = (int)(i & 1);
+        if (used[b]) {  // drain the previous use of this buffer
+            if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
+            memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
+        }
+        if (hipMemcpyAsync(c->h_stage[b].p, static_cast<const char*>(src) + off, n,
+                           hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipEventRecord(ev[b], c->stream) != hipSuccess) {
+            rc = HG_ERR_HIP;
+            break;
+        }
+        used[b] = true;
+        pend_off[b] = off;
+        pend_n[b] = n;
+    }
+    for (int k = 0; k < 2 && rc == HG_OK; ++k) {
+        const int b = (int)((i + k) & 1);
+        if (!used[b]) continue;
+        if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
+        memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
+        used[b] = false;
+    }
+    hipStreamSynchronize(c->stream);
+    hipEventDestroy(ev[0]);
+    hipEventDestroy(ev[1]);
+    return rc;
+}
+
+int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spans, uint64_t cap,
+                   uint64_t* n_out, hg_err* err) {
+    if (!c || (len && !h_sst) || (cap && !h_spans)) return HG_ERR_INVALID_ARG;
+    if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    // A file of L bytes holds at most L/16 records.
+    const uint64_t dcap = std::min<uint64_t>(cap, len / 16);
+    int r;
+    if ((r = ensure(c, c->d_in, len ? len : 1)) != HG_OK) return r;
+    if ((r = ensure(c, c->d_out, (dcap ? dcap : 1) * sizeof(hg_span))) != HG_OK) return r;
+    if (len && (r = h2d_pipelined(c, c->d_in.p, h_sst, len)) != HG_OK) return r;
+    uint64_t n = 0;
+    hg_err e{};
+    r = hg_decode_dev(c, static_cast<const uint8_t*>(c->d_in.p), len,
+                      static_cast<hg_span*>(c->d_out.p), dcap, &n, &e);
+    if (r != HG_OK && r != HG_ERR_CAPACITY && e.kind == HG_OK) return r;  // runtime failure
+    const uint64_t ncopy = std::min(n, dcap);
+    if (ncopy && d2h_pipelined(c, h_spans, c->d_out.p, ncopy * sizeof(hg_span)) != HG_OK)
+        return HG_ERR_HIP;
+    if (n_out) *n_out = n;
+    if (err) *err = e;
+    if (e.kind != HG_OK) return e.kind;
+    return n > cap ? HG_ERR_CAPACITY : HG_OK;
+}
+
+// ---- encode ------------------------------------------------------------------
+int hg_encode_dev_async(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                        uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
+                        hg_block* d_blocks, hg_encode_result* d_result) {
+    if (!c || !d_result || (n && !d_pairs) || (cap && !d_out)) return HG_ERR_INVALID_ARG;
+    if (d_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;  // slice::chunks(0) panics
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (n == 0)
+        return hipMemsetAsync(d_result, 0, sizeof(hg_encode_result), c->stream) == hipSuccess
+                   ? HG_OK
+                   : HG_ERR_HIP;
+    int r = ensure(c, c->ws, hgk_encode_workspace_bytes(n));
+    if (r != HG_OK) return r;
+    if (d_blocks && !d_rec_off) {
+        if ((r = ensure(c, c->recoff, n * sizeof(uint64_t))) != HG_OK) return r;
+        d_rec_off = static_cast<uint64_t*>(c->recoff.p);
+    }
+    return hgk_encode_launch(d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride, d_blocks,
+                             d_result, reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+}
+
+int hg_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                  uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
+                  hg_block* d_blocks, uint64_t* out_len) {
+    int r = hg_encode_dev_async(c, d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride,
+                                d_blocks, c ? eres(c) : nullptr);
+    if (r != HG_OK) return r;
+    if (hipMemcpyAsync(c->hres.p, eres(c), sizeof(hg_encode_result), hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return HG_ERR_HIP;
+    const hg_encode_result res = *reinterpret_cast<hg_encode_result*>(c->hres.p);
+    if (out_len) *out_len = res.out_len;
+    return res.kind;
+}
+
+int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const hg_pair* h_pairs,
+                   uint64_t n, uint8_t* h_out, uint64_t cap, uint64_t* h_rec_off,
+                   uint32_t block_stride, hg_block* h_blocks, uint64_t* out_len) {
+    if (!c || (n && !h_pairs) || (arena_len && !h_arena) || (cap && !h_out))
+        return HG_ERR_INVALID_ARG;
+    if (h_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) total += 16ull + h_pairs[i].klen + h_pairs[i].vlen;
+    if (out_len) *out_len = total;
+    if (total > cap) return HG_ERR_CAPACITY;
+    const uint64_t nb = h_blocks ? hg_block_count(n, block_stride) : 0;
+    // d_in: arena ++ pairs; d_out: encoded bytes; d_aux: rec_off ++ blocks
+    const size_t pairs_at = (arena_len + 63) & ~(size_t)63;
+    const size_t in_bytes = pairs_at + n * sizeof(hg_pair);
+    const size_t blocks_at = n * sizeof(uint64_t);
+    int r;
+    if ((r = ensure(c, c->d_in, in_bytes ? in_bytes : 1)) != HG_OK) return r;
+    if ((r = ensure(c, c->d_out, total ? total : 1)) != HG_OK) return r;
+    if ((r = ensure(c, c->d_aux, blocks_at + nb * sizeof(hg_block) + 64)) != HG_OK) return r;
+    char* din = static_cast<char*>(c->d_in.p);
+    if (arena_len && (r = h2d_pipelined(c, din, h_arena, arena_len)) != HG_OK) return r;
+    if (n && (r = h2d_pipelined(c, din + pairs_at, h_pairs, n * sizeof(hg_pair))) != HG_OK)
+        return r;
+    uint64_t* d_rec = static_cast<uint64_t*>(c->d_aux.p);
+    hg_block* d_blk = h_blocks ? reinterpret_cast<hg_block*>(static_cast<char*>(c->d_aux.p) + blocks_at)
+                               : nullptr;
+    uint64_t got = 0;
+    r = hg_encode_dev(c, reinterpret_cast<const uint8_t*>(din),
+                      reinterpret_cast<const hg_pair*>(din + pairs_at), n,
+                      static_cast<uint8_t*>(c->d_out.p), total, d_rec, block_stride, d_blk, &got);
+    if (r != HG_OK) return r;
+    if (total && (r = d2h_pipelined(c, h_out, c->d_out.p, total)) != HG_OK) return r;
+    if (h_rec_off && n && (r = d2h_pipelined(c, h_rec_off, d_rec, n * sizeof(uint64_t))) != HG_OK)
+        return r;
+    if (h_blocks && nb && (r = d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block))) != HG_OK)
+        return r;
+    return HG_OK;
+}
+
+}  // extern "C"

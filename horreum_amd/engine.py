@@ -1,0 +1,170 @@
+"""Device engine: one HIP context (GPU + stream) and its buffers.
+
+PyTorch is used only as plumbing: HBM allocations (`torch.empty(..., device=
+"cuda")`) and the stream the C ABI launches on (torch's current stream by
+default, so torch/HIP events time exactly the launched kernels).  All compute
+happens in libhorreum_gpu.so; there is no CPU fallback.
+"""
+import ctypes
+from collections import namedtuple
+
+import numpy as np
+
+from .abi import (BLOCK_DTYPE, PAIR_DTYPE, SPAN_DTYPE, HgErr, HorreumGpuError, Status, check,
+                  load_library)
+
+DecodeOut = namedtuple("DecodeOut", "spans n kind offset")
+EncodeOut = namedtuple("EncodeOut", "data rec_off blocks out_len")
+
+
+def _torch():
+    import torch  # noqa: WPS433 (deferred: importing torch is slow)
+    return torch
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class Engine:
+    """A context on `device`.  Not thread-safe; use one Engine per thread."""
+
+    def __init__(self, device=0, use_torch_stream=True):
+        self.lib = load_library()
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise HorreumGpuError(Status.HIP, "no HIP device visible")
+        self.device = torch.device("cuda", device)
+        ctx = ctypes.c_void_p()
+        check(self.lib.hg_ctx_create(device, ctypes.byref(ctx)), "hg_ctx_create")
+        self.ctx = ctx
+        if use_torch_stream:
+            self.set_stream(torch.cuda.current_stream(self.device))
+
+    # ---- context --------------------------------------------------------------
+    def set_stream(self, stream):
+        handle = stream.cuda_stream if stream is not None else 0
+        check(self.lib.hg_ctx_set_stream(self.ctx, ctypes.c_void_p(handle)), "hg_ctx_set_stream")
+
+    def reserve(self, max_sst_bytes=0, max_pairs=0):
+        check(self.lib.hg_ctx_reserve(self.ctx, max_sst_bytes, max_pairs), "hg_ctx_reserve")
+
+    def synchronize(self):
+        check(self.lib.hg_ctx_synchronize(self.ctx), "hg_ctx_synchronize")
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.hg_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- device buffers ---------------------------------------------------------
+    def empty(self, nbytes):
+        torch = _torch()
+        return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=self.device)
+
+    def to_device(self, array):
+        torch = _torch()
+        a = np.ascontiguousarray(np.frombuffer(memoryview(array).cast("B"), dtype=np.uint8))
+        return torch.from_numpy(a.copy()).to(self.device) if a.size else self.empty(1)
+
+    # ---- decode -------------------------------------------------------------------
+    def decode_dev(self, sst, length=None, spans=None, cap=None):
+        """Decode `length` bytes of the uint8 device tensor `sst`.
+
+        Returns DecodeOut(spans=device uint8 tensor [cap*16], n, kind, offset);
+        raises HorreumGpuError on runtime failures only (format errors are
+        returned in `kind`, as the ABI does)."""
+        length = sst.numel() if length is None else int(length)
+        if cap is None:
+            cap = length // 16 if spans is None else spans.numel() // SPAN_DTYPE.itemsize
+        if spans is None:
+            spans = self.empty(cap * SPAN_DTYPE.itemsize)
+        n = ctypes.c_uint64()
+        err = HgErr()
+        rc = self.lib.hg_decode_dev(self.ctx, _ptr(sst), length, _ptr(spans), cap,
+                                    ctypes.byref(n), ctypes.byref(err))
+        if rc < 0:
+            raise HorreumGpuError(rc, "hg_decode_dev")
+        return DecodeOut(spans, n.value, err.kind, err.offset)
+
+    def decode_dev_async(self, sst, length, spans, cap, result):
+        check(self.lib.hg_decode_dev_async(self.ctx, _ptr(sst), int(length), _ptr(spans),
+                                           int(cap), _ptr(result)), "hg_decode_dev_async")
+
+    def decode_host(self, data, cap=None):
+        """Host bytes in, numpy SPAN_DTYPE array out (through pinned staging)."""
+        buf = np.ascontiguousarray(np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8))
+        cap = buf.size // 16 if cap is None else int(cap)
+        spans = np.zeros(max(cap, 1), dtype=SPAN_DTYPE)
+        n = ctypes.c_uint64()
+        err = HgErr()
+        rc = self.lib.hg_decode_host(self.ctx, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                     spans.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(n),
+                                     ctypes.byref(err))
+        if rc < 0:
+            raise HorreumGpuError(rc, "hg_decode_host")
+        return DecodeOut(spans[: min(n.value, cap)], n.value, err.kind, err.offset)
+
+    @staticmethod
+    def spans_to_numpy(spans, n):
+        return spans[: n * SPAN_DTYPE.itemsize].cpu().numpy().view(SPAN_DTYPE)
+
+    # ---- encode -------------------------------------------------------------------
+    def encode_dev(self, arena, pairs, n, out=None, cap=None, rec_off=None, block_stride=0,
+                   blocks=None):
+        """Encode `n` hg_pair records (uint8 device tensor `pairs`) whose bytes
+        live in device tensor `arena`.  Returns the encoded length."""
+        if out is None:
+            raise ValueError("out buffer required")
+        cap = out.numel() if cap is None else int(cap)
+        out_len = ctypes.c_uint64()
+        rc = self.lib.hg_encode_dev(self.ctx, _ptr(arena), _ptr(pairs), int(n), _ptr(out), cap,
+                                    _ptr(rec_off), int(block_stride), _ptr(blocks),
+                                    ctypes.byref(out_len))
+        if rc not in (Status.OK, Status.CAPACITY):
+            raise HorreumGpuError(rc, "hg_encode_dev")
+        return rc, out_len.value
+
+    def encode_dev_async(self, arena, pairs, n, out, cap, rec_off, block_stride, blocks, result):
+        check(self.lib.hg_encode_dev_async(self.ctx, _ptr(arena), _ptr(pairs), int(n), _ptr(out),
+                                           int(cap), _ptr(rec_off), int(block_stride),
+                                           _ptr(blocks), _ptr(result)), "hg_encode_dev_async")
+
+    def encode_host(self, arena, pairs, block_stride=0, want_rec_off=False):
+        """numpy arena (uint8) + PAIR_DTYPE records -> EncodeOut (numpy)."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8)
+        pairs = np.ascontiguousarray(pairs, dtype=PAIR_DTYPE)
+        n = pairs.size
+        total = int((16 + pairs["klen"].astype(np.uint64) + pairs["vlen"].astype(np.uint64)).sum())
+        out = np.empty(max(total, 1), dtype=np.uint8)
+        rec_off = np.empty(max(n, 1), dtype=np.uint64) if want_rec_off else None
+        nb = int(self.lib.hg_block_count(n, block_stride)) if block_stride else 0
+        blocks = np.empty(max(nb, 1), dtype=BLOCK_DTYPE) if block_stride else None
+        out_len = ctypes.c_uint64()
+
+        def vp(a):
+            return a.ctypes.data_as(ctypes.c_void_p) if a is not None else ctypes.c_void_p(0)
+
+        rc = self.lib.hg_encode_host(self.ctx, vp(arena), arena.size, vp(pairs), n, vp(out),
+                                     total, vp(rec_off), int(block_stride), vp(blocks),
+                                     ctypes.byref(out_len))
+        check(rc, "hg_encode_host")
+        return EncodeOut(out[:total], rec_off[:n] if rec_off is not None else None,
+                         blocks[:nb] if blocks is not None else None, out_len.value)
+
+
+_default = None
+
+
+def default_engine():
+    """Process-wide engine on cuda:0 (created on first use)."""
+    global _default
+    if _default is None:
+        _default = Engine(0)
+    return _default

@@ -1,0 +1,74 @@
+"""Synthetic, seeded SSTable workloads built directly in HBM (bench + tests).
+
+BASELINE.json config 2: n records of 16-byte big-endian counter keys (sorted,
+unique) and 100-byte uniform random values; config 3: 32 B / 256 B pairs in a
+contiguous key||value arena with hg_pair descriptors.  Random bytes come from
+torch's device generator (Philox) seeded per config; nothing is read from
+disk or the network.
+"""
+import numpy as np
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def be_counter_keys(n, k, device):
+    """[n, k] uint8: big-endian counters 0..n-1."""
+    torch = _torch()
+    idx = torch.arange(n, device=device, dtype=torch.int64)
+    cols = []
+    for b in range(k - 1, -1, -1):
+        cols.append(((idx >> (8 * b)) & 0xFF).to(torch.uint8) if b < 8
+                    else torch.zeros(n, dtype=torch.uint8, device=device))
+    return torch.stack(cols, dim=1)
+
+
+def le64_rows(vals, device):
+    """[n] int64 -> [n, 8] uint8 little-endian."""
+    torch = _torch()
+    return torch.stack([((vals >> (8 * b)) & 0xFF).to(torch.uint8) for b in range(8)], dim=1)
+
+
+def fixed_sst(n, k, v, seed, device):
+    """Encoded SSTable bytes of n fixed-size records, built on the device."""
+    torch = _torch()
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    rec = torch.empty((n, 16 + k + v), dtype=torch.uint8, device=device)
+    rec[:, 0:8] = le64_rows(torch.full((1,), k, dtype=torch.int64, device=device), device)
+    rec[:, 8:16] = le64_rows(torch.full((1,), v, dtype=torch.int64, device=device), device)
+    rec[:, 16:16 + k] = be_counter_keys(n, k, device)
+    rec[:, 16 + k:] = torch.randint(0, 256, (n, v), dtype=torch.uint8, device=device, generator=g)
+    return rec.view(-1)
+
+
+def fixed_arena(n, k, v, seed, device):
+    """(arena [n*(k+v)] uint8, pairs [n*24] uint8 as hg_pair) on the device."""
+    torch = _torch()
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    arena = torch.empty((n, k + v), dtype=torch.uint8, device=device)
+    arena[:, :k] = be_counter_keys(n, k, device)
+    arena[:, k:] = torch.randint(0, 256, (n, v), dtype=torch.uint8, device=device, generator=g)
+    idx = torch.arange(n, device=device, dtype=torch.int64)
+    pairs = torch.empty((n, 3), dtype=torch.int64, device=device)
+    pairs[:, 0] = idx * (k + v)
+    pairs[:, 1] = idx * (k + v) + k
+    pairs[:, 2] = k | (v << 32)
+    return arena.view(-1), pairs.view(torch.uint8).view(-1)
+
+
+def host_fixed_sst(n, k, v, seed):
+    """numpy twin of fixed_sst for CPU baselines (same layout, numpy RNG)."""
+    rng = np.random.default_rng(seed)
+    rec = np.empty((n, 16 + k + v), dtype=np.uint8)
+    rec[:, 0:8] = np.frombuffer(int(k).to_bytes(8, "little"), np.uint8)
+    rec[:, 8:16] = np.frombuffer(int(v).to_bytes(8, "little"), np.uint8)
+    idx = np.arange(n, dtype=np.uint64)
+    for b in range(k):
+        rec[:, 16 + k - 1 - b] = ((idx >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8) \
+            if b < 8 else 0
+    rec[:, 16 + k:] = rng.integers(0, 256, size=(n, v), dtype=np.uint8)
+    return rec.reshape(-1)

@@ -1,0 +1,185 @@
+/*
+ * horreum_gpu.h — C ABI of the MI355X SSTable record codec.
+ *
+ * This is the drop-in boundary for horreum's record codec and SSTable
+ * writer/reader (reference: ikanago/horreum, Rust).  The reference has no FFI
+ * of its own; each entry point below names the Rust function it replaces
+ * (file:line in the reference tree).  A Rust caller binds these with plain
+ * `extern "C"` declarations.
+ *
+ * On-disk record format (src/format.rs:23-37):
+ *     [u64 LE key_len][u64 LE value_len][key bytes][value bytes]
+ * value_len == 0 means "no value" (a deletion / tombstone): `Some(b"")` and
+ * `None` encode identically and decode as `None` (src/format.rs:25-28, 71-75).
+ *
+ * Conventions
+ *   - Every buffer is caller-owned.  The library never allocates output.
+ *   - `_dev` entry points take device (HBM) pointers; `_host` entry points take
+ *     host pointers and stage through pinned memory.
+ *   - `_async` entry points enqueue work on the context's stream and return
+ *     immediately; their result struct lives in device memory and is valid
+ *     after the stream is synchronised.
+ *   - Return value: HG_OK (0) or a status code.  Data-format errors are
+ *     returned (never aborted on), unlike the reference, which unwrap()s them
+ *     (src/sstable/storage.rs:64-66, src/sstable/table.rs:62-64).
+ *   - One context = one GPU + one HIP stream.  Distinct contexts may be used
+ *     from distinct threads; one context must not be used concurrently.
+ */
+#ifndef HORREUM_GPU_H
+#define HORREUM_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HG_ABI_VERSION 1
+
+/* Status codes: return values, and the `kind` field of hg_err / results. */
+enum hg_status {
+    HG_OK = 0,
+    /* Fewer than 16 bytes remain at a record start: the reference's
+     * read_exact of the 16-byte length header fails (src/format.rs:64-65). */
+    HG_ERR_TRUNCATED_HEADER = 1,
+    /* Header read, but offset+16+key_len+value_len runs past the end: the
+     * reference's read_exact of the body fails (src/format.rs:68-69). */
+    HG_ERR_TRUNCATED_BODY = 2,
+    /* key_len + value_len overflows u64 (src/format.rs:68; the reference
+     * panics or wraps here). */
+    HG_ERR_LEN_OVERFLOW = 3,
+    /* A well-formed record whose key_len or value_len is >= 2^32 does not fit
+     * the 16-byte hg_span; engine limit, documented in DESIGN.md. */
+    HG_ERR_SPAN_RANGE = 4,
+    /* Output buffer too small.  The required count/size is still reported. */
+    HG_ERR_CAPACITY = 5,
+    HG_ERR_INVALID_ARG = -1,
+    HG_ERR_HIP = -2,
+    HG_ERR_TOO_LARGE = -3,  /* input length >= 2^40 bytes (engine limit) */
+    HG_ERR_INTERNAL = -4,   /* e.g. a bounded device spin timed out */
+    HG_ERR_EMPTY_MERGE = -5 /* merge of zero records; the reference panics (src/sstable/manager.rs:213) */
+};
+
+/* One decoded record: key at off+16, value at off+16+klen.
+ * vlen == 0 <=> tombstone (value None).  16 bytes, 8-byte aligned. */
+typedef struct hg_span {
+    uint64_t off;
+    uint32_t klen;
+    uint32_t vlen;
+} hg_span;
+
+/* One record to encode, as offsets into a caller arena.  vlen == 0 encodes a
+ * tombstone (InternalPair{value: None}, src/format.rs:6-11). */
+typedef struct hg_pair {
+    uint64_t key_off;
+    uint64_t val_off;
+    uint32_t klen;
+    uint32_t vlen;
+} hg_pair;
+
+/* One block of the in-memory SSTable index (src/sstable/index.rs:6-15):
+ * first key = key of record `first_rec`; bytes [position, position+length). */
+typedef struct hg_block {
+    uint64_t first_rec;
+    uint64_t position;
+    uint64_t length;
+} hg_block;
+
+/* Error detail: kind (enum hg_status) and the byte offset of the failing
+ * record start (the position of the reference's cursor when it failed). */
+typedef struct hg_err {
+    int32_t kind;
+    uint32_t reserved;
+    uint64_t offset;
+} hg_err;
+
+/* Device-resident result of an async decode. */
+typedef struct hg_decode_result {
+    uint64_t n_records;  /* records decoded (before the error, if any) */
+    int32_t kind;        /* enum hg_status */
+    uint32_t reserved;
+    uint64_t err_offset; /* failing record start when kind != HG_OK */
+} hg_decode_result;
+
+/* Device-resident result of an async encode. */
+typedef struct hg_encode_result {
+    uint64_t out_len; /* total encoded bytes, sum(16 + klen + vlen) */
+    int32_t kind;     /* HG_OK or HG_ERR_CAPACITY */
+    uint32_t reserved;
+} hg_encode_result;
+
+typedef struct hg_ctx hg_ctx;
+
+/* ---- library / context ---------------------------------------------- */
+int hg_abi_version(void);
+const char* hg_status_string(int status);
+
+/* Create a context bound to HIP device `device` with its own stream. */
+int hg_ctx_create(int device, hg_ctx** out);
+int hg_ctx_destroy(hg_ctx* ctx);
+/* Use a caller stream (a hipStream_t); NULL restores the context's own. */
+int hg_ctx_set_stream(hg_ctx* ctx, void* hip_stream);
+void* hg_ctx_stream(hg_ctx* ctx);
+int hg_ctx_synchronize(hg_ctx* ctx);
+/* Pre-size the device workspace so later calls never allocate
+ * (keeps them graph-capturable and out of timed regions). */
+int hg_ctx_reserve(hg_ctx* ctx, uint64_t max_sst_bytes, uint64_t max_pairs);
+
+/* ---- decode ----------------------------------------------------------
+ * Replaces InternalPair::deserialize_from_bytes (src/format.rs:50-59) and
+ * deserialize_inner (src/format.rs:63-77), i.e. the decode behind
+ * PersistedFile::read_all (src/sstable/storage.rs:60-67), SSTable::open /
+ * get / get_all (src/sstable/table.rs:33-75) and compaction's table reads
+ * (src/sstable/manager.rs:148-151).
+ *
+ * Finds every record boundary of `len` bytes of SSTable data and writes one
+ * hg_span per record, in file order, to spans[0..n).  If n > cap, only the
+ * first `cap` spans are written and HG_ERR_CAPACITY is returned with *n_out =
+ * n.  On a format error, spans[0..n_out) hold the records before the failing
+ * one and err->offset is the failing record's start. */
+int hg_decode_dev(hg_ctx* ctx, const uint8_t* d_sst, uint64_t len,
+                  hg_span* d_spans, uint64_t cap,
+                  uint64_t* n_out, hg_err* err);
+/* Same, enqueued on the context stream; result lands in *d_result. */
+int hg_decode_dev_async(hg_ctx* ctx, const uint8_t* d_sst, uint64_t len,
+                        hg_span* d_spans, uint64_t cap,
+                        hg_decode_result* d_result);
+/* Host-memory in and out (pinned staging, H2D -> decode -> D2H). */
+int hg_decode_host(hg_ctx* ctx, const uint8_t* h_sst, uint64_t len,
+                   hg_span* h_spans, uint64_t cap,
+                   uint64_t* n_out, hg_err* err);
+
+/* ---- encode ----------------------------------------------------------
+ * Replaces InternalPair::serialize (src/format.rs:23-37) and
+ * serialize_flatten (src/format.rs:40-42) as used by PersistedFile::new
+ * (src/sstable/storage.rs:21-38), and Index::new's second encode that only
+ * learns block lengths (src/sstable/index.rs:55-67).
+ *
+ * Packs pairs[0..n) (offsets into `arena`) into out[0..L), L = sum(16 + klen
+ * + vlen), in the given order.  Optional outputs: rec_off[i] = byte offset of
+ * record i; blocks[b] for every `block_stride` records (block_stride == 0
+ * with a non-NULL blocks is HG_ERR_INVALID_ARG: the reference panics,
+ * slice::chunks(0)).  If L > cap nothing is written past cap and
+ * HG_ERR_CAPACITY is returned with *out_len = L. */
+int hg_encode_dev(hg_ctx* ctx, const uint8_t* d_arena, const hg_pair* d_pairs,
+                  uint64_t n, uint8_t* d_out, uint64_t cap,
+                  uint64_t* d_rec_off, uint32_t block_stride,
+                  hg_block* d_blocks, uint64_t* out_len);
+int hg_encode_dev_async(hg_ctx* ctx, const uint8_t* d_arena,
+                        const hg_pair* d_pairs, uint64_t n, uint8_t* d_out,
+                        uint64_t cap, uint64_t* d_rec_off,
+                        uint32_t block_stride, hg_block* d_blocks,
+                        hg_encode_result* d_result);
+int hg_encode_host(hg_ctx* ctx, const uint8_t* h_arena, uint64_t arena_len,
+                   const hg_pair* h_pairs, uint64_t n, uint8_t* h_out,
+                   uint64_t cap, uint64_t* h_rec_off, uint32_t block_stride,
+                   hg_block* h_blocks, uint64_t* out_len);
+
+/* Number of blocks Index::new produces for n pairs: ceil(n / stride). */
+uint64_t hg_block_count(uint64_t n, uint32_t block_stride);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HORREUM_GPU_H */
