@@ -70,6 +70,7 @@ _PROTOS = {
     "hg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
     "hg_ctx_destroy": (ctypes.c_int, [_vp]),
     "hg_ctx_set_stream": (ctypes.c_int, [_vp, _vp]),
+    "hg_ctx_use_own_stream": (ctypes.c_int, [_vp]),
     "hg_ctx_stream": (_vp, [_vp]),
     "hg_ctx_synchronize": (ctypes.c_int, [_vp]),
     "hg_ctx_reserve": (ctypes.c_int, [_vp, _u64, _u64]),
@@ -97,6 +98,13 @@ def load_library(path=LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise HorreumGpuError(Status.HIP, f"{path} not built (run: make -C horreum_amd/csrc)")
+    # One HIP runtime per process: torch bundles libamdhip64.so.7 and our
+    # library needs the same SONAME.  Loading torch first makes the dynamic
+    # linker reuse its copy, so device pointers and streams are shared.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover - standalone C users
+        pass
     try:
         lib = ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover - environment specific

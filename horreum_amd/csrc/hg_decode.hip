@@ -58,6 +58,15 @@ struct DecodeArgs {
     uint32_t* ticket;            // zeroed before launch
     uint32_t nchunks;
     uint32_t hz;                 // zero high bytes required in klen/vlen
+    uint32_t* diag;              // DIAG builds only: DIAG_WORDS per chunk
+};
+
+// Diagnostic record per chunk (tools/decode_diag.py): phase end stamps
+// (s_memtime, relative to the chunk's start) and path facts.
+constexpr uint32_t DIAG_WORDS = 12;
+enum : uint32_t {
+    D_T_LOAD = 0, D_T_SURV, D_T_LIFT, D_T_AGG, D_T_LB, D_T_END,
+    D_NSURV, D_NLEV, D_GUESS, D_SPINS, D_COUNT, D_FLAGS
 };
 
 struct DecodeSmem {
@@ -130,9 +139,10 @@ struct LookbackOut {
 };
 
 // Called by all 64 lanes of wave 0.
-__device__ LookbackOut lookback(const DecodeArgs& a, uint32_t k) {
+__device__ LookbackOut lookback(const DecodeArgs& a, uint32_t k, uint32_t& spins_out) {
     const uint32_t lane = threadIdx.x & 63u;
     LookbackOut r{0, 0, 0, HG_OK};
+
     uint32_t spins = 0;
     const uint32_t SPIN_LIMIT = 1u << 22;
 restart:
@@ -160,7 +170,7 @@ restart:
             if (!(notready & relevant)) break;
             if (++spins > SPIN_LIMIT) {
                 r.err = HG_ERR_INTERNAL;
-                return r;
+                { spins_out = spins; return r; }
             }
             __builtin_amdgcn_s_sleep(2);
         }
@@ -172,7 +182,7 @@ restart:
                 r.err = __shfl(st_aux(w0), fi, 64);
                 r.errpos = __shfl(E, fi, 64);
                 r.g = __shfl(st_val(w1), fi, 64);
-                return r;
+                { spins_out = spins; return r; }
             }
         }
         // AGG lanes: predicted incoming exit must equal the older neighbour's exit.
@@ -193,7 +203,7 @@ restart:
                 if (st_flag(v0) == st_flag(v1) && st_flag(v0) >= ST_INCL) break;
                 if (++spins > SPIN_LIMIT) {
                     r.err = HG_ERR_INTERNAL;
-                    return r;
+                    { spins_out = spins; return r; }
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
@@ -204,7 +214,7 @@ restart:
         if (fi < 64) {
             r.g = __shfl(st_val(w1), fi, 64) + acc;
             r.x = xk;
-            return r;
+            { spins_out = spins; return r; }
         }
         first = false;
         j0 -= 63;  // lane 63 becomes the next window's lane 0
@@ -290,14 +300,25 @@ __device__ void serial_walk_emit(DecodeSmem& s, const DecodeArgs& a, uint64_t ba
     __syncthreads();
 }
 
+template <bool DIAG>
 __global__ __launch_bounds__(DEC_THREADS) void decode_kernel(DecodeArgs a) {
     __shared__ DecodeSmem s;
     const uint32_t tid = threadIdx.x;
     uint8_t* data = reinterpret_cast<uint8_t*>(s.data64);
+    uint64_t t_start = 0;
+    uint32_t* dg = nullptr;
+#define HG_STAMP(slot)                                                              \
+    do {                                                                            \
+        if (DIAG && tid == 0) dg[slot] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start); \
+    } while (0)
 
     if (tid == 0) s.chunk = atomicAdd(a.ticket, 1u);
     __syncthreads();
     const uint32_t k = s.chunk;
+    if (DIAG) {
+        t_start = __builtin_amdgcn_s_memtime();
+        dg = a.diag + (size_t)k * DIAG_WORDS;
+    }
     const uint64_t base = (uint64_t)k * DEC_CHUNK;
     const uint64_t rem = a.len - base;  // bytes from chunk start to end of input
     const uint32_t clen = rem < DEC_CHUNK ? (uint32_t)rem : DEC_CHUNK;
@@ -338,6 +359,7 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_kernel(DecodeArgs a) {
         *reinterpret_cast<uint4*>(data + off) = v;
     }
     __syncthreads();
+    HG_STAMP(D_T_LOAD);
 
     // ---- 2a. pre-candidate masks (zero-pattern filter) ----------------------
     // Positions p with base+p+16 > len can never start a record.
@@ -405,6 +427,7 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_kernel(DecodeArgs a) {
         s.zm[DEC_NGRAN] = 0;
     }
     __syncthreads();
+    HG_STAMP(D_T_SURV);
     const uint32_t N = s.nsurv;
     bool lifting = !s.slow;
 
@@ -457,6 +480,11 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_kernel(DecodeArgs a) {
         }
         if (tid == 0) s.nlev = K;
         __syncthreads();
+    }
+    HG_STAMP(D_T_LIFT);
+    if (DIAG && tid == 0) {
+        dg[D_NSURV] = N;
+        dg[D_NLEV] = lifting ? s.nlev : 0;
     }
 
     // ---- 5. speculative entry + AGG publish (wave 0) ---------------------------
@@ -525,8 +553,16 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_kernel(DecodeArgs a) {
             st_agent(&a.status[2 * k + 1], pack_status(ST_AGG, gxrel, 0));
             st_agent(&a.status[2 * k], pack_status(ST_AGG, gcount, gexit));
         }
+        HG_STAMP(D_T_AGG);
         // ---- 6. look-back ----------------------------------------------------
-        LookbackOut lb = lookback(a, k);
+        uint32_t spins = 0;
+        LookbackOut lb = lookback(a, k, spins);
+        HG_STAMP(D_T_LB);
+        if (DIAG && lane == 0) {
+            dg[D_SPINS] = spins;
+            dg[D_GUESS] = (have ? 1u : 0u) | (gxrel != NONE_REL ? 2u : 0u) |
+                          ((lb.x == (gxrel != NONE_REL ? base + gxrel : gexit)) ? 4u : 0u);
+        }
         if (lane == 0) {
             s.xk = lb.x;
             s.gk = lb.g;
@@ -618,6 +654,12 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_kernel(DecodeArgs a) {
         st_agent(&a.status[2 * k + 1], pack_status(ST_ERR, 0, gk));
         st_agent(&a.status[2 * k], pack_status(ST_ERR, kind, errpos));
     }
+    HG_STAMP(D_T_END);
+    if (DIAG && tid == 0) {
+        dg[D_COUNT] = (uint32_t)count;
+        dg[D_FLAGS] = (lifting ? 1u : 0u) | (perr != HG_OK ? 2u : 0u) | (kind != HG_OK ? 4u : 0u);
+    }
+#undef HG_STAMP
     // ---- 9. the last chunk reports the whole-file result ----------------------
     if (tid == 0 && k == a.nchunks - 1) {
         hg_decode_result r;
@@ -634,9 +676,10 @@ __global__ __launch_bounds__(DEC_THREADS) void decode_kernel(DecodeArgs a) {
 // Host-side launcher (called by the runtime; stream-ordered, no sync).
 // d_status must hold hgk_decode_workspace_bytes(len) bytes; the launcher
 // zeroes the statuses and the ticket word that follows them.
-extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
-                                 uint64_t cap, hg_decode_result* d_result,
-                                 unsigned long long* d_status, hipStream_t stream) {
+extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
+                                      uint64_t cap, hg_decode_result* d_result,
+                                      unsigned long long* d_status, uint32_t* d_diag,
+                                      hipStream_t stream) {
     using namespace hgk;
     const uint64_t nch = (len + DEC_CHUNK - 1) / DEC_CHUNK;
     // Zero high bytes every genuine length field must have: any record fits
@@ -653,11 +696,23 @@ extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_
     a.ticket = reinterpret_cast<uint32_t*>(d_status + 2 * nch);
     a.nchunks = (uint32_t)nch;
     a.hz = 8 - nb;
+    a.diag = d_diag;
     hipError_t e = hipMemsetAsync(d_status, 0, (size_t)(2 * nch + 2) * sizeof(unsigned long long),
                                   stream);
     if (e != hipSuccess) return HG_ERR_HIP;
-    hipLaunchKernelGGL(decode_kernel, dim3((uint32_t)nch), dim3(DEC_THREADS), 0, stream, a);
+    if (d_diag)
+        hipLaunchKernelGGL(decode_kernel<true>, dim3((uint32_t)nch), dim3(DEC_THREADS), 0, stream,
+                           a);
+    else
+        hipLaunchKernelGGL(decode_kernel<false>, dim3((uint32_t)nch), dim3(DEC_THREADS), 0,
+                           stream, a);
     return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
+                                 uint64_t cap, hg_decode_result* d_result,
+                                 unsigned long long* d_status, hipStream_t stream) {
+    return hgk_decode_launch_diag(d_sst, len, d_spans, cap, d_result, d_status, nullptr, stream);
 }
 
 extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) {

@@ -140,7 +140,13 @@ int hg_ctx_destroy(hg_ctx* c) {
 
 int hg_ctx_set_stream(hg_ctx* c, void* s) {
     if (!c) return HG_ERR_INVALID_ARG;
-    c->stream = s ? reinterpret_cast<hipStream_t>(s) : c->own;
+    c->stream = reinterpret_cast<hipStream_t>(s);
+    return HG_OK;
+}
+
+int hg_ctx_use_own_stream(hg_ctx* c) {
+    if (!c) return HG_ERR_INVALID_ARG;
+    c->stream = c->own;
     return HG_OK;
 }
 

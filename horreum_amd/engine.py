@@ -43,8 +43,13 @@ class Engine:
 
     # ---- context --------------------------------------------------------------
     def set_stream(self, stream):
-        handle = stream.cuda_stream if stream is not None else 0
-        check(self.lib.hg_ctx_set_stream(self.ctx, ctypes.c_void_p(handle)), "hg_ctx_set_stream")
+        """Launch on a torch stream (its handle may be 0: the null stream);
+        None selects the context's own stream."""
+        if stream is None:
+            check(self.lib.hg_ctx_use_own_stream(self.ctx), "hg_ctx_use_own_stream")
+            return
+        check(self.lib.hg_ctx_set_stream(self.ctx, ctypes.c_void_p(stream.cuda_stream)),
+              "hg_ctx_set_stream")
 
     def reserve(self, max_sst_bytes=0, max_pairs=0):
         check(self.lib.hg_ctx_reserve(self.ctx, max_sst_bytes, max_pairs), "hg_ctx_reserve")

@@ -118,8 +118,10 @@ const char* hg_status_string(int status);
 /* Create a context bound to HIP device `device` with its own stream. */
 int hg_ctx_create(int device, hg_ctx** out);
 int hg_ctx_destroy(hg_ctx* ctx);
-/* Use a caller stream (a hipStream_t); NULL restores the context's own. */
+/* Launch on a caller stream (a hipStream_t; NULL = the null stream). */
 int hg_ctx_set_stream(hg_ctx* ctx, void* hip_stream);
+/* Go back to the stream the context created for itself. */
+int hg_ctx_use_own_stream(hg_ctx* ctx);
 void* hg_ctx_stream(hg_ctx* ctx);
 int hg_ctx_synchronize(hg_ctx* ctx);
 /* Pre-size the device workspace so later calls never allocate

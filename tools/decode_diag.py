@@ -1,0 +1,111 @@
+#!/usr/bin/env python3
+"""Per-chunk decode diagnostics (DIAG build of decode_kernel).
+
+Prints phase durations (s_memtime cycles, relative to each chunk's start),
+survivor counts, lifting levels, how the entry guess was made and whether it
+held, and look-back spin counts, for the cfg2 table and a mixed-size table.
+Timing of the DIAG build is not quoted anywhere: it exists for shares.
+"""
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from horreum_amd import abi, synth  # noqa: E402
+from horreum_amd.engine import Engine  # noqa: E402
+
+NAMES = ["t_load", "t_surv", "t_lift", "t_agg", "t_lb", "t_end", "nsurv", "nlev", "guess",
+         "spins", "count", "flags"]
+
+
+def run(eng, sst, L, label):
+    lib = abi.load_library()
+    lib.hgk_decode_launch_diag.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p]
+    lib.hgk_decode_workspace_bytes.argtypes = [ctypes.c_uint64]
+    lib.hgk_decode_workspace_bytes.restype = ctypes.c_uint64
+    nch = (L + 16383) // 16384
+    ws = torch.zeros(int(lib.hgk_decode_workspace_bytes(L)), dtype=torch.uint8, device=eng.device)
+    cap = L // 16
+    spans = eng.empty(cap * 16)
+    res = eng.empty(64)
+    diag = torch.zeros(nch * 12, dtype=torch.int32, device=eng.device)
+    stream = torch.cuda.current_stream(eng.device).cuda_stream
+    out = {}
+    for mode in ("plain", "diag"):
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        times = []
+        for _ in range(6):
+            ev0.record()
+            rc = lib.hgk_decode_launch_diag(
+                ctypes.c_void_p(sst.data_ptr()), L, ctypes.c_void_p(spans.data_ptr()), cap,
+                ctypes.c_void_p(res.data_ptr()), ctypes.c_void_p(ws.data_ptr()),
+                ctypes.c_void_p(diag.data_ptr() if mode == "diag" else 0), ctypes.c_void_p(stream))
+            ev1.record()
+            torch.cuda.synchronize()
+            assert rc == 0
+            times.append(ev0.elapsed_time(ev1))
+        out[mode + "_ms"] = sorted(times)[len(times) // 2]
+    r = res[:24].cpu().numpy()
+    out["n"] = int(r[:8].view("<u8")[0])
+    out["kind"] = int(r[8:12].view("<i4")[0])
+    d = diag.cpu().numpy().astype(np.uint32).reshape(nch, 12)
+    stats = {}
+    for i, nm in enumerate(NAMES):
+        col = d[:, i].astype(np.float64)
+        stats[nm] = {"p10": float(np.percentile(col, 10)), "p50": float(np.median(col)),
+                     "p90": float(np.percentile(col, 90)), "max": float(col.max())}
+    g = d[:, 8]
+    out["guess_have"] = float(((g & 1) != 0).mean())
+    out["guess_ok"] = float(((g & 4) != 0).mean())
+    out["lifting"] = float(((d[:, 11] & 1) != 0).mean())
+    out["stats"] = stats
+    out["label"] = label
+    print(json.dumps(out), flush=True)
+    return out
+
+
+def main():
+    eng = Engine(0)
+    n = 8_134_407
+    sst = synth.fixed_sst(n, 16, 100, seed=2, device=eng.device)
+    run(eng, sst, sst.numel(), "cfg2 16B/100B")
+    del sst
+    # mixed sizes: values 8..4096 (cfg4-like), from the oracle-free device builder
+    rng = np.random.default_rng(4)
+    m = 200_000
+    kl = np.full(m, 16, np.int64)
+    vl = rng.integers(8, 4097, m)
+    vl[rng.random(m) < 0.05] = 0
+    sizes = 16 + kl + vl
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
+    for i in range(16):
+        buf[offs[:-1] + i] = hdr[:, i]
+    t = torch.from_numpy(buf).to(eng.device)
+    run(eng, t, t.numel(), "mixed 16B/8..4096B")
+    # small mixed records
+    m = 2_000_000
+    kl = rng.integers(0, 24, m)
+    vl = rng.integers(0, 64, m)
+    sizes = 16 + kl + vl
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
+    for i in range(16):
+        buf[offs[:-1] + i] = hdr[:, i]
+    t = torch.from_numpy(buf).to(eng.device)
+    run(eng, t, t.numel(), "small mixed 0..24B/0..64B")
+
+
+if __name__ == "__main__":
+    main()
