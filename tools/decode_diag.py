@@ -21,7 +21,7 @@ import torch  # noqa: E402
 from horreum_amd import abi, synth  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
 
-NAMES = ["t_load", "t_surv", "t_lift", "t_agg", "t_lb", "t_end", "nsurv", "nlev", "guess",
+NAMES = ["t_load", "mode", "t_res", "t_agg", "t_lb", "t_end", "rounds", "rounds2", "guess",
          "spins", "count", "flags"]
 
 
@@ -65,8 +65,13 @@ def run(eng, sst, L, label):
                      "p90": float(np.percentile(col, 90)), "max": float(col.max())}
     g = d[:, 8]
     out["guess_have"] = float(((g & 1) != 0).mean())
+    out["guess_from_pred"] = float(((g & 2) != 0).mean())
     out["guess_ok"] = float(((g & 4) != 0).mean())
-    out["lifting"] = float(((d[:, 11] & 1) != 0).mean())
+    mode = d[:, 1]
+    out["mode_stride"] = float((mode == 1).mean())
+    out["mode_relax"] = float((mode == 2).mean())
+    out["mode_serial"] = float((mode == 3).mean())
+    out["general_used"] = float(((d[:, 11] & 8) != 0).mean())
     out["stats"] = stats
     out["label"] = label
     print(json.dumps(out), flush=True)

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round GPU check: parity tests, decode diagnostics, bench.  Every GPU step
-# has its own time limit; a fault/timeout (rc >= 124) stops the script.
+# Round GPU check: parity tests (every decode geometry), variants A/B, bench.
+# Every GPU step has its own time limit; a fault/timeout (rc >= 124) stops.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 step() {  # step <name> <seconds> <cmd...>
@@ -11,6 +11,9 @@ step() {  # step <name> <seconds> <cmd...>
   if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-TAILN=15 step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
-step diag 300 python tools/decode_diag.py
+for c in ${CHUNKS:-16384}; do
+  HG_DECODE_CHUNK=$c TAILN=4 step pytest_gpu_$c 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
+done
+[ -n "$VARIANTS" ] && step variants 400 python tools/decode_variants.py
+[ -n "$DIAG" ] && step diag 300 python tools/decode_diag.py
 step bench 400 python bench.py --steps 20 --warmup 5 --cpu-sample-mb 256
