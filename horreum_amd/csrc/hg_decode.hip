@@ -7,54 +7,61 @@
 // is one long dependency chain with no sync points on disk
 // (src/sstable/storage.rs:31-32).  Here it becomes a single pass over HBM.
 //
-// Chunk (16 KiB, one 256-thread workgroup, taken by atomic ticket so chunk
-// k-1 is always already running and the look-back cannot deadlock):
-//  1. Stage the chunk (+16 B halo) in LDS with 16-byte loads; per-granule
-//     zero-byte masks give a bit-parallel header filter (a genuine length
-//     field has `hz` zero high bytes, since every record fits in `len`).
-//  2. Speculative segmented walk: lane t owns bytes [64t, 64t+64).  It guesses
-//     its first record start (first position passing the filter, a full
-//     bound check and one step of look-ahead) and walks from it to its
-//     segment end: <= 4 records, kept in registers.
-//  3. Relaxation: given an entry X, each lane's true entry is its left
-//     neighbour's exit; lanes whose guess disagrees re-walk.  Rounds of
-//     (read neighbour exit from LDS, barrier) until nothing changes; the
-//     fixed point is exact.  Typically 1-2 rounds.
-//  4. The chunk entry is speculated (predecessor's published exit if it is
-//     already out, else the earliest lane whose guessed chain agrees with
-//     the most following lanes) and the chunk publishes AGG(count, entry,
-//     exit).  A decoupled look-back (one wave, 63 predecessors per step)
-//     yields the exact entry X_k and record base G_k: the nearest INCL
-//     predecessor plus the AGGs after it, provided each AGG's guessed entry
-//     equals its predecessor's exit (checked with one ballot); a mismatch
-//     waits for that chunk's self-corrected INCL.
-//  5. If X_k differs from the guess, relax again from X_k (lane walks are
-//     reused), publish INCL(G_k + count, exit) and emit spans[G_k + ...]
-//     straight from the lane walks.  Format errors and pathological chunks
-//     (too many relaxation rounds) fall back to an exact serial walk in LDS.
+// Work unit = a BATCH of PIECES (8 x 16 KiB), one 256-thread workgroup, taken
+// by one atomic ticket (so batch b-1 is always already running: the look-back
+// cannot deadlock; one returning atomic per 128 KiB keeps the ticket far from
+// its ~88/us limit).  Per batch:
+//  1. Entry guess for piece 0: the predecessor batch's published exit if it is
+//     out, else a record whose 16-byte header repeats 3 lengths ahead, else
+//     the general engine's guess (below).
+//  2. Pieces are staged in LDS one at a time (the next piece's 16-byte loads
+//     are in flight in registers meanwhile) and walked from the exact exit of
+//     the previous piece — speculation happens once per batch:
+//     - stride run: if the header at X repeats at X+R, X+2R ... to the piece
+//       end (one compare per lane), the records are that progression; kept as
+//       a 32-byte summary and emitted arithmetically later;
+//     - general engine otherwise: bit-parallel header filter over zero-byte
+//       masks (a genuine length field has `hz` zero high bytes), exact bound
+//       check and one look-ahead step give "strong" candidates; a candidate
+//       is "backed" if another candidate's next lands on it (true records are
+//       backed by their predecessor; shifted reads of a header are not).  Each
+//       lane owns 64 bytes, guesses its first backed candidate, walks <= 4
+//       records, and a relaxation (entry := left neighbour's exit, re-walk on
+//       disagreement, seeded by a block max-scan over chain lanes) reaches the
+//       exact fixed point; spans go to a scratch area until the batch's record
+//       base is known.  Pathological pieces use an exact serial walk.
+//  3. Publish AGG(count, guessed entry, exit); decoupled look-back (one wave,
+//     63 predecessors per step): the nearest INCL plus the AGGs after it give
+//     the exact entry X_b and record base G_b, provided every AGG's guessed
+//     entry equals its predecessor's exit (one ballot); a mismatch waits for
+//     that batch's self-corrected INCL.
+//  4. Guess right: emit stride pieces arithmetically and copy scratch spans to
+//     spans[G_b + ...], publish INCL.  Guess wrong or a format error: redo the
+//     batch exactly from X_b (pieces re-read), emitting directly.
 #include <stdlib.h>
 
 #include "hg_device.hpp"
 
 namespace hgk {
 
-// Chunk geometry is a template parameter (DEC_CHUNK bytes per workgroup of
-// DEC_THREADS threads; each lane owns a 64-byte segment).
-#define HG_DEC_GEOM                                                               \
-    constexpr uint32_t DEC_THREADS = DEC_CHUNK / 64;                             \
-    constexpr uint32_t DEC_NW = DEC_THREADS / 64;                                \
-    constexpr uint32_t DEC_SEG = 64;                                             \
-    constexpr uint32_t DEC_NGRAN = DEC_CHUNK / 16;                               \
-    constexpr uint32_t DEC_GPT = DEC_NGRAN / DEC_THREADS;                        \
-    constexpr uint32_t DEC_LOG = DEC_CHUNK / 16;                                 \
-    (void)DEC_NW; (void)DEC_SEG; (void)DEC_NGRAN; (void)DEC_GPT; (void)DEC_LOG;
-constexpr uint32_t DEC_CHUNK_MIN = 4096;
-constexpr uint32_t DEC_MAX_ROUNDS = 24;
-constexpr uint32_t DEC_CAND_CAP = 16;                   // strong candidates examined per lane
-constexpr uint32_t NONE_REL = 0x3FFFFFu;                // "no record starts here"
+constexpr uint32_t PIECE = 16384;                 // bytes staged in LDS at a time
+constexpr uint32_t THREADS = 256;                 // one 64-byte segment per lane
+constexpr uint32_t NW = THREADS / 64;
+constexpr uint32_t SEG = PIECE / THREADS;         // 64
+constexpr uint32_t NGRAN = PIECE / 16;            // 1024 granules of 16 B
+constexpr uint32_t GPT = NGRAN / THREADS;         // 4 granules per thread
+constexpr uint32_t BATCH = 8;                     // pieces per ticket / status
+constexpr uint64_t BATCH_BYTES = (uint64_t)PIECE * BATCH;
+constexpr uint32_t MAX_REC_PIECE = PIECE / 16;    // records per piece (>= 16 B each)
+constexpr uint32_t WALK_LOG = PIECE / 16;         // serial-walk batch
+constexpr uint32_t MAX_ROUNDS = 24;
+constexpr uint32_t CAND_CAP = 16;                 // strong candidates examined per lane
+constexpr uint32_t SHORT_WALK = 24;               // serial pre-walk budget (large records)
+constexpr uint32_t NONE_REL = 0x3FFFFFu;          // "no record starts here"
 constexpr uint32_t NO_GUESS = 0xFFFFFFFFu;
 
 enum : uint32_t { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2, ST_ERR = 3 };
+enum : uint32_t { PK_EMPTY = 0, PK_STRIDE = 1, PK_SCRATCH = 2 };
 
 struct DecodeArgs {
     const uint8_t* sst;
@@ -62,55 +69,94 @@ struct DecodeArgs {
     hg_span* spans;
     uint64_t cap;
     hg_decode_result* result;
-    unsigned long long* status;  // 2 words per chunk, zeroed before launch
+    unsigned long long* status;  // 2 words per batch, zeroed before launch
     uint32_t* ticket;            // zeroed before launch
-    uint32_t nchunks;
+    hg_span* scratch;            // MAX_REC_PIECE spans per piece (speculative general pieces)
+    uint32_t nbatches;
+    uint32_t npieces;
     uint32_t hz;                 // zero high bytes required in klen/vlen
-    uint32_t* diag;              // DIAG builds only: DIAG_WORDS per chunk
+    uint32_t* diag;              // DIAG builds only: DIAG_WORDS per batch
 };
 
-// Diagnostic record per chunk (tools/decode_diag.py): phase end stamps
-// (s_memtime, relative to the chunk's start) and path facts.
-constexpr uint32_t DIAG_WORDS = 12;
+// Diagnostic record per batch (tools/decode_diag.py).
+constexpr uint32_t DIAG_WORDS = 24;
+constexpr uint32_t NPROF = 8;  // DIAG phase cycle counters, words 16..23
 enum : uint32_t {
-    D_T_LOAD = 0, D_T_SPEC, D_T_RES, D_T_AGG, D_T_LB, D_T_END,
-    D_ROUNDS, D_ROUNDS2, D_GUESS, D_SPINS, D_COUNT, D_FLAGS
+    D_T_SPEC = 0, D_T_AGG, D_T_LB, D_T_END, D_NSTRIDE, D_NGEN, D_NSERIAL,
+    D_GUESS, D_SPINS, D_COUNT, D_FLAGS, D_REDO, D_C_PREP, D_C_RELAX, D_ROUNDS, D_NSHORT
 };
 
-template <uint32_t DEC_CHUNK>
+struct PieceSum {
+    uint64_t x;     // entry (absolute)
+    uint64_t exit;  // first start at or after the piece end (absolute)
+    uint64_t R;     // stride run record length
+    uint32_t kl, vl;
+    uint32_t count;
+    uint32_t kind;  // PK_*
+};
+
 struct DecodeSmem {
-    static constexpr uint32_t DEC_THREADS = DEC_CHUNK / 64;
-    static constexpr uint32_t DEC_NW = DEC_THREADS / 64;
-    uint64_t data64[(DEC_CHUNK + 64) / 8];  // chunk bytes + 16 B halo + read slack
-    uint16_t pc[DEC_CHUNK / 16 + 8];        // header-filter masks; later the serial-walk log
-    uint64_t sx[2][DEC_THREADS];            // per-lane exits, double-buffered by round
-    uint32_t sg[DEC_THREADS];               // per-lane guesses
-    uint8_t tgt[DEC_THREADS];               // lane is the target of another lane's exit
-    uint32_t bk[DEC_CHUNK / 32];            // "backed": some strong candidate's next lands here
-    uint32_t scan_tmp[DEC_NW];
-    unsigned long long best, best2;         // entry-heuristic reductions
-    uint32_t chunk, walk_n, walk_done, x_count, pred_ok;
+    uint64_t data64[(PIECE + 64) / 8];  // piece bytes + 16 B halo + read slack
+    uint16_t pc[NGRAN + 8];             // header-filter masks; later the serial-walk log
+    uint64_t sx[2][THREADS];            // per-lane exits, double-buffered by round
+    uint32_t sg[THREADS];               // per-lane guesses
+    uint8_t tgt[THREADS];               // lane is the target of another lane's exit
+    uint32_t bk[PIECE / 32];            // "backed": some strong candidate's next lands here
+    uint4 halo[BATCH];                  // first 16 bytes after each piece of the batch
+    PieceSum sum[BATCH];
+    uint32_t scan_tmp[NW];
+    unsigned long long best, best2;     // entry-heuristic reductions
+    uint32_t batch, walk_n, walk_done, pred_ok;
     uint64_t pred_exit;
     uint64_t xk, gk, exitk;
+    uint32_t rounds;                    // relaxation rounds of the last relax()
+    uint32_t prof[NPROF];               // DIAG: cycles per phase (see HG_PROF)
+    uint64_t plast;                     // DIAG: last phase stamp
     int32_t err_kind;
     uint64_t err_pos;
 };
 
+// Block-uniform values read from LDS: keep them in SGPRs.
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int32_t uni(int32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t uni(uint64_t x) {
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)x) |
+           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32);
+}
+
+// DIAG phase accounting: cycles since the last stamp go to counter `slot`
+// (0 filter, 1 candidates, 2 lane walks, 3 relax seeding, 4 relax rounds,
+// 5 scan+emit, 6 staging, 7 stride attempt).
+#define HG_PROF(slot)                                                \
+    do {                                                             \
+        if (DIAG && threadIdx.x == 0) {                              \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();      \
+            s.prof[slot] += (uint32_t)(now_ - s.plast);              \
+            s.plast = now_;                                          \
+        }                                                            \
+    } while (0)
+
 // ---- lane walk --------------------------------------------------------------
-// Records starting in [x, segend) (chunk-relative), validated exactly as the
+// Records starting in [x, segend) (piece-relative), validated exactly as the
 // reference would read them.  dead = a record that cannot be read (the
 // reference would fail there).  Exit = first start at or after segend.
 struct Walk {
-    uint64_t exit;  // absolute
-    uint32_t p0, p1, p2, p3;
+    uint64_t exit;      // absolute
+    uint32_t p01, p23;  // up to four 16-bit positions
     uint32_t cnt;
     bool dead;
 };
+
+__device__ __forceinline__ uint32_t walk_pos(const Walk& w, uint32_t i) {
+    const uint32_t v = i < 2 ? w.p01 : w.p23;
+    return (i & 1) ? (v >> 16) : (v & 0xFFFFu);
+}
 
 __device__ __forceinline__ void lane_walk(const uint8_t* data, uint64_t base, uint64_t len,
                                           uint32_t x, uint32_t segend, Walk& w) {
     w.cnt = 0;
     w.dead = false;
+    w.p01 = w.p23 = 0;
     uint64_t cur = x;
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
@@ -126,18 +172,36 @@ __device__ __forceinline__ void lane_walk(const uint8_t* data, uint64_t base, ui
             w.dead = true;
             break;
         }
-        if (it == 0) w.p0 = (uint32_t)cur;
-        if (it == 1) w.p1 = (uint32_t)cur;
-        if (it == 2) w.p2 = (uint32_t)cur;
-        if (it == 3) w.p3 = (uint32_t)cur;
+        if (it == 0) w.p01 = (uint32_t)cur;
+        if (it == 1) w.p01 |= (uint32_t)cur << 16;
+        if (it == 2) w.p23 = (uint32_t)cur;
+        if (it == 3) w.p23 |= (uint32_t)cur << 16;
         ++w.cnt;
         cur += 16 + kl + vl;
     }
     w.exit = base + cur;
 }
 
+__device__ __forceinline__ void write_span(hg_span* out, uint64_t gi, uint64_t off, uint64_t kl,
+                                           uint64_t vl) {
+    uint4 sp;
+    sp.x = (uint32_t)off;
+    sp.y = (uint32_t)(off >> 32);
+    sp.z = (uint32_t)kl;
+    sp.w = (uint32_t)vl;
+    *reinterpret_cast<uint4*>(out + gi) = sp;
+}
+
+__device__ __forceinline__ void store_span(hg_span* out, uint64_t cap, uint64_t gi,
+                                           const uint8_t* data, uint64_t base, uint32_t p) {
+    if (gi >= cap) return;
+    uint64_t kl, vl;
+    lds_header(data, p, kl, vl);
+    write_span(out, gi, base + p, kl, vl);
+}
+
 // ---- relaxation ---------------------------------------------------------------
-// Exact per-lane state for chunk entry X (absolute).  All threads call it.
+// Exact per-lane state for piece entry X (absolute).  All threads call it.
 // Each lane caches one walk (from guess g).  A lane is a pass-through when
 // its true entry lies at or past its segment end (a record spans it).
 // Seeding: a lane is "on the chain" if it is the entry lane or another
@@ -145,20 +209,18 @@ __device__ __forceinline__ void lane_walk(const uint8_t* data, uint64_t base, ui
 // cached exit of the nearest chain lane at or before it (block max-scan), so
 // with correct guesses one verification round suffices.  Rounds then re-walk
 // lanes whose true entry differs from their guess until nothing changes;
-// that fixed point is exact.  Returns false if it did not converge (the
-// caller falls back to a serial walk).  On return cnt = this lane's records,
-// any_dead says whether the true path hits an unreadable record, and s.exitk
-// is the chunk exit.
-template <uint32_t DEC_CHUNK>
-__device__ bool relax(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t base, uint64_t len,
+// that fixed point is exact.  Returns false if it did not converge.  On
+// return cnt = this lane's records, any_dead says whether the true path hits
+// an unreadable record, and s.exitk is the piece exit.
+template <bool DIAG>
+__device__ bool relax(DecodeSmem& s, const uint8_t* data, uint64_t base, uint64_t len,
                       uint32_t clen, uint64_t X, uint32_t& g, Walk& w, uint32_t& cnt,
-                      bool& any_dead, uint32_t& rounds) {
-    HG_DEC_GEOM
+                      bool& any_dead) {
     const uint32_t t = threadIdx.x;
     const uint32_t lane = t & 63u, wid = t >> 6;
-    const uint32_t segend = min((t + 1) * DEC_SEG, clen);
+    const uint32_t segend = min((t + 1) * SEG, clen);
     const uint64_t seg_end_abs = base + segend;
-    const uint32_t je = (X >= base + clen) ? DEC_THREADS : (uint32_t)((X - base) / DEC_SEG);
+    const uint32_t je = (X >= base + clen) ? THREADS : (uint32_t)((X - base) / SEG);
     const bool active = t >= je;
     if (t == je && (g == NO_GUESS || base + g != X)) {
         g = (uint32_t)(X - base);
@@ -170,7 +232,7 @@ __device__ bool relax(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t ba
     s.tgt[t] = 0;
     __syncthreads();
     if (active && valid && w.exit < base + clen) {  // link into the lane holding our exit
-        const uint32_t u = (uint32_t)((w.exit - base) / DEC_SEG);
+        const uint32_t u = (uint32_t)((w.exit - base) / SEG);
         if (s.sg[u] == (uint32_t)(w.exit - base)) s.tgt[u] = 1;
     }
     __syncthreads();
@@ -188,16 +250,17 @@ __device__ bool relax(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t ba
     __syncthreads();
     s.sx[1][t] = seed;
     __syncthreads();
+    HG_PROF(3);
     bool ok = false, pass = false;
     uint32_t r = 1;
-    for (; r <= DEC_MAX_ROUNDS; ++r) {
+    for (; r <= MAX_ROUNDS; ++r) {
         const uint64_t* cur = s.sx[r & 1];
         uint64_t* nxt = s.sx[(r + 1) & 1];
         int changed = 0;
         if (active) {
             const uint64_t ein = (t == je) ? X : cur[t - 1];
             uint64_t val;
-            if (ein >= seg_end_abs) {  // a record (or the chunk exit) spans this segment
+            if (ein >= seg_end_abs) {  // a record (or the piece exit) spans this segment
                 pass = true;
                 val = ein;
             } else {
@@ -219,11 +282,14 @@ __device__ bool relax(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t ba
             break;
         }
     }
-    rounds = r;
     cnt = (active && !pass) ? w.cnt : 0;
     any_dead = __syncthreads_or(active && !pass && w.dead);
-    if (t == DEC_THREADS - 1) s.exitk = s.sx[(r + 1) & 1][t];
+    if (t == THREADS - 1) {
+        s.exitk = s.sx[(r + 1) & 1][t];
+        s.rounds = r;
+    }
     __syncthreads();
+    HG_PROF(4);
     return ok;
 }
 
@@ -233,8 +299,7 @@ struct LookbackOut {
     int32_t err;  // HG_OK or error kind to propagate
 };
 
-// Called by all 64 lanes of wave 0.
-template <uint32_t DEC_CHUNK>
+// Exact entry and record base of batch k.  Called by all 64 lanes of wave 0.
 __device__ LookbackOut lookback(const DecodeArgs& a, uint32_t k, uint32_t& spins_out) {
     const uint32_t lane = threadIdx.x & 63u;
     LookbackOut r{0, 0, 0, HG_OK};
@@ -250,7 +315,7 @@ restart:
         uint32_t f;
         int fi;
         for (;;) {
-            if (j < 0) {  // virtual chunk -1: exact exit 0, 0 records
+            if (j < 0) {  // virtual batch -1: exact exit 0, 0 records
                 w0 = pack_status(ST_INCL, 0, 0);
                 w1 = pack_status(ST_INCL, NONE_REL, 0);
             } else {
@@ -284,13 +349,13 @@ restart:
         }
         // AGG lanes: predicted incoming exit must equal the older neighbour's exit.
         const uint32_t xrel = st_aux(w1);
-        const uint64_t P = (xrel != NONE_REL) ? (uint64_t)j * DEC_CHUNK + xrel : E;
+        const uint64_t P = (xrel != NONE_REL) ? (uint64_t)j * BATCH_BYTES + xrel : E;
         const uint64_t Eolder = __shfl_down(E, 1, 64);
         const int lim = fi < 64 ? fi : 63;  // lanes [0, lim) are checked
         const bool bad = (int)lane < lim && P != Eolder;
         const unsigned long long badm = __ballot(bad);
         if (badm) {
-            // The oldest mismatch is a chunk whose guess was wrong; it
+            // The oldest mismatch is a batch whose guess was wrong; it
             // corrects itself after its own look-back.  Wait for its INCL.
             const int m = 63 - __clzll((long long)badm);
             const int64_t jm = j0 - m;
@@ -320,48 +385,15 @@ restart:
     }
 }
 
-// ---- serial count (AGG for chunks the relaxation cannot settle) -------------
-// Thread 0 walks the guessed path from absolute x to the chunk end without
-// emitting; all threads get (count, exit, dead) through LDS.
-template <uint32_t DEC_CHUNK>
-__device__ void serial_count(DecodeSmem<DEC_CHUNK>& s, const DecodeArgs& a, uint64_t base, uint32_t clen,
-                             uint64_t x, uint64_t& count, uint64_t& exit, bool& dead) {
-    HG_DEC_GEOM
-    const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
-    if (threadIdx.x == 0) {
-        uint64_t cur = x, n = 0;
-        bool bad = false;
-        while (cur < base + clen) {
-            if (cur + 16 > a.len) { bad = true; break; }
-            uint64_t kl, vl;
-            lds_header(data, (uint32_t)(cur - base), kl, vl);
-            if (kl > ~0ull - vl || kl + vl > a.len - cur - 16 || ((kl >> 32) | (vl >> 32))) {
-                bad = true;
-                break;
-            }
-            ++n;
-            cur += 16 + kl + vl;
-        }
-        s.walk_n = (uint32_t)n;
-        s.walk_done = bad;
-        s.exitk = cur;
-    }
-    __syncthreads();
-    count = s.walk_n;
-    dead = s.walk_done;
-    exit = s.exitk;
-    __syncthreads();
-}
-
-// ---- serial walk (exact; errors and pathological chunks) -------------------
-// Thread 0 walks from absolute x, logging up to DEC_LOG starts into s.pc; the
-// whole block then emits the batch.
-template <uint32_t DEC_CHUNK>
-__device__ void serial_walk_emit(DecodeSmem<DEC_CHUNK>& s, const DecodeArgs& a, uint64_t base,
-                                 uint32_t clen, uint64_t x, uint64_t g) {
-    HG_DEC_GEOM
+// ---- serial walk (exact; errors and pathological pieces) ---------------------
+// Thread 0 walks from absolute x, logging up to WALK_LOG starts into s.pc;
+// the whole block then writes the batch to out[gbase + i] (i < cap - gbase).
+// Returns the count; s.err_kind / s.err_pos / s.exitk describe the end.
+__device__ uint64_t serial_walk_emit(DecodeSmem& s, uint64_t len, uint64_t base, uint32_t clen,
+                                     uint64_t x, hg_span* out, uint64_t cap, uint64_t gbase) {
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     uint64_t emitted = 0;
+    __syncthreads();
     if (threadIdx.x == 0) {
         s.err_kind = HG_OK;
         s.exitk = x;
@@ -372,12 +404,12 @@ __device__ void serial_walk_emit(DecodeSmem<DEC_CHUNK>& s, const DecodeArgs& a, 
             uint32_t n = 0;
             uint64_t cur = s.exitk;
             bool done = false;
-            while (n < DEC_LOG) {
+            while (n < WALK_LOG) {
                 if (cur >= base + clen) {
                     done = true;
                     break;
                 }
-                if (cur + 16 > a.len) {
+                if (cur + 16 > len) {
                     s.err_kind = HG_ERR_TRUNCATED_HEADER;
                     done = true;
                     break;
@@ -389,7 +421,7 @@ __device__ void serial_walk_emit(DecodeSmem<DEC_CHUNK>& s, const DecodeArgs& a, 
                     done = true;
                     break;
                 }
-                if (kl + vl > a.len - cur - 16) {
+                if (kl + vl > len - cur - 16) {
                     s.err_kind = HG_ERR_TRUNCATED_BODY;
                     done = true;
                     break;
@@ -408,88 +440,59 @@ __device__ void serial_walk_emit(DecodeSmem<DEC_CHUNK>& s, const DecodeArgs& a, 
         }
         __syncthreads();
         const uint32_t n = s.walk_n;
-        for (uint32_t t = threadIdx.x; t < n; t += DEC_THREADS) {
-            uint32_t p = s.pc[t];
-            uint64_t kl, vl;
-            lds_header(data, p, kl, vl);
-            uint64_t gi = g + emitted + t;
-            if (gi < a.cap) {
-                uint4 sp;
-                uint64_t off = base + p;
-                sp.x = (uint32_t)off;
-                sp.y = (uint32_t)(off >> 32);
-                sp.z = (uint32_t)kl;
-                sp.w = (uint32_t)vl;
-                *reinterpret_cast<uint4*>(a.spans + gi) = sp;
-            }
-        }
+        for (uint32_t t = threadIdx.x; t < n; t += THREADS)
+            store_span(out, cap, gbase + emitted + t, data, base, s.pc[t]);
         emitted += n;
         const bool done = s.walk_done;
         if (done) break;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        s.x_count = (uint32_t)emitted;
-        if (s.err_kind != HG_OK) s.err_pos = s.exitk;
-    }
+    if (threadIdx.x == 0 && s.err_kind != HG_OK) s.err_pos = s.exitk;
     __syncthreads();
+    return emitted;
 }
-
-__device__ __forceinline__ void store_span(hg_span* spans, uint64_t cap, uint64_t gi,
-                                           const uint8_t* data, uint64_t base, uint32_t p) {
-    if (gi >= cap) return;
-    uint64_t kl, vl;
-    lds_header(data, p, kl, vl);
-    const uint64_t off = base + p;
-    uint4 sp;
-    sp.x = (uint32_t)off;
-    sp.y = (uint32_t)(off >> 32);
-    sp.z = (uint32_t)kl;
-    sp.w = (uint32_t)vl;
-    *reinterpret_cast<uint4*>(spans + gi) = sp;
-}
-
 
 // ---- stride fast path ---------------------------------------------------------
-// Header (klen, vlen) at chunk-relative p.
 __device__ __forceinline__ bool hdr_eq(const uint8_t* data, uint32_t p, uint64_t kl, uint64_t vl) {
     uint64_t a, b;
     lds_header(data, p, a, b);
     return a == kl && b == vl;
 }
 
-// Starts in [X, chunk end) if every record there repeats the header at X:
+// Starts in [X, piece end) if every record there repeats the header at X:
 // record t starts at X + t*R.  All threads call it; one parallel compare per
 // record.  Exact: if all headers match, each record's next is the following
 // one.  Returns false (not an error) when the run breaks or X cannot be read.
-template <uint32_t DEC_CHUNK>
-__device__ bool stride_run(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t base, uint64_t len,
-                           uint32_t clen, uint64_t X, uint64_t& count, uint64_t& exit,
-                           uint64_t& R, uint32_t& rk, uint32_t& rv) {
-    HG_DEC_GEOM
-    if (X >= base + clen) {  // no record starts in this chunk
-        count = 0;
-        exit = X;
-        R = 0;
+__device__ bool stride_run(const uint8_t* data, uint64_t base, uint64_t len, uint32_t clen,
+                           uint64_t X, PieceSum& ps) {
+    ps.x = X;
+    if (X >= base + clen) {  // no record starts in this piece
+        ps.count = 0;
+        ps.R = 0;
+        ps.kl = ps.vl = 0;
+        ps.kind = PK_EMPTY;
         return true;
     }
     const uint32_t xr = (uint32_t)(X - base);
     if (X + 16 > len) return false;
     uint64_t kl, vl;
     lds_header(data, xr, kl, vl);
+    kl = uni(kl);
+    vl = uni(vl);
     if (kl > ~0ull - vl || kl + vl > len - X - 16 || ((kl >> 32) | (vl >> 32))) return false;
-    R = 16 + kl + vl;
-    const uint64_t m = (clen - xr + R - 1) / R;  // records starting in [xr, clen)
-    if (X + m * R > len) return false;          // the last one would not fit
+    const uint64_t R = 16 + kl + vl;
+    const uint32_t m = (uint32_t)((clen - xr + R - 1) / R);  // records starting in [xr, clen)
+    if (X + m * R > len) return false;                       // the last one would not fit
     int bad = 0;
-    for (uint64_t t = 1 + threadIdx.x; t < m; t += DEC_THREADS)
+    for (uint32_t t = 1 + threadIdx.x; t < m; t += THREADS)
         bad |= !hdr_eq(data, xr + (uint32_t)(t * R), kl, vl);
     bad = __syncthreads_or(bad);
     if (bad) return false;
-    count = m;
-    exit = X + m * R;
-    rk = (uint32_t)kl;
-    rv = (uint32_t)vl;
+    ps.count = m;
+    ps.R = R;
+    ps.kl = (uint32_t)kl;
+    ps.vl = (uint32_t)vl;
+    ps.kind = PK_STRIDE;
     return true;
 }
 
@@ -510,12 +513,9 @@ __device__ __forceinline__ uint32_t filter_bits(const uint8_t* data, uint32_t gi
     return c;
 }
 
-// Wave 0: the first position in the chunk's first KiB whose header repeats
-// 3 strides ahead (inside the chunk), or NO_GUESS.
-template <uint32_t DEC_CHUNK>
-__device__ uint32_t stride_guess(const DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t rem,
-                                 uint32_t clen, uint32_t hz) {
-    HG_DEC_GEOM
+// Wave 0: the first position in the piece's first KiB whose header repeats
+// 3 lengths ahead (inside the piece), or NO_GUESS.
+__device__ uint32_t stride_guess(const uint8_t* data, uint64_t rem, uint32_t clen, uint32_t hz) {
     const uint32_t lane = threadIdx.x & 63u;
     const bool any_valid = rem >= 16;
     const uint64_t plim64 = any_valid ? rem - 16 : 0;
@@ -545,33 +545,29 @@ __device__ uint32_t stride_guess(const DecodeSmem<DEC_CHUNK>& s, const uint8_t* 
 // ---- general engine -------------------------------------------------------------
 // Header filter, strong candidates, "backed" marks, lane guess and the lane's
 // speculative walk (see the file comment).  All threads call it.
-template <uint32_t DEC_CHUNK>
-__device__ void general_prepare(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t base, uint64_t len,
+template <bool DIAG>
+__device__ void general_prepare(DecodeSmem& s, const uint8_t* data, uint64_t base, uint64_t len,
                                 uint64_t rem, uint32_t clen, uint32_t hz, uint32_t& g, Walk& w) {
-    HG_DEC_GEOM
     const uint32_t tid = threadIdx.x;
     const bool any_valid = rem >= 16;
     const uint64_t plim64 = any_valid ? rem - 16 : 0;
     const uint32_t plim = plim64 < 0xFFFFFFFFull ? (uint32_t)plim64 : 0xFFFFFFFFu;
+    __syncthreads();
 #pragma unroll
-    for (uint32_t i = 0; i < DEC_GPT; ++i) {
-        const uint32_t gi = i * DEC_THREADS + tid;
+    for (uint32_t i = 0; i < GPT; ++i) {
+        const uint32_t gi = i * THREADS + tid;
         s.pc[gi] = (uint16_t)filter_bits(data, gi, hz, clen, plim, any_valid);
     }
-    for (uint32_t i = tid; i < DEC_CHUNK / 32; i += DEC_THREADS) s.bk[i] = 0;
+    for (uint32_t i = tid; i < PIECE / 32; i += THREADS) s.bk[i] = 0;
     __syncthreads();
-    // strong = passes the filter, the exact bound check and one step of
-    // look-ahead (next start passes the filter or leaves the chunk).  A true
-    // record start is "backed": its predecessor's next lands on it.  Shifted
-    // reads of a header (hdr-1, hdr-2, hdr+6 ...) pass the filter too but are
-    // almost never backed.
-    const uint32_t seg0 = tid * DEC_SEG;
-    const uint32_t segend = min(seg0 + DEC_SEG, clen);
+    HG_PROF(0);
+    const uint32_t seg0 = tid * SEG;
+    const uint32_t segend = min(seg0 + SEG, clen);
     uint64_t strong = 0;
     uint32_t seen = 0;
-    for (uint32_t j = 0; j < DEC_GPT && seen < DEC_CAND_CAP; ++j) {
-        uint32_t c = s.pc[tid * DEC_GPT + j];
-        while (c && seen < DEC_CAND_CAP) {
+    for (uint32_t j = 0; j < GPT && seen < CAND_CAP; ++j) {
+        uint32_t c = s.pc[tid * GPT + j];
+        while (c && seen < CAND_CAP) {
             const uint32_t b = __ffs(c) - 1;
             c &= c - 1;
             ++seen;
@@ -588,45 +584,49 @@ __device__ void general_prepare(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, u
         }
     }
     __syncthreads();
+    HG_PROF(1);
     const uint64_t backed = (uint64_t)s.bk[seg0 >> 5] | ((uint64_t)s.bk[(seg0 >> 5) + 1] << 32);
     const uint64_t gm = strong & backed;
     g = gm ? seg0 + (uint32_t)(__ffsll((long long)gm) - 1) : NO_GUESS;
     w.exit = 0;
     w.cnt = 0;
     w.dead = true;
+    w.p01 = w.p23 = 0;
     if (g != NO_GUESS) lane_walk(data, base, len, g, segend, w);
     s.sg[tid] = (g != NO_GUESS && !w.dead) ? g : NO_GUESS;
-    // keep the strong mask for the entry guess
-    s.sx[0][tid] = strong;
+    s.sx[0][tid] = strong;  // the strong mask, for the entry guess
     __syncthreads();
+    HG_PROF(2);
 }
 
-// Chunk entry guess from the general engine: the first strong candidate whose
-// next start is another lane's guess (the chunk's first record backs its
-// second); else the strong candidate with the shortest record (shifted reads
-// of a header decode as huge lengths).  ~0 if the chunk has no candidate.
-template <uint32_t DEC_CHUNK>
-__device__ uint64_t general_entry_guess(DecodeSmem<DEC_CHUNK>& s, const uint8_t* data, uint64_t base,
-                                        uint32_t clen, uint32_t /*g*/) {
-    HG_DEC_GEOM
+// Piece entry guess from the general engine.  p1 = the first strong
+// candidate whose next start is another lane's guess ("links": the first
+// record backs the second).  The true entry is in [p1, next(p1)) and links
+// too; a shifted read of a small header also links sometimes, but decodes
+// as a ~256x longer record — so the guess is the linking candidate with the
+// shortest record in that window.  With no link at all: the strong candidate
+// with the shortest record.  ~0 if the piece has no candidate.
+__device__ uint64_t general_entry_guess(DecodeSmem& s, const uint8_t* data, uint64_t base,
+                                        uint32_t clen) {
     const uint32_t tid = threadIdx.x;
-    const uint32_t seg0 = tid * DEC_SEG;
+    const uint32_t seg0 = tid * SEG;
     if (tid == 0) {
         s.best = ~0ull;
         s.best2 = ~0ull;
     }
-    uint64_t m = s.sx[0][tid];
+    const uint64_t m0 = s.sx[0][tid];
     __syncthreads();
+    uint64_t m = m0;
     unsigned long long first_link = ~0ull, shortest = ~0ull;
-    for (uint32_t it = 0; m && it < DEC_CAND_CAP; ++it) {
+    for (uint32_t it = 0; m && it < CAND_CAP; ++it) {
         const uint32_t b = __ffsll((long long)m) - 1;
         m &= m - 1;
         const uint32_t p = seg0 + b;
         uint64_t kl, vl;
         lds_header(data, p, kl, vl);
         const uint64_t nx = (uint64_t)p + 16 + kl + vl;
-        if (nx < clen && s.sg[nx / DEC_SEG] == (uint32_t)nx) {
-            first_link = p;
+        if (nx < clen && s.sg[nx / SEG] == (uint32_t)nx) {
+            first_link = ((unsigned long long)p << 32) | (uint32_t)nx;
             break;
         }
         const unsigned long long key = ((16 + kl + vl) << 16) | p;
@@ -645,17 +645,214 @@ __device__ uint64_t general_entry_guess(DecodeSmem<DEC_CHUNK>& s, const uint8_t*
     __syncthreads();
     const unsigned long long b1 = s.best, b2 = s.best2;
     __syncthreads();
-    if (b1 != ~0ull) return base + b1;
-    if (b2 != ~0ull) return base + (b2 & 0xFFFFu);
-    return ~0ull;
+    if (b1 == ~0ull) return b2 != ~0ull ? base + (b2 & 0xFFFFu) : ~0ull;
+    const uint32_t p1 = (uint32_t)(b1 >> 32), n1 = (uint32_t)b1;
+    // shortest linking candidate in [p1, n1)
+    unsigned long long best = ~0ull;
+    if (seg0 < n1 && seg0 + SEG > p1) {
+        m = m0;
+        for (uint32_t it = 0; m && it < CAND_CAP; ++it) {
+            const uint32_t b = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const uint32_t p = seg0 + b;
+            if (p < p1 || p >= n1) continue;
+            uint64_t kl, vl;
+            lds_header(data, p, kl, vl);
+            const uint64_t nx = (uint64_t)p + 16 + kl + vl;
+            if (nx < clen && s.sg[nx / SEG] == (uint32_t)nx) {
+                const unsigned long long key = ((16 + kl + vl) << 16) | p;
+                best = key < best ? key : best;
+            }
+        }
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(best, d, 64);
+        best = o < best ? o : best;
+    }
+    if (tid == 0) s.best = ~0ull;
+    __syncthreads();
+    if ((tid & 63) == 0) atomicMin(&s.best, best);
+    __syncthreads();
+    const unsigned long long bb = s.best;
+    __syncthreads();
+    return base + (bb != ~0ull ? (uint32_t)(bb & 0xFFFFu) : p1);
 }
 
-template <uint32_t DEC_CHUNK, bool DIAG>
-__global__ __launch_bounds__(DEC_CHUNK / 64) void decode_kernel(DecodeArgs a) {
-    HG_DEC_GEOM
-    __shared__ DecodeSmem<DEC_CHUNK> s;
-    const uint32_t tid = threadIdx.x;
+// ---- piece staging ------------------------------------------------------------
+// 16 bytes at off (absolute), zero past len; register-only byte assembly at
+// the file tail.
+__device__ __forceinline__ uint4 load16(const DecodeArgs& a, uint64_t off) {
+    if (off + 16 <= a.len) return *reinterpret_cast<const uint4*>(a.sst + off);
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint64_t o = off + q * 4 + b;
+            if (o < a.len) w[q] |= (uint32_t)a.sst[o] << (8 * b);
+        }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void load_piece(const DecodeArgs& a, uint32_t p, uint4 (&v)[GPT]) {
+    const uint64_t base = (uint64_t)p * PIECE;
+#pragma unroll
+    for (uint32_t i = 0; i < GPT; ++i) v[i] = load16(a, base + (i * THREADS + threadIdx.x) * 16);
+}
+
+// All threads: v -> LDS (after the previous piece is done with it), halo, slack.
+__device__ __forceinline__ void stage_piece(DecodeSmem& s, const uint4 (&v)[GPT], uint32_t i) {
     uint8_t* data = reinterpret_cast<uint8_t*>(s.data64);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t q = 0; q < GPT; ++q)
+        *reinterpret_cast<uint4*>(data + (q * THREADS + threadIdx.x) * 16) = v[q];
+    if (threadIdx.x < 4)
+        *reinterpret_cast<uint4*>(data + PIECE + threadIdx.x * 16) =
+            threadIdx.x == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
+    __syncthreads();
+}
+
+// Thread 0 walks at most SHORT_WALK records from X.  True if the piece ends
+// within that budget with every record readable: the starts are then in
+// s.pc[0, s.walk_n) and s.exitk is the exit.  Pieces of a few large records
+// skip the general engine this way.
+__device__ bool short_walk(DecodeSmem& s, const uint8_t* data, uint64_t len, uint64_t base,
+                           uint32_t clen, uint64_t X) {
+    if (threadIdx.x == 0) {
+        uint32_t n = 0;
+        uint64_t cur = X;
+        bool ok = false;
+        for (;;) {
+            if (cur >= base + clen) {
+                ok = true;
+                break;
+            }
+            if (n == SHORT_WALK || cur + 16 > len) break;
+            uint64_t kl, vl;
+            lds_header(data, (uint32_t)(cur - base), kl, vl);
+            if (kl > ~0ull - vl || kl + vl > len - cur - 16 || ((kl >> 32) | (vl >> 32))) break;
+            s.pc[n++] = (uint16_t)(cur - base);
+            cur += 16 + kl + vl;
+        }
+        s.walk_n = n;
+        s.walk_done = ok;
+        s.exitk = cur;
+    }
+    __syncthreads();
+    return s.walk_done;
+}
+
+constexpr uint64_t X_UNKNOWN = ~0ull;
+constexpr int32_t E_NO_GUESS = 100;  // speculative entry guess found nothing
+
+// ---- one piece ------------------------------------------------------------------
+// Path of the piece starting at X (absolute; X_UNKNOWN = guess it first: a
+// record whose header repeats 3 lengths ahead, else the general engine's
+// entry guess).  Stride pieces are summarised (emit_now: also emitted at
+// out[gbase + t]); other pieces are emitted at out[gbase + ...] (the scratch
+// area while the record base is unknown).  Returns HG_OK, E_NO_GUESS, or an
+// error kind with s.err_pos (the failing record) — the records before it are
+// emitted and counted in ps.count.  X is updated to the entry used.
+template <bool DIAG>
+__device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, uint64_t& X,
+                              bool emit_now, bool try_short, hg_span* out, uint64_t cap,
+                              uint64_t gbase, PieceSum& ps, uint64_t& exit, uint32_t& mode) {
+    const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
+    const uint64_t base = (uint64_t)p * PIECE;
+    const uint64_t rem = a.len - base;
+    const uint32_t clen = rem < PIECE ? (uint32_t)rem : PIECE;
+    uint32_t g = NO_GUESS, cnt = 0;
+    Walk w;
+    w.exit = 0;
+    w.cnt = 0;
+    w.dead = true;
+    w.p01 = w.p23 = 0;
+    bool prepared = false;
+    if (X == X_UNKNOWN) {
+        if (threadIdx.x < 64) {
+            const uint32_t f = stride_guess(data, rem, clen, a.hz);
+            if (threadIdx.x == 0) s.walk_n = f;
+        }
+        __syncthreads();
+        const uint32_t f = uni(s.walk_n);
+        if (f != NO_GUESS) {
+            X = base + f;
+        } else {
+            general_prepare<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w);
+            prepared = true;
+            // Park the lane walk in LDS that is free until relax() (keeps the
+            // guess's registers off the walk's): exit -> sx[1], positions ->
+            // bk, count|dead -> tgt; g is s.sg (NO_GUESS when dead).
+            const uint32_t t = threadIdx.x;
+            s.sx[1][t] = w.exit;
+            s.bk[t] = w.p01;
+            s.bk[THREADS + t] = w.p23;
+            s.tgt[t] = (uint8_t)(w.cnt | (w.dead ? 16u : 0u));
+            X = uni(general_entry_guess(s, data, base, clen));
+            g = s.sg[t];
+            w.exit = s.sx[1][t];
+            w.p01 = s.bk[t];
+            w.p23 = s.bk[THREADS + t];
+            w.cnt = s.tgt[t] & 15u;
+            w.dead = (s.tgt[t] & 16u) != 0;
+            if (X == ~0ull) {
+                X = X_UNKNOWN;
+                mode = 0;
+                return E_NO_GUESS;
+            }
+        }
+    }
+    HG_PROF(6);
+    if (!prepared && stride_run(data, base, a.len, clen, X, ps)) {
+        mode = 1;
+        exit = ps.kind == PK_EMPTY ? X : X + ps.count * ps.R;
+        ps.exit = exit;
+        if (emit_now && ps.kind == PK_STRIDE)
+            for (uint32_t t = threadIdx.x; t < ps.count; t += THREADS)
+                if (gbase + t < cap) write_span(out, gbase + t, X + t * ps.R, ps.kl, ps.vl);
+        return HG_OK;
+    }
+    HG_PROF(7);
+    ps.x = X;
+    ps.R = 0;
+    ps.kl = ps.vl = 0;
+    ps.kind = PK_SCRATCH;
+    if (!prepared && try_short && short_walk(s, data, a.len, base, clen, X)) {
+        mode = 4;
+        const uint32_t n = uni(s.walk_n);
+        for (uint32_t t = threadIdx.x; t < n; t += THREADS)
+            store_span(out, cap, gbase + t, data, base, s.pc[t]);
+        ps.count = n;
+        exit = ps.exit = uni(s.exitk);
+        return HG_OK;
+    }
+    if (!prepared) general_prepare<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w);
+    bool dead = false;
+    const bool conv = relax<DIAG>(s, data, base, a.len, clen, X, g, w, cnt, dead);
+    if (conv && !dead) {
+        mode = 2;
+        uint32_t tot;
+        const uint32_t pre = block_excl_scan<NW>(cnt, s.scan_tmp, tot);
+        for (uint32_t i = 0; i < cnt; ++i)
+            store_span(out, cap, gbase + pre + i, data, base, walk_pos(w, i));
+        ps.count = uni(tot);
+        exit = ps.exit = uni(s.exitk);
+        __syncthreads();
+        HG_PROF(5);
+        return HG_OK;
+    }
+    mode = 3;
+    ps.count = uni((uint32_t)serial_walk_emit(s, a.len, base, clen, X, out, cap, gbase));
+    exit = ps.exit = uni(s.exitk);
+    return uni(s.err_kind);
+}
+
+// ---- kernel ------------------------------------------------------------------------
+template <bool DIAG>
+__global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
+    __shared__ DecodeSmem s;
+    const uint32_t tid = threadIdx.x;
     uint64_t t_start = 0;
     uint32_t* dg = nullptr;
 #define HG_STAMP(slot)                                                                      \
@@ -663,241 +860,195 @@ __global__ __launch_bounds__(DEC_CHUNK / 64) void decode_kernel(DecodeArgs a) {
         if (DIAG && tid == 0) dg[slot] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start); \
     } while (0)
 
-    if (tid == 0) s.chunk = atomicAdd(a.ticket, 1u);
+    if (tid == 0) s.batch = atomicAdd(a.ticket, 1u);
     __syncthreads();
-    const uint32_t k = s.chunk;
+    const uint32_t b = s.batch;
+    const uint32_t p0 = b * BATCH;
+    const uint32_t np = min(BATCH, a.npieces - p0);
     if (DIAG) {
         t_start = __builtin_amdgcn_s_memtime();
-        dg = a.diag + (size_t)k * DIAG_WORDS;
+        dg = a.diag + (size_t)b * DIAG_WORDS;
     }
-    const uint64_t base = (uint64_t)k * DEC_CHUNK;
-    const uint64_t rem = a.len - base;  // bytes from chunk start to end of input
-    const uint32_t clen = rem < DEC_CHUNK ? (uint32_t)rem : DEC_CHUNK;
-
-    // ---- 1. stage chunk (+16 B halo) in LDS ------------------------------------
-    const bool full = rem >= (uint64_t)DEC_CHUNK + 16;
-    uint4 v[DEC_GPT];
-#pragma unroll
-    for (uint32_t i = 0; i < DEC_GPT; ++i) {
-        const uint32_t off = (i * DEC_THREADS + tid) * 16;
-        if (full || off + 16 <= rem) {
-            v[i] = *reinterpret_cast<const uint4*>(a.sst + base + off);
-        } else {
-            uint8_t tmp[16];
-#pragma unroll
-            for (int b = 0; b < 16; ++b) tmp[b] = (off + b < rem) ? a.sst[base + off + b] : 0;
-            v[i] = *reinterpret_cast<uint4*>(tmp);
-        }
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < DEC_GPT; ++i)
-        *reinterpret_cast<uint4*>(data + (i * DEC_THREADS + tid) * 16) = v[i];
-    if (tid < 4) {  // halo granule (16 B) + zeroed read slack
-        const uint32_t off = DEC_CHUNK + tid * 16;
-        uint4 h = make_uint4(0, 0, 0, 0);
-        if (tid == 0) {
-            if (full) {
-                h = *reinterpret_cast<const uint4*>(a.sst + base + off);
-            } else {
-                uint8_t tmp[16];
-#pragma unroll
-                for (int b = 0; b < 16; ++b)
-                    tmp[b] = ((uint64_t)off + b < rem) ? a.sst[base + off + b] : 0;
-                h = *reinterpret_cast<uint4*>(tmp);
-            }
-        }
-        *reinterpret_cast<uint4*>(data + off) = h;
-    }
-    if (tid == 0) {  // is the predecessor's exit already published?
-        s.pred_ok = k == 0;
+    uint4 v[GPT];
+    load_piece(a, p0, v);
+    if (tid < np) s.halo[tid] = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
+    if (tid == 0) {  // is the predecessor batch's exit already published?
+        s.pred_ok = b == 0;
         s.pred_exit = 0;
-        if (k > 0) {
-            unsigned long long v0 = ld_agent(&a.status[2 * (k - 1)]);
-            unsigned long long v1 = ld_agent(&a.status[2 * (k - 1) + 1]);
+        if (b > 0) {
+            unsigned long long v0 = ld_agent(&a.status[2 * (b - 1)]);
+            unsigned long long v1 = ld_agent(&a.status[2 * (b - 1) + 1]);
             if (st_flag(v0) == st_flag(v1) && (st_flag(v0) == ST_AGG || st_flag(v0) == ST_INCL)) {
                 s.pred_ok = 1;
                 s.pred_exit = st_val(v0);
             }
         }
     }
+    hg_span* const scratch = a.scratch + (size_t)p0 * MAX_REC_PIECE;
+    const uint64_t bbase = (uint64_t)p0 * PIECE;
+
+    // Pass 0 is speculative (entry guessed, spans to scratch, stride pieces
+    // summarised).  Pass 1 runs only when the guess was wrong or the guessed
+    // path fails: exactly from the looked-back entry, emitting directly, until
+    // a piece's exact exit equals its speculative exit — from there on the
+    // speculative pieces are exact (a piece's path depends only on its entry)
+    // and only their record base moves.
+    uint64_t X0 = X_UNKNOWN, x = X_UNKNOWN, total = 0, gk = 0, xk = 0, errpos = 0, gi = 0;
+    uint64_t gres = 0;  // record index of piece `resume`
+    int32_t kind = HG_OK, perr = HG_OK;
+    bool spec_ok = true, redo = false;
+    uint32_t nstride = 0, ngen = 0, nserial = 0, nshort = 0, resume = 0, nredo = 0;
+    if (DIAG && tid == 0) {
+        for (uint32_t q = 0; q < NPROF; ++q) s.prof[q] = 0;
+        s.plast = __builtin_amdgcn_s_memtime();
+    }
+    uint32_t rounds_acc = 0;
     __syncthreads();
-    HG_STAMP(D_T_LOAD);
-
-    const uint32_t hz = a.hz;
-
-    // ---- 2. entry guess: predecessor's exit, else a stride-consistent head record
-    uint64_t X = ~0ull;
-    bool have = false;
-    if (s.pred_ok) {
-        X = s.pred_exit;
-        have = true;
-    } else {
-        if (tid < 64) {
-            const uint32_t f = stride_guess(s, data, rem, clen, hz);
-            if (tid == 0) s.walk_n = f;
+    if (uni(s.pred_ok)) x = uni(s.pred_exit);
+#pragma nounroll
+    for (uint32_t pass = 0;; ++pass) {
+        gi = gk;
+        uint32_t prev_count = 0;
+        uint32_t i = 0;
+#pragma nounroll
+        for (; i < np; ++i) {
+            if (pass == 1) load_piece(a, p0 + i, v);  // (rare pass: no prefetch, fewer VGPRs)
+            stage_piece(s, v, i);
+            if (pass == 0 && i + 1 < np) load_piece(a, p0 + i + 1, v);  // in flight meanwhile
+            PieceSum ps;
+            uint64_t ex;
+            uint32_t mode = 0;
+            hg_span* out = pass ? a.spans : scratch + (size_t)i * MAX_REC_PIECE;
+            const int32_t e = piece_path<DIAG>(s, a, p0 + i, x, pass == 1, prev_count <= SHORT_WALK,
+                                               out, pass ? a.cap : ~0ull, pass ? gi : 0, ps, ex, mode);
+            if (i == 0 && pass == 0) X0 = x;
+            nstride += mode == 1;
+            ngen += mode == 2;
+            nserial += mode == 3;
+            nshort += mode == 4;
+            if (DIAG && mode == 2) rounds_acc += s.rounds;
+            nredo += pass;
+            prev_count = ps.count;
+            if (e != HG_OK) {
+                if (pass == 0) {  // the guessed path fails: the exact pass reports it
+                    spec_ok = false;
+                } else {
+                    kind = e;
+                    errpos = s.err_pos;
+                    gi += ps.count;
+                }
+                break;
+            }
+            if (pass == 0 && tid == 0) s.sum[i] = ps;
+            gi += ps.count;
+            x = ex;
+            if (pass == 1 && spec_ok && ex == uni(s.sum[i].exit)) {  // re-joined the speculative path
+                ++i;
+                break;
+            }
+        }
+        resume = pass == 0 ? 0 : i;
+        gres = gi;
+        if (pass == 1) {
+            if (kind == HG_OK && spec_ok && resume < np) {
+                for (uint32_t j = resume; j < np; ++j) gi += uni(s.sum[j].count);
+                x = uni(s.sum[np - 1].exit);
+            }
+            total = gi - gk;
+            break;
+        }
+        total = gi;  // gk == 0 in pass 0
+        HG_STAMP(D_T_SPEC);
+        if (spec_ok && tid == 0) {
+            const uint32_t xrel =
+                X0 < bbase + (uint64_t)np * PIECE ? (uint32_t)(X0 - bbase) : NONE_REL;
+            st_agent(&a.status[2 * b + 1], pack_status(ST_AGG, xrel, 0));
+            st_agent(&a.status[2 * b], pack_status(ST_AGG, (uint32_t)total, x));
+        }
+        HG_STAMP(D_T_AGG);
+        if (tid < 64) {  // look-back (wave 0)
+            uint32_t spins = 0;
+            LookbackOut lb = lookback(a, b, spins);
+            if (tid == 0) {
+                s.xk = lb.x;
+                s.gk = lb.g;
+                s.err_kind = lb.err;
+                s.err_pos = lb.errpos;
+                if (DIAG) dg[D_SPINS] = spins;
+            }
         }
         __syncthreads();
-        if (s.walk_n != NO_GUESS) {
-            X = base + s.walk_n;
-            have = true;
-        }
-    }
-
-    // ---- 3. path for the guess: one stride run, else the general engine -------
-    uint64_t gcount = 0, gexit = 0;
-    uint32_t rk = 0, rv = 0;  // stride run's key/value lengths
-    uint64_t rlen = 0;        // stride run's record length
-    bool stride_ok = false, conv = false, any_dead = false, gen_ready = false;
-    uint32_t g = NO_GUESS, cnt = 0, prefix = 0, rounds = 0, rounds2 = 0, mode = 0;
-    Walk w;
-    w.exit = 0;
-    w.cnt = 0;
-    w.dead = true;
-    w.p0 = w.p1 = w.p2 = w.p3 = 0;
-    if (have) stride_ok = stride_run(s, data, base, a.len, clen, X, gcount, gexit, rlen, rk, rv);
-    if (!stride_ok) {
-        general_prepare(s, data, base, a.len, rem, clen, hz, g, w);
-        gen_ready = true;
-        if (!have) {
-            X = general_entry_guess(s, data, base, clen, g);
-            have = X != ~0ull;
-        }
-        if (have) {
-            conv = relax(s, data, base, a.len, clen, X, g, w, cnt, any_dead, rounds);
-            uint32_t tot;
-            prefix = block_excl_scan<DEC_NW>(cnt, s.scan_tmp, tot);
-            gcount = tot;
-            gexit = X >= base + clen ? X : s.exitk;
-            if (!conv) {  // still publish an AGG so successors are not serialised behind us
-                bool dead = false;
-                serial_count(s, a, base, clen, X, gcount, gexit, dead);
-                any_dead = dead;
-            }
-            if (any_dead) have = false;
-        }
-    }
-    HG_STAMP(D_T_RES);
-    if (have && tid == 0) {
-        const uint32_t xrel = X < base + clen ? (uint32_t)(X - base) : NONE_REL;
-        st_agent(&a.status[2 * k + 1], pack_status(ST_AGG, xrel, 0));
-        st_agent(&a.status[2 * k], pack_status(ST_AGG, (uint32_t)gcount, gexit));
-    }
-    HG_STAMP(D_T_AGG);
-
-    // ---- 4. look-back (wave 0) ----------------------------------------------------
-    if (tid < 64) {
-        uint32_t spins = 0;
-        LookbackOut lb = lookback<DEC_CHUNK>(a, k, spins);
-        if (tid == 0) {
-            s.xk = lb.x;
-            s.gk = lb.g;
-            s.err_kind = lb.err;
-            s.err_pos = lb.errpos;
-            if (DIAG) dg[D_SPINS] = spins;
-        }
-    }
-    __syncthreads();
-    HG_STAMP(D_T_LB);
-
-    const int32_t perr = s.err_kind;
-    const uint64_t xk = s.xk, gk = s.gk;
-    int32_t kind = HG_OK;
-    uint64_t errpos = 0, count = 0, exitk = 0;
-    if (perr != HG_OK) {  // an earlier chunk failed: propagate, emit nothing
-        kind = perr;
-        errpos = s.err_pos;
-    } else {
-        // ---- 5. exact path from X_k -------------------------------------------------
-        // mode 1: stride run, 2: relaxed lanes, 3: serial walk
-        if (have && xk == X && stride_ok) {
-            mode = 1;
-        } else if (have && xk == X && conv) {
-            mode = 2;
-        } else {
-            stride_ok = stride_run(s, data, base, a.len, clen, xk, gcount, gexit, rlen, rk, rv);
-            if (stride_ok) {
-                mode = 1;
-            } else {
-                if (!gen_ready) general_prepare(s, data, base, a.len, rem, clen, hz, g, w);
-                any_dead = false;
-                conv = relax(s, data, base, a.len, clen, xk, g, w, cnt, any_dead, rounds2);
-                uint32_t tot;
-                prefix = block_excl_scan<DEC_NW>(cnt, s.scan_tmp, tot);
-                gcount = tot;
-                gexit = xk >= base + clen ? xk : s.exitk;
-                mode = (conv && !any_dead) ? 2 : 3;
-            }
-        }
-        if (mode != 3) {
-            count = gcount;
-            exitk = gexit;
-            if (tid == 0) {
-                st_agent(&a.status[2 * k + 1],
-                         pack_status(ST_INCL, xk < base + clen ? (uint32_t)(xk - base) : NONE_REL,
-                                     gk + count));
-                st_agent(&a.status[2 * k], pack_status(ST_INCL, (uint32_t)count, exitk));
-            }
-        }
-        // ---- 6. emission ------------------------------------------------------------
-        if (mode == 1) {  // arithmetic: record t starts at X_k + t*R
-            for (uint32_t t = tid; t < count; t += DEC_THREADS) {
-                const uint64_t gi = gk + t;
-                if (gi < a.cap) {
-                    const uint64_t off = xk + (uint64_t)t * rlen;
-                    uint4 sp;
-                    sp.x = (uint32_t)off;
-                    sp.y = (uint32_t)(off >> 32);
-                    sp.z = rk;
-                    sp.w = rv;
-                    *reinterpret_cast<uint4*>(a.spans + gi) = sp;
-                }
-            }
-        } else if (mode == 2) {  // straight from the lane walks
-            const uint64_t gi = gk + prefix;
-            if (cnt > 0) store_span(a.spans, a.cap, gi, data, base, w.p0);
-            if (cnt > 1) store_span(a.spans, a.cap, gi + 1, data, base, w.p1);
-            if (cnt > 2) store_span(a.spans, a.cap, gi + 2, data, base, w.p2);
-            if (cnt > 3) store_span(a.spans, a.cap, gi + 3, data, base, w.p3);
-        } else {
-            serial_walk_emit(s, a, base, clen, xk, gk);
-            count = s.x_count;
-            kind = s.err_kind;
+        HG_STAMP(D_T_LB);
+        perr = uni(s.err_kind);
+        xk = uni(s.xk);
+        gk = uni(s.gk);
+        if (perr != HG_OK) {  // an earlier batch failed: propagate, emit nothing
+            kind = perr;
             errpos = s.err_pos;
-            exitk = s.exitk;
-            if (tid == 0) {
-                if (kind == HG_OK) {
-                    st_agent(&a.status[2 * k + 1],
-                             pack_status(ST_INCL,
-                                         xk < base + clen ? (uint32_t)(xk - base) : NONE_REL,
-                                         gk + count));
-                    st_agent(&a.status[2 * k], pack_status(ST_INCL, (uint32_t)count, exitk));
-                } else {
-                    st_agent(&a.status[2 * k + 1], pack_status(ST_ERR, 0, gk + count));
-                    st_agent(&a.status[2 * k],
-                             pack_status(ST_ERR, (uint32_t)(kind + 16), errpos));
-                }
-            }
+            total = 0;
+            resume = np;
+            break;
+        }
+        if (spec_ok && xk == X0) {
+            gres = gk;
+            break;
+        }
+        redo = true;
+        x = xk;
+    }
+    // ---- publish, then emit the speculative pieces from `resume` on -------------------
+    if (tid == 0) {
+        if (kind == HG_OK) {
+            st_agent(&a.status[2 * b + 1], pack_status(ST_INCL, 0, gk + total));
+            st_agent(&a.status[2 * b], pack_status(ST_INCL, (uint32_t)total, x));
+        } else {
+            st_agent(&a.status[2 * b + 1], pack_status(ST_ERR, 0, gk + total));
+            st_agent(&a.status[2 * b], pack_status(ST_ERR, (uint32_t)(kind + 16), errpos));
         }
     }
-    if (perr != HG_OK && tid == 0) {
-        st_agent(&a.status[2 * k + 1], pack_status(ST_ERR, 0, gk));
-        st_agent(&a.status[2 * k], pack_status(ST_ERR, (uint32_t)(kind + 16), errpos));
+    if (kind == HG_OK && spec_ok) {
+        uint64_t go = gres;
+        for (uint32_t i = resume; i < np; ++i) {
+            PieceSum ps = s.sum[i];
+            ps.x = uni(ps.x);
+            ps.R = uni(ps.R);
+            ps.kl = uni(ps.kl);
+            ps.vl = uni(ps.vl);
+            ps.count = uni(ps.count);
+            ps.kind = uni(ps.kind);
+            if (ps.kind == PK_STRIDE) {
+                for (uint32_t t = tid; t < ps.count; t += THREADS)
+                    if (go + t < a.cap) write_span(a.spans, go + t, ps.x + t * ps.R, ps.kl, ps.vl);
+            } else if (ps.kind == PK_SCRATCH) {
+                const hg_span* src = scratch + (size_t)i * MAX_REC_PIECE;
+                for (uint32_t t = tid; t < ps.count; t += THREADS)
+                    if (go + t < a.cap)
+                        *reinterpret_cast<uint4*>(a.spans + go + t) =
+                            *reinterpret_cast<const uint4*>(src + t);
+            }
+            go += ps.count;
+        }
     }
     HG_STAMP(D_T_END);
     if (DIAG && tid == 0) {
-        dg[D_T_SPEC] = mode;
-        dg[D_ROUNDS] = rounds;
-        dg[D_ROUNDS2] = rounds2;
-        dg[D_GUESS] = (have ? 1u : 0u) | (s.pred_ok ? 2u : 0u) | ((have && xk == X) ? 4u : 0u);
-        dg[D_COUNT] = (uint32_t)count;
-        dg[D_FLAGS] = (perr != HG_OK ? 2u : 0u) | (kind != HG_OK ? 4u : 0u) |
-                      (gen_ready ? 8u : 0u);
+        dg[D_NSTRIDE] = nstride;
+        dg[D_NGEN] = ngen;
+        dg[D_NSERIAL] = nserial;
+        dg[D_GUESS] = (X0 != X_UNKNOWN ? 1u : 0u) | (s.pred_ok ? 2u : 0u) | ((xk == X0) ? 4u : 0u);
+        dg[D_COUNT] = (uint32_t)total;
+        dg[D_FLAGS] = (perr != HG_OK ? 2u : 0u) | (kind != HG_OK ? 4u : 0u) | (spec_ok ? 8u : 0u);
+        dg[D_REDO] = redo ? 1u + nredo : 0u;
+        dg[D_C_PREP] = s.prof[0] + s.prof[1] + s.prof[2];
+        dg[D_C_RELAX] = s.prof[3] + s.prof[4];
+        for (uint32_t q = 0; q < NPROF; ++q) dg[16 + q] = s.prof[q];
+        dg[D_ROUNDS] = rounds_acc;
+        dg[D_NSHORT] = nshort;
     }
 #undef HG_STAMP
-    // ---- 7. the last chunk reports the whole-file result ----------------------
-    if (tid == 0 && k == a.nchunks - 1) {
+    // ---- the last batch reports the whole-file result --------------------------------
+    if (tid == 0 && b == a.nbatches - 1) {
         hg_decode_result r;
-        r.n_records = gk + count;
+        r.n_records = gk + total;
         r.kind = kind;
         r.reserved = 0;
         r.err_offset = kind != HG_OK ? errpos : 0;
@@ -907,16 +1058,32 @@ __global__ __launch_bounds__(DEC_CHUNK / 64) void decode_kernel(DecodeArgs a) {
 
 }  // namespace hgk
 
-// d_status must hold hgk_decode_workspace_bytes(len) bytes; the launcher
-// zeroes the statuses and the ticket word that follows them.  chunk selects
-// the geometry (4096, 8192 or 16384 bytes per workgroup).
-extern "C" int hgk_decode_launch_variant(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
-                                         uint64_t cap, hg_decode_result* d_result,
-                                         unsigned long long* d_status, uint32_t* d_diag,
-                                         uint32_t chunk, hipStream_t stream) {
+namespace {
+struct DecodeLayout {
+    uint64_t npieces, nbatches, status_words, scratch_off, bytes;
+};
+DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
-    if (chunk != 4096 && chunk != 8192 && chunk != 16384) return HG_ERR_INVALID_ARG;
-    const uint64_t nch = (len + chunk - 1) / chunk;
+    DecodeLayout l;
+    l.npieces = (len + PIECE - 1) / PIECE;
+    l.nbatches = (l.npieces + BATCH - 1) / BATCH;
+    l.status_words = 2 * l.nbatches + 2;  // + ticket
+    l.scratch_off = (l.status_words * 8 + 255) & ~255ull;
+    l.bytes = l.scratch_off + l.nbatches * BATCH * MAX_REC_PIECE * sizeof(hg_span);
+    return l;
+}
+}  // namespace
+
+extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) { return decode_layout(len).bytes; }
+
+// d_ws must hold hgk_decode_workspace_bytes(len) bytes.  The launcher zeroes
+// the statuses and the ticket (the scratch area needs no initialisation).
+// len == 0 is handled by the caller (no launch).
+extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
+                                      uint64_t cap, hg_decode_result* d_result, void* d_ws,
+                                      uint32_t* d_diag, hipStream_t stream) {
+    using namespace hgk;
+    const DecodeLayout l = decode_layout(len);
     // Zero high bytes every genuine length field must have: any record fits
     // in len bytes, so klen, vlen < 2^(8*nb) with nb = bytes needed for len.
     uint32_t nb = 0;
@@ -927,54 +1094,23 @@ extern "C" int hgk_decode_launch_variant(const uint8_t* d_sst, uint64_t len, hg_
     a.spans = d_spans;
     a.cap = cap;
     a.result = d_result;
-    a.status = d_status;
-    a.ticket = reinterpret_cast<uint32_t*>(d_status + 2 * nch);
-    a.nchunks = (uint32_t)nch;
+    a.status = static_cast<unsigned long long*>(d_ws);
+    a.ticket = reinterpret_cast<uint32_t*>(a.status + 2 * l.nbatches);
+    a.scratch = reinterpret_cast<hg_span*>(static_cast<char*>(d_ws) + l.scratch_off);
+    a.nbatches = (uint32_t)l.nbatches;
+    a.npieces = (uint32_t)l.npieces;
     a.hz = 8 - nb;
     a.diag = d_diag;
-    hipError_t e = hipMemsetAsync(d_status, 0, (size_t)(2 * nch + 2) * sizeof(unsigned long long),
-                                  stream);
-    if (e != hipSuccess) return HG_ERR_HIP;
-    const dim3 grid((uint32_t)nch);
-#define HG_LAUNCH(C)                                                                          \
-    if (chunk == C) {                                                                         \
-        if (d_diag)                                                                           \
-            hipLaunchKernelGGL((decode_kernel<C, true>), grid, dim3(C / 64), 0, stream, a);   \
-        else                                                                                  \
-            hipLaunchKernelGGL((decode_kernel<C, false>), grid, dim3(C / 64), 0, stream, a);  \
-    }
-    HG_LAUNCH(4096)
-    HG_LAUNCH(8192)
-    HG_LAUNCH(16384)
-#undef HG_LAUNCH
+    if (hipMemsetAsync(d_ws, 0, l.status_words * 8, stream) != hipSuccess) return HG_ERR_HIP;
+    if (d_diag)
+        hipLaunchKernelGGL(decode_kernel<true>, dim3(a.nbatches), dim3(THREADS), 0, stream, a);
+    else
+        hipLaunchKernelGGL(decode_kernel<false>, dim3(a.nbatches), dim3(THREADS), 0, stream, a);
     return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
-static uint32_t default_chunk() {
-    static uint32_t c = 0;
-    if (!c) {
-        const char* e = getenv("HG_DECODE_CHUNK");
-        c = e ? (uint32_t)atoi(e) : 16384u;
-        if (c != 4096 && c != 8192 && c != 16384) c = 16384;
-    }
-    return c;
-}
-
-extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
-                                      uint64_t cap, hg_decode_result* d_result,
-                                      unsigned long long* d_status, uint32_t* d_diag,
-                                      hipStream_t stream) {
-    return hgk_decode_launch_variant(d_sst, len, d_spans, cap, d_result, d_status, d_diag,
-                                     default_chunk(), stream);
-}
-
 extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
-                                 uint64_t cap, hg_decode_result* d_result,
-                                 unsigned long long* d_status, hipStream_t stream) {
-    return hgk_decode_launch_diag(d_sst, len, d_spans, cap, d_result, d_status, nullptr, stream);
-}
-
-extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) {
-    const uint64_t nch = (len + hgk::DEC_CHUNK_MIN - 1) / hgk::DEC_CHUNK_MIN;
-    return (2 * nch + 2) * sizeof(unsigned long long);
+                                 uint64_t cap, hg_decode_result* d_result, void* d_ws,
+                                 hipStream_t stream) {
+    return hgk_decode_launch_diag(d_sst, len, d_spans, cap, d_result, d_ws, nullptr, stream);
 }

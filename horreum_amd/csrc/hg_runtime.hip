@@ -11,7 +11,7 @@
 #include "../../include/horreum_gpu.h"
 
 extern "C" int hgk_decode_launch(const uint8_t*, uint64_t, hg_span*, uint64_t, hg_decode_result*,
-                                 unsigned long long*, hipStream_t);
+                                 void*, hipStream_t);
 extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t);
 extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
                                  uint64_t*, uint32_t, hg_block*, hg_encode_result*,
@@ -183,8 +183,7 @@ int hg_decode_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* 
                    : HG_ERR_HIP;
     int r = ensure(c, c->ws, hgk_decode_workspace_bytes(len));
     if (r != HG_OK) return r;
-    return hgk_decode_launch(d_sst, len, d_spans, cap, d_result,
-                             reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+    return hgk_decode_launch(d_sst, len, d_spans, cap, d_result, c->ws.p, c->stream);
 }
 
 static int finish_decode(const hg_decode_result& res, uint64_t cap, uint64_t* n_out,

@@ -10,7 +10,8 @@ from tests import corpus
 
 pytestmark = pytest.mark.gpu
 
-CHUNK = 16384
+CHUNK = 16384          # bytes per piece staged in LDS
+BATCH = 8 * CHUNK      # bytes per workgroup ticket / look-back status
 
 
 def gpu_decode(engine, data, cap=None):
@@ -113,6 +114,53 @@ def test_capacity(engine):
         gs, gn, gk, go = gpu_decode(engine, data, cap)
         assert (gn, gk, go) == (wn, wk, wo) and rc == 5
         assert np.array_equal(gs, ws)
+
+
+def test_batch_edges(engine):
+    """Cuts at look-back batch edges (128 KiB) and piece edges inside a batch."""
+    arena, pairs = corpus.mixed(20000, 24, 96, seed=5)
+    data, _, _, _ = oracle.encode(arena, pairs)
+    assert data.size > 4 * BATCH
+    cuts = set()
+    for k in range(1, data.size // BATCH + 1):
+        for d in (-17, -1, 0, 1, 16):
+            cuts.add(k * BATCH + d)
+    for k in (1, 3, 7, 9, 15):
+        for d in (-1, 0, 9):
+            cuts.add(k * CHUNK + d)
+    for cut in sorted(c for c in cuts if 0 < c < data.size):
+        assert_same(engine, data[:cut])
+
+
+def _fake_header_table(n, fake_at, fake_k, fake_v, seed):
+    """16 B keys / 100 B values whose value bytes carry a plausible header
+    (fake_k, fake_v) at value offset fake_at: a position whose header repeats
+    one record length ahead, so entry guesses can lock onto the wrong phase."""
+    rng = np.random.default_rng(seed)
+    kl = np.full(n, 16, np.int64)
+    vl = np.full(n, 100, np.int64)
+    arena = rng.integers(0, 256, size=n * 116, dtype=np.uint8).reshape(n, 116)
+    fake = np.frombuffer(int(fake_k).to_bytes(8, "little") + int(fake_v).to_bytes(8, "little"),
+                         np.uint8)
+    arena[:, 16 + fake_at:16 + fake_at + 16] = fake
+    arena = arena.reshape(-1)
+    pairs = np.zeros(n, dtype=oracle.PAIR_DTYPE)
+    pairs["key_off"] = np.arange(n) * 116
+    pairs["val_off"] = np.arange(n) * 116 + 16
+    pairs["klen"] = kl
+    pairs["vlen"] = vl
+    data, _, _, _ = oracle.encode(arena, pairs)
+    return data
+
+
+@pytest.mark.parametrize("fake", [(10, 4, 96), (40, 0, 100), (2, 50, 50), (60, 1, 3)])
+def test_fake_headers_in_values(engine, fake):
+    """Adversarial phase: every record carries a self-consistent fake header.
+    Wrong batch guesses must be redone exactly from the looked-back entry."""
+    data = _fake_header_table(60000, *fake, seed=11)
+    assert_same(engine, data)
+    for cut in (BATCH * 3 + 5, BATCH * 17 - 1, data.size - 7):
+        assert_same(engine, data[:cut])
 
 
 def test_many_chunks_mixed(engine):

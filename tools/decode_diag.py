@@ -21,8 +21,11 @@ import torch  # noqa: E402
 from horreum_amd import abi, synth  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
 
-NAMES = ["t_load", "mode", "t_res", "t_agg", "t_lb", "t_end", "rounds", "rounds2", "guess",
-         "spins", "count", "flags"]
+NAMES = ["t_spec", "t_agg", "t_lb", "t_end", "n_stride", "n_general", "n_serial", "guess",
+         "spins", "count", "flags", "redo", "c_prep", "c_relax", "rounds", "n_short",
+         "p_filter", "p_cand", "p_walk", "p_seed", "p_rounds", "p_emit", "p_stage", "p_stride"]
+W = len(NAMES)
+BATCH_BYTES = 8 * 16384
 
 
 def run(eng, sst, L, label):
@@ -32,13 +35,14 @@ def run(eng, sst, L, label):
                                            ctypes.c_void_p, ctypes.c_void_p]
     lib.hgk_decode_workspace_bytes.argtypes = [ctypes.c_uint64]
     lib.hgk_decode_workspace_bytes.restype = ctypes.c_uint64
-    nch = (L + 16383) // 16384
+    nch = (L + BATCH_BYTES - 1) // BATCH_BYTES
     ws = torch.zeros(int(lib.hgk_decode_workspace_bytes(L)), dtype=torch.uint8, device=eng.device)
     cap = L // 16
     spans = eng.empty(cap * 16)
     res = eng.empty(64)
-    diag = torch.zeros(nch * 12, dtype=torch.int32, device=eng.device)
+    diag = torch.zeros(nch * W, dtype=torch.int32, device=eng.device)
     stream = torch.cuda.current_stream(eng.device).cuda_stream
+    eng.set_stream(torch.cuda.current_stream(eng.device))
     out = {}
     for mode in ("plain", "diag"):
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -57,21 +61,20 @@ def run(eng, sst, L, label):
     r = res[:24].cpu().numpy()
     out["n"] = int(r[:8].view("<u8")[0])
     out["kind"] = int(r[8:12].view("<i4")[0])
-    d = diag.cpu().numpy().astype(np.uint32).reshape(nch, 12)
+    d = diag.cpu().numpy().astype(np.uint32).reshape(nch, W)
     stats = {}
     for i, nm in enumerate(NAMES):
         col = d[:, i].astype(np.float64)
         stats[nm] = {"p10": float(np.percentile(col, 10)), "p50": float(np.median(col)),
                      "p90": float(np.percentile(col, 90)), "max": float(col.max())}
-    g = d[:, 8]
+    g = d[:, 7]
     out["guess_have"] = float(((g & 1) != 0).mean())
     out["guess_from_pred"] = float(((g & 2) != 0).mean())
     out["guess_ok"] = float(((g & 4) != 0).mean())
-    mode = d[:, 1]
-    out["mode_stride"] = float((mode == 1).mean())
-    out["mode_relax"] = float((mode == 2).mean())
-    out["mode_serial"] = float((mode == 3).mean())
-    out["general_used"] = float(((d[:, 11] & 8) != 0).mean())
+    out["spec_ok"] = float(((d[:, 10] & 8) != 0).mean())
+    out["redo"] = float((d[:, 11] != 0).mean())
+    pieces = d[:, [4, 5, 6, 15]].sum(axis=0).astype(np.float64)
+    out["pieces_stride_general_serial_short"] = (pieces / max(pieces.sum(), 1)).round(4).tolist()
     out["stats"] = stats
     out["label"] = label
     print(json.dumps(out), flush=True)

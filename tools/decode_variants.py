@@ -1,10 +1,9 @@
 #!/usr/bin/env python3
-"""A/B the decode kernel geometries (bytes per workgroup) in one process.
+"""Time the decode kernel on three workload shapes in one process.
 
-For each workload, every variant is run interleaved (rounds x variants) and
-the median launch time is reported, with a parity check of every run's
-result against the 16 KiB variant's spans (bit-exact)."""
-import ctypes
+cfg2 (fixed 16 B / 100 B records, 1 GiB), mixed 16 B / 8..4096 B values and
+small mixed records.  Median launch time over 7 timed launches; every run's
+spans are checked bit-exact against the oracle (test infrastructure)."""
 import json
 import os
 import sys
@@ -15,10 +14,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 
-from horreum_amd import abi, synth  # noqa: E402
+from horreum_amd import synth  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
-
-VARIANTS = [4096, 8192, 16384]
+from oracle import oracle  # noqa: E402
 
 
 def workloads(dev):
@@ -39,50 +37,35 @@ def workloads(dev):
 
 
 def main():
-    lib = abi.load_library()
-    f = lib.hgk_decode_launch_variant
-    f.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
-                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
-                  ctypes.c_void_p]
-    lib.hgk_decode_workspace_bytes.argtypes = [ctypes.c_uint64]
-    lib.hgk_decode_workspace_bytes.restype = ctypes.c_uint64
     eng = Engine(0)
-    stream = torch.cuda.current_stream(eng.device).cuda_stream
+    eng.set_stream(torch.cuda.current_stream(eng.device))
     for label, sst in workloads(eng.device):
         L = sst.numel()
         cap = L // 16
-        ws = torch.zeros(int(lib.hgk_decode_workspace_bytes(L)), dtype=torch.uint8,
-                         device=eng.device)
-        spans = {c: eng.empty(cap * 16) for c in VARIANTS}
-        res = {c: eng.empty(64) for c in VARIANTS}
-        times = {c: [] for c in VARIANTS}
+        spans = eng.empty(cap * 16)
+        res = eng.empty(64)
+        eng.reserve(L, 0)
+        times = []
         for rnd in range(8):
-            for c in VARIANTS:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                e0.record()
-                rc = f(ctypes.c_void_p(sst.data_ptr()), L, ctypes.c_void_p(spans[c].data_ptr()),
-                       cap, ctypes.c_void_p(res[c].data_ptr()), ctypes.c_void_p(ws.data_ptr()),
-                       None, c, ctypes.c_void_p(stream))
-                e1.record()
-                torch.cuda.synchronize()
-                assert rc == 0
-                if rnd > 0:
-                    times[c].append(e0.elapsed_time(e1))
-        out = {"workload": label, "bytes": L}
-        ref = None
-        for c in VARIANTS[::-1]:
-            r = res[c][:24].cpu().numpy()
-            n = int(r[:8].view("<u8")[0])
-            kind = int(r[8:12].view("<i4")[0])
-            sp = spans[c][: n * 16]
-            if ref is None:
-                ref = (n, kind, sp)
-            same = (n, kind) == ref[:2] and torch.equal(sp, ref[2])
-            ms = float(np.median(times[c]))
-            out[str(c)] = {"ms": round(ms, 4), "GBps": round(L / ms / 1e6, 1), "n": n,
-                           "kind": kind, "same_as_16k": bool(same)}
-        print(json.dumps(out), flush=True)
-        del sst, spans
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            eng.decode_dev_async(sst, L, spans, cap, res)
+            e1.record()
+            torch.cuda.synchronize()
+            if rnd > 0:
+                times.append(e0.elapsed_time(e1))
+        r = res[:24].cpu().numpy()
+        n = int(r[:8].view("<u8")[0])
+        kind = int(r[8:12].view("<i4")[0])
+        host = sst.cpu().numpy()
+        want, wn, wkind, _, _ = oracle.decode(host)
+        got = spans[: n * 16].cpu().numpy().view(oracle.SPAN_DTYPE)
+        ok = kind == wkind and n == wn and np.array_equal(got, want)
+        ms = float(np.median(times))
+        print(json.dumps({"workload": label, "bytes": L, "records": n, "ms": round(ms, 4),
+                          "GBps_alg": round((L + 16 * n) / ms / 1e6, 1), "parity": bool(ok)}),
+              flush=True)
+        del spans, sst
 
 
 if __name__ == "__main__":

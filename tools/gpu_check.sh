@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round GPU check: parity tests (every decode geometry), variants A/B, bench.
+# Round GPU check: parity tests, decode workload timings, diagnostics, bench.
 # Every GPU step has its own time limit; a fault/timeout (rc >= 124) stops.
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
@@ -11,9 +11,7 @@ step() {  # step <name> <seconds> <cmd...>
   if [ $rc -ge 124 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
   return 0
 }
-for c in ${CHUNKS:-16384}; do
-  HG_DECODE_CHUNK=$c TAILN=4 step pytest_gpu_$c 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
-done
+TAILN=4 step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
 [ -n "$VARIANTS" ] && step variants 400 python tools/decode_variants.py
 [ -n "$DIAG" ] && step diag 300 python tools/decode_diag.py
 step bench 400 python bench.py --steps 20 --warmup 5 --cpu-sample-mb 256
