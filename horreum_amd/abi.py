@@ -12,7 +12,7 @@ import re
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libhorreum_gpu.so")
+LIB_PATH = os.environ.get("HG_LIBRARY") or os.path.join(PKG_DIR, "libhorreum_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_DIR), "include", "horreum_gpu.h")
 
 

@@ -7,9 +7,9 @@
 // is one long dependency chain with no sync points on disk
 // (src/sstable/storage.rs:31-32).  Here it becomes a single pass over HBM.
 //
-// Work unit = a BATCH of PIECES (8 x 16 KiB), one 256-thread workgroup, taken
+// Work unit = a BATCH of PIECES (16..64 x 16 KiB), one 256-thread workgroup, taken
 // by one atomic ticket (so batch b-1 is always already running: the look-back
-// cannot deadlock; one returning atomic per 128 KiB keeps the ticket far from
+// cannot deadlock; one returning atomic per >= 256 KiB keeps the ticket far from
 // its ~88/us limit).  Per batch:
 //  1. Entry guess for piece 0: the predecessor batch's published exit if it is
 //     out, else a record whose 16-byte header repeats 3 lengths ahead, else
@@ -50,8 +50,12 @@ constexpr uint32_t NW = THREADS / 64;
 constexpr uint32_t SEG = PIECE / THREADS;         // 64
 constexpr uint32_t NGRAN = PIECE / 16;            // 1024 granules of 16 B
 constexpr uint32_t GPT = NGRAN / THREADS;         // 4 granules per thread
-constexpr uint32_t BATCH = 8;                     // pieces per ticket / status
-constexpr uint64_t BATCH_BYTES = (uint64_t)PIECE * BATCH;
+// Pieces per batch (ticket / look-back status) are chosen per launch: enough
+// that the batches fill the resident grid in about one round (each batch pays
+// one look-back and emission tail, during which its workgroup has no loads in
+// flight), between BATCH_MIN and BATCH (the LDS arrays' size).
+constexpr uint32_t BATCH = 64;
+constexpr uint32_t BATCH_MIN = 16;
 constexpr uint32_t MAX_REC_PIECE = PIECE / 16;    // records per piece (>= 16 B each)
 constexpr uint32_t WALK_LOG = PIECE / 16;         // serial-walk batch
 constexpr uint32_t MAX_ROUNDS = 24;
@@ -75,7 +79,30 @@ struct DecodeArgs {
     uint32_t nbatches;
     uint32_t npieces;
     uint32_t hz;                 // zero high bytes required in klen/vlen
+    uint32_t bp;                 // pieces per batch (BATCH_MIN..BATCH)
     uint32_t* diag;              // DIAG builds only: DIAG_WORDS per batch
+    // Stride pre-pass results (decode_spec/scan kernels): batches of SPEC_BP
+    // pieces [0, *first_bad) are resolved and emitted already.
+    const struct SpecBatch* sbatch;
+    const uint32_t* first_bad;
+    uint32_t nspec;              // stride pre-pass batches
+    uint32_t sbp;                // pieces per pre-pass batch (SPEC_BP_MIN..SPEC_BP)
+    uint32_t q;                  // pre-pass batches per general batch (bp / sbp)
+};
+
+// ---- stride pre-pass records --------------------------------------------------------
+constexpr uint32_t SPEC_BP = 64;      // most pieces per pre-pass batch (LDS halo array)
+constexpr uint32_t SPEC_BP_MIN = 4;
+struct SpecBatch {                // one per pre-pass batch
+    uint64_t x0;                  // guessed entry (absolute)
+    uint64_t exit;                // first record start at or after the batch end
+    uint32_t count;               // records starting in the batch
+    uint32_t ok;                  // every piece verified as a stride run from x0
+    uint64_t gbase;               // record index of x0 (scan; valid below first_bad)
+};
+struct SpecPiece {                // one per piece of an ok pre-pass batch
+    uint64_t x, R;
+    uint32_t kl, vl, count, pad;
 };
 
 // Diagnostic record per batch (tools/decode_diag.py).
@@ -349,7 +376,7 @@ restart:
         }
         // AGG lanes: predicted incoming exit must equal the older neighbour's exit.
         const uint32_t xrel = st_aux(w1);
-        const uint64_t P = (xrel != NONE_REL) ? (uint64_t)j * BATCH_BYTES + xrel : E;
+        const uint64_t P = (xrel != NONE_REL) ? (uint64_t)j * a.bp * PIECE + xrel : E;
         const uint64_t Eolder = __shfl_down(E, 1, 64);
         const int lim = fi < 64 ? fi : 63;  // lanes [0, lim) are checked
         const bool bad = (int)lane < lim && P != Eolder;
@@ -696,8 +723,14 @@ __device__ __forceinline__ uint4 load16(const DecodeArgs& a, uint64_t off) {
 
 __device__ __forceinline__ void load_piece(const DecodeArgs& a, uint32_t p, uint4 (&v)[GPT]) {
     const uint64_t base = (uint64_t)p * PIECE;
+    if (base + PIECE <= a.len) {  // uniform: plain 16-byte loads, no per-lane branch
+        const uint4* src = reinterpret_cast<const uint4*>(a.sst + base) + threadIdx.x;
 #pragma unroll
-    for (uint32_t i = 0; i < GPT; ++i) v[i] = load16(a, base + (i * THREADS + threadIdx.x) * 16);
+        for (uint32_t i = 0; i < GPT; ++i) v[i] = src[i * THREADS];
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < GPT; ++i) v[i] = load16(a, base + (i * THREADS + threadIdx.x) * 16);
+    }
 }
 
 // All threads: v -> LDS (after the previous piece is done with it), halo, slack.
@@ -860,11 +893,25 @@ __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
         if (DIAG && tid == 0) dg[slot] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start); \
     } while (0)
 
+    const uint32_t fb = *a.first_bad;
+    if (fb >= a.nspec) return;  // the stride pre-pass resolved the whole file
     if (tid == 0) s.batch = atomicAdd(a.ticket, 1u);
     __syncthreads();
+    if (min((s.batch + 1) * a.q, a.nspec) <= fb) {
+        // Resolved and emitted by the pre-pass: publish its INCL and stop.
+        if (tid == 0) {
+            const SpecBatch& sb = a.sbatch[min((s.batch + 1) * a.q, a.nspec) - 1];
+            const uint32_t b0 = s.batch;
+            const uint64_t gend = sb.gbase + sb.count;
+            const uint64_t g0 = a.sbatch[b0 * a.q].gbase;
+            st_agent(&a.status[2 * b0 + 1], pack_status(ST_INCL, 0, gend));
+            st_agent(&a.status[2 * b0], pack_status(ST_INCL, (uint32_t)(gend - g0), sb.exit));
+        }
+        return;
+    }
     const uint32_t b = s.batch;
-    const uint32_t p0 = b * BATCH;
-    const uint32_t np = min(BATCH, a.npieces - p0);
+    const uint32_t p0 = b * a.bp;
+    const uint32_t np = min(a.bp, a.npieces - p0);
     if (DIAG) {
         t_start = __builtin_amdgcn_s_memtime();
         dg = a.diag + (size_t)b * DIAG_WORDS;
@@ -1056,25 +1103,287 @@ __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
     }
 }
 
+// ---- stride pre-pass ---------------------------------------------------------------
+// decode_spec_kernel: one workgroup per SPEC_BP pieces, no inter-workgroup
+// communication: guesses the batch entry (stride_guess), verifies every piece
+// as a stride run from the previous piece's exit and records per-piece
+// summaries.  Pure streaming (register prefetch of the next piece).  A batch
+// that is not one verified chain of stride runs is left to decode_kernel.
+struct SpecSmem {
+    uint64_t data64[(PIECE + 64) / 8];
+    uint4 halo[SPEC_BP];
+    uint32_t guess;
+};
+
+__global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
+                                                              SpecPiece* sp) {
+    __shared__ SpecSmem s;
+    const uint32_t tid = threadIdx.x;
+    const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
+    const uint32_t b = blockIdx.x;
+    const uint32_t p0 = b * a.sbp;
+    const uint32_t np = min(a.sbp, a.npieces - p0);
+    uint4 v[GPT];
+    load_piece(a, p0, v);
+    uint4 h = make_uint4(0, 0, 0, 0);
+    if (tid < np) h = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
+    uint64_t X = 0, X0 = 0, total = 0;
+    bool ok = true;
+    for (uint32_t i = 0; i < np; ++i) {
+        const uint32_t p = p0 + i;
+        const uint64_t base = (uint64_t)p * PIECE;
+        const uint64_t rem = a.len - base;
+        const uint32_t clen = rem < PIECE ? (uint32_t)rem : PIECE;
+        __syncthreads();
+        if (i == 0 && tid < np) s.halo[tid] = h;
+#pragma unroll
+        for (uint32_t q = 0; q < GPT; ++q)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s.data64) +
+                                      (q * THREADS + tid) * 16) = v[q];
+        __syncthreads();
+        if (tid < 4)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s.data64) + PIECE + tid * 16) =
+                tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
+        if (i == 0) {
+            if (tid < 64) {
+                const uint32_t f = stride_guess(data, rem, clen, a.hz);
+                if (tid == 0) s.guess = f;
+            }
+            __syncthreads();
+            const uint32_t f = uni(s.guess);
+            if (f == NO_GUESS) {
+                ok = false;
+                break;
+            }
+            X = X0 = base + f;
+        }
+        PieceSum ps;
+        if (!stride_run(data, base, a.len, clen, X, ps)) {
+            ok = false;
+            break;
+        }
+        if (tid == 0) {
+            SpecPiece o;
+            o.x = ps.x;
+            o.R = ps.R;
+            o.kl = ps.kl;
+            o.vl = ps.vl;
+            o.count = ps.count;
+            o.pad = 0;
+            sp[p] = o;
+        }
+        total += ps.count;
+        X = ps.kind == PK_EMPTY ? X : X + (uint64_t)ps.count * ps.R;
+    }
+    if (tid == 0) {
+        SpecBatch o;
+        o.x0 = X0;
+        o.exit = X;
+        o.count = (uint32_t)total;
+        o.ok = ok ? 1u : 0u;
+        o.gbase = 0;
+        sb[b] = o;
+    }
+}
+
+// decode_scan_kernel (one workgroup of 1024 threads): the longest prefix of
+// pre-pass batches that chains exactly (batch 0 enters at 0, every later
+// batch's guessed entry is its predecessor's exit, all verified) and the
+// record base of each of them.  Writes *first_bad; when the prefix is the
+// whole file it also writes the decode result.  Chunks of SCAN_THREADS x
+// SCAN_PER batches: every thread issues its SCAN_PER loads at once.
+constexpr uint32_t SCAN_THREADS = 1024, SCAN_PER = 8;
+__global__ __launch_bounds__(SCAN_THREADS) void decode_scan_kernel(SpecBatch* sb, uint32_t n,
+                                                                    uint32_t* first_bad,
+                                                                    hg_decode_result* result) {
+    __shared__ uint64_t wtot[SCAN_THREADS / 64];
+    __shared__ uint32_t wbad[SCAN_THREADS / 64];
+    __shared__ uint64_t carry_s;
+    __shared__ uint32_t bad_s;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    uint64_t carry = 0;  // records before this chunk
+    uint32_t m = n;      // first bad batch
+    for (uint32_t c0 = 0; c0 < n; c0 += SCAN_THREADS * SCAN_PER) {
+        const uint32_t j0 = c0 + tid * SCAN_PER;
+        uint64_t x0[SCAN_PER], ex[SCAN_PER], prev_exit;
+        uint32_t cnt[SCAN_PER], ok[SCAN_PER];
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; ++k) {
+            const uint32_t j = min(j0 + k, n - 1);
+            x0[k] = sb[j].x0;
+            ex[k] = sb[j].exit;
+            cnt[k] = sb[j].count;
+            ok[k] = sb[j].ok;
+        }
+        prev_exit = (j0 == 0 || j0 > n) ? 0 : sb[min(j0, n) - 1].exit;
+        uint32_t mybad = n;
+        uint64_t sum = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; ++k) {
+            const uint32_t j = j0 + k;
+            const uint64_t want = k == 0 ? prev_exit : ex[k - 1];
+            if (j < n && mybad == n) {
+                if (!ok[k] || x0[k] != want) mybad = j;
+                else sum += cnt[k];
+            }
+        }
+        uint32_t bm = mybad;
+        for (int d = 32; d >= 1; d >>= 1) bm = min(bm, (uint32_t)__shfl_xor((int)bm, d, 64));
+        if (lane == 0) wbad[wid] = bm;
+        __syncthreads();
+        bm = m;
+        for (uint32_t w = 0; w < SCAN_THREADS / 64; ++w) bm = min(bm, wbad[w]);
+        if (j0 >= bm) sum = 0;  // only batches below the first bad one count
+        uint64_t incl = sum;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
+        }
+        if (lane == 63) wtot[wid] = incl;
+        __syncthreads();
+        uint64_t base = carry + incl - sum, chunk = 0;
+        for (uint32_t w = 0; w < SCAN_THREADS / 64; ++w) {
+            if (w < wid) base += wtot[w];
+            chunk += wtot[w];
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < SCAN_PER; ++k) {
+            const uint32_t j = j0 + k;
+            if (j < min(n, bm)) {
+                sb[j].gbase = base;
+                base += cnt[k];
+            }
+        }
+        carry += chunk;
+        m = bm;
+        __syncthreads();
+        if (m < n) break;
+    }
+    if (tid == 0) {
+        *first_bad = m;
+        if (m == n) {
+            hg_decode_result r;
+            r.n_records = carry;
+            r.kind = HG_OK;
+            r.reserved = 0;
+            r.err_offset = 0;
+            *result = r;
+        }
+    }
+    (void)carry_s;
+    (void)bad_s;
+}
+
+// decode_emit_kernel: spans of the resolved pre-pass batches (pure writes;
+// the batch's piece records are staged in LDS first, one load per thread).
+__global__ __launch_bounds__(THREADS) void decode_emit_kernel(DecodeArgs a, const SpecBatch* sb,
+                                                              const SpecPiece* sp) {
+    __shared__ SpecPiece pc[SPEC_BP];
+    __shared__ uint64_t pbase[SPEC_BP];
+    const uint32_t b = blockIdx.x;
+    if (b >= *a.first_bad) return;
+    const uint32_t p0 = b * a.sbp;
+    const uint32_t np = min(a.sbp, a.npieces - p0);
+    const uint32_t tid = threadIdx.x;
+    if (tid < np) pc[tid] = sp[p0 + tid];
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t g = sb[b].gbase;
+        for (uint32_t i = 0; i < np; ++i) {
+            pbase[i] = g;
+            g += pc[i].count;
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = 0; i < np; ++i) {
+        const uint64_t g = uni(pbase[i]);
+        const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
+        const uint32_t kl = uni(pc[i].kl), vl = uni(pc[i].vl), cnt = uni(pc[i].count);
+        for (uint32_t t = tid; t < cnt; t += THREADS)
+            if (g + t < a.cap) write_span(a.spans, g + t, x + t * R, kl, vl);
+    }
+}
+
 }  // namespace hgk
 
 namespace {
 struct DecodeLayout {
-    uint64_t npieces, nbatches, status_words, scratch_off, bytes;
+    uint64_t npieces, nbatches, status_words, scratch_off, nspec, sbatch_off, spiece_off, fb_off,
+        bytes;
 };
 DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
     DecodeLayout l;
     l.npieces = (len + PIECE - 1) / PIECE;
-    l.nbatches = (l.npieces + BATCH - 1) / BATCH;
-    l.status_words = 2 * l.nbatches + 2;  // + ticket
+    l.nbatches = (l.npieces + BATCH_MIN - 1) / BATCH_MIN;  // most batches any launch uses
+    l.status_words = 2 * l.nbatches + 2;                    // + ticket
     l.scratch_off = (l.status_words * 8 + 255) & ~255ull;
-    l.bytes = l.scratch_off + l.nbatches * BATCH * MAX_REC_PIECE * sizeof(hg_span);
+    l.nspec = (l.npieces + SPEC_BP_MIN - 1) / SPEC_BP_MIN;  // most pre-pass batches
+    l.sbatch_off = l.scratch_off + l.npieces * MAX_REC_PIECE * sizeof(hg_span);
+    l.spiece_off = l.sbatch_off + ((l.nspec * sizeof(SpecBatch) + 255) & ~255ull);
+    l.fb_off = l.spiece_off + ((l.npieces * sizeof(SpecPiece) + 255) & ~255ull);
+    l.bytes = l.fb_off + 256;
     return l;
 }
 }  // namespace
 
 extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) { return decode_layout(len).bytes; }
+
+namespace {
+// Workgroups of `kernel` (256 threads) resident at once on the current device.
+template <typename K>
+uint32_t resident_workgroups(K kernel, int slot) {
+    static int cached[4][64] = {{0}};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cached[slot][dev]) {
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, hgk::THREADS, 0) !=
+                hipSuccess ||
+            per_cu <= 0)
+            per_cu = 1;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 1;
+        cached[slot][dev] = per_cu * cus;
+    }
+    return (uint32_t)cached[slot][dev];
+}
+
+uint64_t env_or(const char* name, uint64_t dflt) {
+    if (const char* e = getenv(name)) {
+        const long v = atol(e);
+        if (v > 0) return (uint64_t)v;
+    }
+    return dflt;
+}
+
+// Pieces per pre-pass batch: 16 (256 KiB).  Measured on cfg2 (1 GiB, tools/
+// sweep_spec.sh): 8, 16, 32 and 64 pieces at 4-8 workgroups per CU all land
+// within 0.247-0.263 ms, 16 at the low end; HG_DECODE_SBP (a power of two in
+// [SPEC_BP_MIN, SPEC_BP]) overrides.  Pieces per general batch: about one
+// round of batches over decode_kernel's resident grid, rounded up to whole
+// pre-pass batches, in [BATCH_MIN, BATCH] (HG_DECODE_BP overrides).
+uint32_t spec_pieces(uint64_t npieces, uint32_t resident) {
+    using namespace hgk;
+    (void)npieces;
+    (void)resident;
+    const uint64_t want = env_or("HG_DECODE_SBP", 16);
+    uint32_t sbp = SPEC_BP_MIN;
+    while (sbp < SPEC_BP && sbp < want) sbp <<= 1;
+    return sbp;
+}
+uint32_t general_pieces(uint64_t npieces, uint32_t resident, uint32_t sbp) {
+    using namespace hgk;
+    uint64_t bp = env_or("HG_DECODE_BP", (npieces + resident - 1) / resident);
+    bp = (bp + sbp - 1) / sbp * sbp;
+    if (bp < BATCH_MIN) bp = (BATCH_MIN + sbp - 1) / sbp * sbp;
+    if (bp > BATCH) bp = BATCH;  // BATCH is a multiple of every sbp
+    return (uint32_t)bp;
+}
+}  // namespace
 
 // d_ws must hold hgk_decode_workspace_bytes(len) bytes.  The launcher zeroes
 // the statuses and the ticket (the scratch area needs no initialisation).
@@ -1097,11 +1406,36 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
     a.status = static_cast<unsigned long long*>(d_ws);
     a.ticket = reinterpret_cast<uint32_t*>(a.status + 2 * l.nbatches);
     a.scratch = reinterpret_cast<hg_span*>(static_cast<char*>(d_ws) + l.scratch_off);
-    a.nbatches = (uint32_t)l.nbatches;
+    const uint32_t res_spec = resident_workgroups(decode_spec_kernel, 0);
+    const uint32_t res_gen = d_diag ? resident_workgroups(decode_kernel<true>, 1)
+                                    : resident_workgroups(decode_kernel<false>, 2);
+    a.sbp = spec_pieces(l.npieces, res_spec);
+    a.bp = general_pieces(l.npieces, res_gen, a.sbp);
+    a.nbatches = (uint32_t)((l.npieces + a.bp - 1) / a.bp);
     a.npieces = (uint32_t)l.npieces;
     a.hz = 8 - nb;
     a.diag = d_diag;
+    char* ws = static_cast<char*>(d_ws);
+    SpecBatch* sb = reinterpret_cast<SpecBatch*>(ws + l.sbatch_off);
+    SpecPiece* sp = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
+    uint32_t* fb = reinterpret_cast<uint32_t*>(ws + l.fb_off);
+    a.sbatch = sb;
+    a.first_bad = fb;
+    a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
+    a.q = a.bp / a.sbp;
     if (hipMemsetAsync(d_ws, 0, l.status_words * 8, stream) != hipSuccess) return HG_ERR_HIP;
+    // 1. stride pre-pass  2. chain check + record bases  3. spans of the resolved prefix
+    // HG_DECODE_SPEC_PAD: extra dynamic LDS per pre-pass workgroup (bytes) to cap
+    // its occupancy (experiments).
+    const size_t spec_pad = (size_t)env_or("HG_DECODE_SPEC_PAD", 0) > 65536 ? 0
+                          : (size_t)env_or("HG_DECODE_SPEC_PAD", 0);
+    hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), spec_pad, stream, a, sb,
+                       sp);
+    hipLaunchKernelGGL(decode_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, sb, a.nspec, fb,
+                       d_result);
+    hipLaunchKernelGGL(decode_emit_kernel, dim3(a.nspec), dim3(THREADS), 0, stream, a,
+                       (const SpecBatch*)sb, (const SpecPiece*)sp);
+    // 4. the general engine from the first unresolved batch on (exits at once if none)
     if (d_diag)
         hipLaunchKernelGGL(decode_kernel<true>, dim3(a.nbatches), dim3(THREADS), 0, stream, a);
     else

@@ -11,7 +11,19 @@ from tests import corpus
 pytestmark = pytest.mark.gpu
 
 CHUNK = 16384          # bytes per piece staged in LDS
-BATCH = 8 * CHUNK      # bytes per workgroup ticket / look-back status
+BATCH = 16 * CHUNK     # average bytes per workgroup ticket / look-back status
+_BATCH_PRE = [0, 12, 25, 39, 54, 71, 89, 108]  # hg_decode.hip batch_pre(): varied batch sizes
+
+
+def batch_edges(size):
+    """Byte offsets where decode batches start (pieces 12..20 per batch)."""
+    out, b = [], 1
+    while True:
+        e = ((b // 8) * 128 + _BATCH_PRE[b % 8]) * CHUNK
+        if e >= size:
+            return out
+        out.append(e)
+        b += 1
 
 
 def gpu_decode(engine, data, cap=None):
@@ -122,9 +134,9 @@ def test_batch_edges(engine):
     data, _, _, _ = oracle.encode(arena, pairs)
     assert data.size > 4 * BATCH
     cuts = set()
-    for k in range(1, data.size // BATCH + 1):
+    for e in batch_edges(data.size):
         for d in (-17, -1, 0, 1, 16):
-            cuts.add(k * BATCH + d)
+            cuts.add(e + d)
     for k in (1, 3, 7, 9, 15):
         for d in (-1, 0, 9):
             cuts.add(k * CHUNK + d)

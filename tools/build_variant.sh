@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build an experimental libhorreum_gpu.so with extra defines into build_exp/<name>/
+# (git-ignored; travels to the GPU box).  Usage: tools/build_variant.sh NAME "-DFOO=1 ..."
+set -e
+name=$1; defs=$2
+root=$(cd "$(dirname "$0")/.." && pwd)
+out=$root/build_exp/$name
+mkdir -p "$out"
+cd "$root/horreum_amd/csrc"
+F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-value -Wno-unused-result $defs"
+for f in hg_decode hg_encode hg_runtime; do /opt/rocm/bin/hipcc $F -c $f.hip -o "$out/$f.o" & done; wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/libhorreum_gpu.so" "$out"/hg_decode.o "$out"/hg_encode.o "$out"/hg_runtime.o
+echo "$out/libhorreum_gpu.so"

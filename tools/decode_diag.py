@@ -25,7 +25,12 @@ NAMES = ["t_spec", "t_agg", "t_lb", "t_end", "n_stride", "n_general", "n_serial"
          "spins", "count", "flags", "redo", "c_prep", "c_relax", "rounds", "n_short",
          "p_filter", "p_cand", "p_walk", "p_seed", "p_rounds", "p_emit", "p_stage", "p_stride"]
 W = len(NAMES)
-BATCH_BYTES = 8 * 16384
+PIECE = 16384
+BATCH_MIN = 16  # hg_decode.hip: at most npieces / BATCH_MIN batches per launch
+
+
+def n_batches(L):
+    return ((L + PIECE - 1) // PIECE + BATCH_MIN - 1) // BATCH_MIN
 
 
 def run(eng, sst, L, label):
@@ -35,7 +40,7 @@ def run(eng, sst, L, label):
                                            ctypes.c_void_p, ctypes.c_void_p]
     lib.hgk_decode_workspace_bytes.argtypes = [ctypes.c_uint64]
     lib.hgk_decode_workspace_bytes.restype = ctypes.c_uint64
-    nch = (L + BATCH_BYTES - 1) // BATCH_BYTES
+    nch = n_batches(L)
     ws = torch.zeros(int(lib.hgk_decode_workspace_bytes(L)), dtype=torch.uint8, device=eng.device)
     cap = L // 16
     spans = eng.empty(cap * 16)
@@ -62,6 +67,8 @@ def run(eng, sst, L, label):
     out["n"] = int(r[:8].view("<u8")[0])
     out["kind"] = int(r[8:12].view("<i4")[0])
     d = diag.cpu().numpy().astype(np.uint32).reshape(nch, W)
+    d = d[d[:, 3] != 0]  # rows of batches that ran (t_end stamped)
+    out["batches"] = int(d.shape[0])
     stats = {}
     for i, nm in enumerate(NAMES):
         col = d[:, i].astype(np.float64)

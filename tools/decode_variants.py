@@ -37,9 +37,12 @@ def workloads(dev):
 
 
 def main():
+    only = sys.argv[1] if len(sys.argv) > 1 else None
     eng = Engine(0)
     eng.set_stream(torch.cuda.current_stream(eng.device))
     for label, sst in workloads(eng.device):
+        if only and only not in label:
+            continue
         L = sst.numel()
         cap = L // 16
         spans = eng.empty(cap * 16)

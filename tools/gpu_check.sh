@@ -14,4 +14,4 @@ step() {  # step <name> <seconds> <cmd...>
 TAILN=4 step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider
 [ -n "$VARIANTS" ] && step variants 400 python tools/decode_variants.py
 [ -n "$DIAG" ] && step diag 300 python tools/decode_diag.py
-step bench 400 python bench.py --steps 20 --warmup 5 --cpu-sample-mb 256
+step bench 400 python bench.py

@@ -6,6 +6,7 @@ Per MI355X_MICROARCH.md §HBM, on gfx950 FETCH_SIZE reports half the bytes of a
 wide coalesced streaming read, so it is doubled; WRITE_SIZE is taken as is.
 """
 import csv
+import re
 import glob
 import json
 import os
@@ -16,7 +17,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def find(d, pat):
-    return sorted(glob.glob(os.path.join(d, "**", pat), recursive=True))
+    """Files of the NEWEST rocprofv3 run under d (older runs may linger in
+    gpurun_out/), newest first."""
+    files = glob.glob(os.path.join(d, "**", pat), recursive=True)
+    if not files:
+        return []
+    newest = max(files, key=os.path.getmtime)
+    run_dir = os.path.dirname(newest)
+    prefix = os.path.basename(newest).split("_")[0]
+    return sorted((f for f in files if os.path.dirname(f) == run_dir
+                   and os.path.basename(f).startswith(prefix + "_")), key=os.path.getmtime,
+                  reverse=True)
 
 
 def short(name):
@@ -67,7 +78,9 @@ def main():
     summary["pmc"] = pmc
     flat = {}
     for k, v in pmc.items():
-        key = "decode_kernel" if "decode_kernel" in k else ("encode_kernel" if "encode_kernel" in k else k)
+        if "hgk::" not in k:
+            continue  # torch setup / check kernels of the bench, not ours
+        key = re.sub(r"<.*", "", k.split("hgk::")[-1])
         flat[key] = {"hbm_bytes_per_launch": v["hbm_bytes_per_launch"],
                      "hbm_read_bytes_per_launch": v["hbm_read_bytes_per_launch"],
                      "hbm_write_bytes_per_launch": v["hbm_write_bytes_per_launch"],
