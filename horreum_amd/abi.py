@@ -37,6 +37,7 @@ class Status(enum.IntEnum):
     TOO_LARGE = -3
     INTERNAL = -4
     EMPTY_MERGE = -5
+    UNSORTED = -6
 
 
 # ---- struct layouts (must match include/horreum_gpu.h) -------------------------
@@ -46,11 +47,18 @@ BLOCK_DTYPE = np.dtype([("first_rec", "<u8"), ("position", "<u8"), ("length", "<
 DECODE_RESULT_DTYPE = np.dtype([("n_records", "<u8"), ("kind", "<i4"), ("reserved", "<u4"),
                                 ("err_offset", "<u8")])
 ENCODE_RESULT_DTYPE = np.dtype([("out_len", "<u8"), ("kind", "<i4"), ("reserved", "<u4")])
+MERGE_RESULT_DTYPE = np.dtype([("n_out", "<u8"), ("kind", "<i4"), ("table", "<u4"),
+                               ("index", "<u8")])
 
 
 class HgErr(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int32), ("reserved", ctypes.c_uint32),
                 ("offset", ctypes.c_uint64)]
+
+
+class HgMergeResult(ctypes.Structure):
+    _fields_ = [("n_out", ctypes.c_uint64), ("kind", ctypes.c_int32),
+                ("table", ctypes.c_uint32), ("index", ctypes.c_uint64)]
 
 
 def header_exports(path=HEADER_PATH):
@@ -86,6 +94,13 @@ _PROTOS = {
     "hg_encode_host": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, _u8p, _u64, _vp, _u32, _vp,
                                       ctypes.POINTER(_u64)]),
     "hg_block_count": (_u64, [_u64, _u32]),
+    # merge(ctx, ntables, arena, arena_len, table_off*, spans**, counts*, out, cap, result)
+    "hg_merge_dev": (ctypes.c_int, [_vp, _u32, _u8p, _u64, _vp, _vp, _vp, _vp, _u64,
+                                    ctypes.POINTER(HgMergeResult)]),
+    "hg_merge_dev_async": (ctypes.c_int, [_vp, _u32, _u8p, _u64, _vp, _vp, _vp, _vp, _u64, _vp]),
+    # compact(ctx, ntables, tables**, lens*, out, cap, out_len*, stride, blocks, result*)
+    "hg_compact_host": (ctypes.c_int, [_vp, _u32, _vp, _vp, _u8p, _u64, ctypes.POINTER(_u64),
+                                       _u32, _vp, ctypes.POINTER(HgMergeResult)]),
 }
 
 _lib = None

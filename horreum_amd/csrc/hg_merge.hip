@@ -1,0 +1,499 @@
+// hg_merge.hip — device k-way merge for SSTable compaction (gfx950).
+//
+// Replaces SSTableManager::compact_inner (reference src/sstable/manager.rs:
+// 199-234): tables are given in priority order (index 0 wins ties; compact()
+// passes them newest first, manager.rs:146-149).  The output is the sorted
+// union of the keys, each taken from the highest-priority table holding it;
+// tombstones are kept (no filtering, :216-217).  For tables that are sorted
+// with unique keys -- every table horreum writes (memtable BTreeMap flush,
+// compaction output) -- that is exactly the reference loop's result; the
+// engine verifies the invariant and returns HG_ERR_UNSORTED otherwise.
+//
+// Design (MI355X): keys are compared through 32-byte merge entries: a 16-byte
+// big-endian key prefix (one 128-bit compare decides almost every pair), the
+// key length and a (table, record) reference; only keys that agree on their
+// first 16 bytes and are both longer fetch the rest from HBM.
+//   1. merge_prep_kernel: one entry per record (runs laid out table by table).
+//   2. merge_check_kernel: each table strictly increasing (else UNSORTED).
+//   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
+//      priority, B = lower) merge by merge path: a workgroup owns TILE output
+//      positions, finds its A/B split with a 64-ary search by one wave, stages
+//      both segments in LDS and places every element by a binary search in
+//      the other segment (ties: A first).  A B element whose key also occurs
+//      in A is marked dead (newest wins).  Output runs occupy the same index
+//      ranges as their two inputs.
+//   4. merge_count / merge_scan / merge_emit kernels: the live entries, in
+//      order, become hg_pair records pointing into the arena -- the input of
+//      hg_encode_*, so compaction is decode -> merge -> encode on device.
+#include "hg_device.hpp"
+
+namespace hgm {
+
+constexpr uint32_t THREADS = 256;
+constexpr uint32_t TILE = 1024;      // merged positions per workgroup
+constexpr uint32_t EPT = TILE / THREADS;
+constexpr uint32_t DEAD = 0x80000000u;
+constexpr uint32_t MAX_TABLES = 1u << 16;
+
+struct MEnt {          // 32 bytes
+    uint64_t p0, p1;   // key bytes [0,8) and [8,16), big-endian, zero padded
+    uint32_t klen;
+    uint32_t tdead;    // table index | DEAD
+    uint64_t rec;      // record index within its table
+};
+
+struct MergeArgs {
+    const uint8_t* arena;
+    uint64_t arena_len;
+    const uint64_t* table_off;   // [ntables] byte offset of each table in the arena
+    const hg_span* const* spans; // [ntables] device pointers
+    const uint64_t* run_off;     // [ntables + 1] entry offsets of the tables' runs
+    uint32_t ntables;
+    uint64_t n;                  // total entries
+};
+
+__device__ __forceinline__ const uint8_t* key_ptr(const MergeArgs& a, uint32_t t, uint64_t rec) {
+    return a.arena + a.table_off[t] + a.spans[t][rec].off + 16;
+}
+
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// Bytes [from, to) of two keys that agree on their first `from` bytes.
+__device__ int tail_cmp(const MergeArgs& a, const MEnt& x, const MEnt& y) {
+    const uint8_t* kx = key_ptr(a, x.tdead & ~DEAD, x.rec);
+    const uint8_t* ky = key_ptr(a, y.tdead & ~DEAD, y.rec);
+    const uint32_t m = min(x.klen, y.klen);
+    for (uint32_t i = 16; i < m; ++i) {
+        const uint8_t bx = kx[i], by = ky[i];
+        if (bx != by) return bx < by ? -1 : 1;
+    }
+    return x.klen < y.klen ? -1 : x.klen > y.klen ? 1 : 0;
+}
+
+// Lexicographic byte order, a shorter key first when it is a prefix
+// (Vec<u8> Ord, src/format.rs:5).
+__device__ __forceinline__ int key_cmp(const MergeArgs& a, const MEnt& x, const MEnt& y) {
+    if (x.p0 != y.p0) return x.p0 < y.p0 ? -1 : 1;
+    if (x.p1 != y.p1) return x.p1 < y.p1 ? -1 : 1;
+    if (x.klen <= 16 || y.klen <= 16) return x.klen < y.klen ? -1 : x.klen > y.klen ? 1 : 0;
+    return tail_cmp(a, x, y);
+}
+
+// ---- 1. entries ---------------------------------------------------------------------
+__device__ __forceinline__ uint32_t run_of(const MergeArgs& a, uint64_t g) {
+    uint32_t lo = 0, hi = a.ntables;  // last run with run_off[r] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.run_off[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* e) {
+    const uint64_t g = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
+    if (g >= a.n) return;
+    const uint32_t t = run_of(a, g);
+    const uint64_t rec = g - a.run_off[t];
+    const hg_span sp = a.spans[t][rec];
+    const uint8_t* k = a.arena + a.table_off[t] + sp.off + 16;
+    uint8_t b[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) b[i] = (uint32_t)i < sp.klen ? k[i] : 0;
+    uint64_t w0 = 0, w1 = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        w0 = (w0 << 8) | b[i];
+        w1 = (w1 << 8) | b[8 + i];
+    }
+    MEnt m;
+    m.p0 = w0;
+    m.p1 = w1;
+    m.klen = sp.klen;
+    m.tdead = t;
+    m.rec = rec;
+    e[g] = m;
+}
+
+// ---- 2. each table strictly increasing ----------------------------------------------
+// err[0] = lowest offending global entry index (initialised to ~0).
+__global__ __launch_bounds__(THREADS) void merge_check_kernel(MergeArgs a, const MEnt* e,
+                                                              unsigned long long* err) {
+    const uint64_t g = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
+    if (g >= a.n || g == 0) return;
+    const MEnt cur = e[g], prev = e[g - 1];
+    if ((cur.tdead & ~DEAD) != (prev.tdead & ~DEAD)) return;  // first record of a table
+    if (key_cmp(a, prev, cur) >= 0) atomicMin(err, (unsigned long long)g);
+}
+
+// ---- 3. one merge round ---------------------------------------------------------------
+struct LevelArgs {
+    const uint64_t* roff;  // [nruns + 1] run offsets of this round's input
+    uint32_t nruns;
+};
+
+// Number of A elements among the first d merged elements (ties: A first),
+// by a 64-ary search run by one wave.  Returns the same value in every lane.
+__device__ uint64_t merge_path(const MergeArgs& a, const MEnt* A, uint64_t na, const MEnt* B,
+                               uint64_t nb, uint64_t d) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;  // answer in [lo, hi]
+    while (hi > lo) {
+        // candidate c: "A[c] is among the first d" <=> A[c] <= B[d-c-1]
+        const uint64_t span = hi - lo;
+        const uint64_t c = lo + (span * lane) / 64;  // lanes probe lo .. hi-1
+        bool before = false;
+        if (c < hi) {
+            const MEnt x = A[c];
+            const MEnt y = B[d - c - 1];
+            before = key_cmp(a, x, y) <= 0;
+        }
+        // predicate is monotone (true ... true false ... false) over c
+        const unsigned long long m = __ballot(c < hi && !before);
+        if (!m) {
+            // every probed c is "before": answer > last probe
+            const uint64_t last = lo + (span * 63) / 64;
+            lo = last + 1;
+        } else {
+            const int f = __ffsll((long long)m) - 1;  // first probe that is not before
+            const uint64_t cf = lo + (span * (uint64_t)f) / 64;
+            const uint64_t cp = f > 0 ? lo + (span * (uint64_t)(f - 1)) / 64 + 1 : lo;
+            lo = cp;
+            hi = cf;
+        }
+    }
+    return lo;
+}
+
+struct LevelSmem {
+    MEnt seg[TILE + 2];      // A segment then B segment
+    MEnt aprev;              // A element just before the tile's A segment
+    uint64_t i0, i1;         // A split at the tile's start / end
+    uint32_t has_prev;
+};
+
+// Lower bound of x in s[0, n) (first element >= x); upper = first > x.
+__device__ __forceinline__ uint32_t lds_bound(const MergeArgs& a, const MEnt* s, uint32_t n,
+                                              const MEnt& x, bool upper) {
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const int c = key_cmp(a, s[mid], x);
+        if (c < 0 || (upper && c == 0)) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// err: the order check's result; merging unsorted runs is meaningless (and
+// their merge paths are not monotone), so every round skips work once set.
+__global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, LevelArgs l,
+                                                              const MEnt* in, MEnt* out,
+                                                              unsigned long long* err) {
+    __shared__ LevelSmem s;
+    const uint32_t tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+    if (t0 >= a.n || *err != ~0ull) return;
+    const uint64_t t1 = min(t0 + TILE, a.n);
+    // The tile may span several output runs (pairs); handle each piece.
+    uint64_t d0 = t0;
+    while (d0 < t1) {
+        // pair containing output position d0
+        uint32_t lo = 0, hi = l.nruns;
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (l.roff[mid] <= d0) lo = mid;
+            else hi = mid;
+        }
+        const uint32_t pa = lo & ~1u;  // A run of the pair
+        const uint64_t o = l.roff[pa];
+        const uint64_t amid = l.roff[min(pa + 1, l.nruns)];
+        const uint64_t oend = l.roff[min(pa + 2, l.nruns)];
+        const uint64_t d1 = min(t1, oend);
+        const MEnt* A = in + o;
+        const MEnt* B = in + amid;
+        const uint64_t na = amid - o, nb = oend - amid;
+        if (nb == 0) {  // odd run out: copied as is
+            for (uint64_t d = d0 + tid; d < d1; d += THREADS) out[d] = in[d];
+            d0 = d1;
+            __syncthreads();
+            continue;
+        }
+        if (tid < 64) {
+            const uint64_t i0 = merge_path(a, A, na, B, nb, d0 - o);
+            const uint64_t i1 = merge_path(a, A, na, B, nb, d1 - o);
+            if (tid == 0) {
+                s.i0 = i0;
+                s.i1 = i1;
+                s.has_prev = i0 > 0;
+                if (i0 > 0) s.aprev = A[i0 - 1];
+            }
+        }
+        __syncthreads();
+        const uint64_t i0 = s.i0, i1 = s.i1;
+        if (i1 < i0 || i0 > d0 - o || i1 > d1 - o || (d1 - o) - i1 < (d0 - o) - i0) {
+            // splits of sorted runs are monotone; anything else means the
+            // input was not sorted: flag it (reported as UNSORTED) and stop
+            if (tid == 0) atomicMin(err, (unsigned long long)o);
+            return;
+        }
+        const uint64_t j0 = (d0 - o) - i0, j1 = (d1 - o) - i1;
+        const uint32_t nA = (uint32_t)(i1 - i0), nB = (uint32_t)(j1 - j0);
+        for (uint32_t q = tid; q < nA; q += THREADS) s.seg[q] = A[i0 + q];
+        for (uint32_t q = tid; q < nB; q += THREADS) s.seg[nA + q] = B[j0 + q];
+        __syncthreads();
+        const MEnt* SA = s.seg;
+        const MEnt* SB = s.seg + nA;
+        MEnt* dst = out + d0;
+        for (uint32_t q = tid; q < nA + nB; q += THREADS) {
+            MEnt x = s.seg[q];
+            uint32_t pos;
+            if (q < nA) {
+                pos = q + lds_bound(a, SB, nB, x, false);
+            } else {
+                const uint32_t jb = q - nA;
+                const uint32_t ub = lds_bound(a, SA, nA, x, true);
+                pos = jb + ub;
+                // newest wins: an equal key in A (inside the tile, or the A
+                // element just before it) kills this lower-priority copy
+                const bool eq_in = ub > 0 && key_cmp(a, SA[ub - 1], x) == 0;
+                const bool eq_prev = ub == 0 && s.has_prev && key_cmp(a, s.aprev, x) == 0;
+                if (eq_in || eq_prev) x.tdead |= DEAD;
+            }
+            dst[pos] = x;
+        }
+        d0 = d1;
+        __syncthreads();
+    }
+}
+
+// ---- 4. live entries -> hg_pair ---------------------------------------------------------
+__global__ __launch_bounds__(THREADS) void merge_count_kernel(MergeArgs a, const MEnt* e,
+                                                              uint32_t* tile_live) {
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+    uint32_t c = 0;
+    for (uint32_t q = threadIdx.x; q < TILE; q += THREADS) {
+        const uint64_t g = t0 + q;
+        if (g < a.n && !(e[g].tdead & DEAD)) ++c;
+    }
+    __shared__ uint32_t ws[THREADS / 64];
+    c = hgk::wave_sum<uint32_t>(c);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (uint32_t w = 0; w < THREADS / 64; ++w) s += ws[w];
+        tile_live[blockIdx.x] = s;
+    }
+}
+
+// Exclusive scan of the tile counts by one workgroup (ntiles = n / TILE).
+__global__ __launch_bounds__(1024) void merge_scan_kernel(const uint32_t* tile_live, uint32_t ntiles,
+                                                          uint64_t* tile_base,
+                                                          hg_merge_result* result) {
+    __shared__ uint64_t wt[16];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    uint64_t carry = 0;
+    for (uint32_t c0 = 0; c0 < ntiles; c0 += 1024) {
+        const uint32_t j = c0 + tid;
+        const uint64_t v = j < ntiles ? tile_live[j] : 0;
+        uint64_t incl = v;
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint64_t o = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += o;
+        }
+        if (lane == 63) wt[wid] = incl;
+        __syncthreads();
+        uint64_t base = carry + incl - v, tot = 0;
+        for (uint32_t w = 0; w < 16; ++w) {
+            if (w < wid) base += wt[w];
+            tot += wt[w];
+        }
+        if (j < ntiles) tile_base[j] = base;
+        carry += tot;
+        __syncthreads();
+    }
+    if (tid == 0) {
+        result->n_out = carry;
+        result->kind = HG_OK;
+        result->table = 0;
+        result->index = 0;
+    }
+}
+
+__global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const MEnt* e,
+                                                             const uint64_t* tile_base,
+                                                             hg_pair* out, uint64_t cap,
+                                                             const unsigned long long* err) {
+    __shared__ uint32_t ws[THREADS / 64];
+    if (*err != ~0ull) return;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+    // each thread owns EPT consecutive positions of the tile
+    const uint64_t g0 = t0 + (uint64_t)tid * EPT;
+    MEnt x[EPT];
+    uint32_t live = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < EPT; ++k) {
+        if (g0 + k < a.n) {
+            x[k] = e[g0 + k];
+            live += !(x[k].tdead & DEAD);
+        } else {
+            x[k].tdead = DEAD;
+        }
+    }
+    uint32_t incl = hgk::wave_incl_scan(live);
+    if (lane == 63) ws[wid] = incl;
+    __syncthreads();
+    uint64_t pos = tile_base[blockIdx.x] + incl - live;
+    for (uint32_t w = 0; w < wid; ++w) pos += ws[w];
+#pragma unroll
+    for (uint32_t k = 0; k < EPT; ++k) {
+        if (x[k].tdead & DEAD) continue;
+        if (pos < cap) {
+            const uint32_t t = x[k].tdead;
+            const hg_span sp = a.spans[t][x[k].rec];
+            hg_pair p;
+            p.key_off = a.table_off[t] + sp.off + 16;
+            p.val_off = p.key_off + sp.klen;
+            p.klen = sp.klen;
+            p.vlen = sp.vlen;
+            out[pos] = p;
+        }
+        ++pos;
+    }
+}
+
+// After the check: turn a found disorder into the result's error.
+__global__ void merge_error_kernel(MergeArgs a, const unsigned long long* err, const MEnt* e,
+                                   hg_merge_result* result) {
+    const unsigned long long g = *err;
+    if (g == ~0ull) return;
+    const MEnt m = e[g < a.n ? g : a.n - 1];
+    result->n_out = 0;
+    result->kind = HG_ERR_UNSORTED;
+    result->table = m.tdead & ~DEAD;
+    result->index = m.rec;
+}
+
+}  // namespace hgm
+
+// ---- launcher ----------------------------------------------------------------------------
+// Workspace (device): two entry buffers, tile counts/bases, run offsets for
+// every round, table offsets and span pointers, the error word.
+extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
+    using namespace hgm;
+    const uint64_t ntiles = (n + TILE - 1) / TILE + 1;
+    uint64_t b = 2 * ((n * sizeof(MEnt) + 255) & ~255ull);
+    b += ((ntiles * 4 + 255) & ~255ull) + ((ntiles * 8 + 255) & ~255ull);
+    b += ((4 * (uint64_t)ntables + 64) * 8 + 255) & ~255ull;  // device copy of the staging
+    b += 256;                                                  // error word
+    return b;
+}
+
+// Host arrays: table_off[ntables], spans[ntables] (device pointers),
+// counts[ntables].  `staging` is pinned host memory of at least
+// hgk_merge_staging_bytes(ntables) bytes (copied to the device on `stream`).
+// [table_off | span ptrs | run offsets of every round]: the rounds' offset
+// lists total at most 2 * ntables + 2 * ceil(log2 ntables) + 2 words.
+extern "C" uint64_t hgk_merge_staging_bytes(uint32_t ntables) {
+    return (4 * (uint64_t)ntables + 64) * 8;
+}
+
+extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint32_t ntables,
+                                const uint64_t* table_off, const hg_span* const* spans,
+                                const uint64_t* counts, hg_pair* d_out, uint64_t cap,
+                                hg_merge_result* d_result, void* d_ws, void* staging,
+                                hipStream_t stream) {
+    using namespace hgm;
+    if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
+    uint64_t n = 0;
+    for (uint32_t t = 0; t < ntables; ++t) n += counts[t];
+    // host staging: [table_off | span ptrs | run offsets of every round]
+    uint64_t* h = static_cast<uint64_t*>(staging);
+    uint64_t* h_toff = h;
+    uint64_t* h_sp = h + ntables;
+    uint64_t* h_roff = h + 2 * (uint64_t)ntables;  // round 0 offsets; later rounds follow
+    uint64_t nr = ntables, total_roff = 0;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        h_toff[t] = table_off[t];
+        h_sp[t] = reinterpret_cast<uint64_t>(spans[t]);
+    }
+    {  // run offsets per round: round r has nr runs (nr + 1 offsets)
+        uint64_t* r = h_roff;
+        r[0] = 0;
+        for (uint32_t t = 0; t < ntables; ++t) r[t + 1] = r[t] + counts[t];
+        total_roff = nr + 1;
+        while (nr > 1) {
+            uint64_t* nxt = r + (nr + 1);
+            const uint64_t m = (nr + 1) / 2;
+            for (uint64_t i = 0; i <= m; ++i) nxt[i] = r[min(2 * i, nr)];
+            total_roff += m + 1;
+            r = nxt;
+            nr = m;
+        }
+    }
+    const uint64_t stage_words = 2 * (uint64_t)ntables + total_roff;
+    if (stage_words * 8 > hgk_merge_staging_bytes(ntables)) return HG_ERR_INTERNAL;
+    char* ws = static_cast<char*>(d_ws);
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
+    MEnt* e0 = reinterpret_cast<MEnt*>(ws);
+    MEnt* e1 = reinterpret_cast<MEnt*>(ws + ((n * sizeof(MEnt) + 255) & ~255ull));
+    char* p = ws + 2 * ((n * sizeof(MEnt) + 255) & ~255ull);
+    uint32_t* tile_live = reinterpret_cast<uint32_t*>(p);
+    p += ((ntiles + 1) * 4 + 255) & ~255ull;
+    uint64_t* tile_base = reinterpret_cast<uint64_t*>(p);
+    p += ((ntiles + 1) * 8 + 255) & ~255ull;
+    uint64_t* d_stage = reinterpret_cast<uint64_t*>(p);
+    p += (stage_words * 8 + 255) & ~255ull;
+    unsigned long long* err = reinterpret_cast<unsigned long long*>(p);
+    if (hipMemcpyAsync(d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
+        return HG_ERR_HIP;
+    if (hipMemsetAsync(err, 0xFF, 8, stream) != hipSuccess) return HG_ERR_HIP;
+
+    MergeArgs a;
+    a.arena = d_arena;
+    a.arena_len = arena_len;
+    a.table_off = d_stage;
+    a.spans = reinterpret_cast<const hg_span* const*>(d_stage + ntables);
+    a.run_off = d_stage + 2 * (uint64_t)ntables;
+    a.ntables = ntables;
+    a.n = n;
+    if (n == 0) {
+        // every table empty: the reference's unwrap on None (manager.rs:213)
+        hg_merge_result r{0, HG_ERR_EMPTY_MERGE, 0, 0};
+        return hipMemcpyAsync(d_result, &r, sizeof r, hipMemcpyHostToDevice, stream) == hipSuccess
+                   ? HG_OK
+                   : HG_ERR_HIP;
+    }
+    const uint32_t g1 = (uint32_t)((n + THREADS - 1) / THREADS);
+    hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, e0);
+    hipLaunchKernelGGL(merge_check_kernel, dim3(g1), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)e0, err);
+    MEnt* cur = e0;
+    MEnt* nxt = e1;
+    const uint64_t* roff = a.run_off;
+    uint64_t nruns = ntables;
+    while (nruns > 1) {
+        LevelArgs l;
+        l.roff = roff;
+        l.nruns = (uint32_t)nruns;
+        hipLaunchKernelGGL(merge_level_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                           l, (const MEnt*)cur, nxt, err);
+        roff += nruns + 1;
+        nruns = (nruns + 1) / 2;
+        MEnt* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+    hipLaunchKernelGGL(merge_count_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)cur, tile_live);
+    hipLaunchKernelGGL(merge_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)tile_live,
+                       (uint32_t)ntiles, tile_base, d_result);
+    hipLaunchKernelGGL(merge_emit_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)cur, (const uint64_t*)tile_base, d_out, cap,
+                       (const unsigned long long*)err);
+    hipLaunchKernelGGL(merge_error_kernel, dim3(1), dim3(1), 0, stream, a,
+                       (const unsigned long long*)err, (const MEnt*)e0, d_result);
+    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}

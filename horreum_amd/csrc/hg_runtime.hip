@@ -17,6 +17,11 @@ extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8
                                  uint64_t*, uint32_t, hg_block*, hg_encode_result*,
                                  unsigned long long*, hipStream_t);
 extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t);
+extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
+extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
+extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
+                                const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
+                                hg_merge_result*, void*, void*, hipStream_t);
 
 namespace {
 
@@ -45,6 +50,11 @@ struct hg_ctx {
     // host-path staging (device side)
     DevBuf d_in, d_out, d_aux;
     PinBuf h_stage[2];
+    // merge: workspace, result, pinned argument staging and its reuse event
+    DevBuf mws, mres, mspans, mpairs;
+    PinBuf mstage;
+    hipEvent_t mstage_ev = nullptr;
+    bool mstage_busy = false;
 };
 
 namespace {
@@ -99,6 +109,7 @@ const char* hg_status_string(int s) {
         case HG_ERR_TOO_LARGE: return "input too large (>= 2^40 bytes)";
         case HG_ERR_INTERNAL: return "internal error (device spin timeout)";
         case HG_ERR_EMPTY_MERGE: return "merge of zero records";
+        case HG_ERR_UNSORTED: return "merge input table not strictly increasing by key";
         default: return "unknown status";
     }
 }
@@ -129,10 +140,12 @@ int hg_ctx_destroy(hg_ctx* c) {
     if (!c) return HG_ERR_INVALID_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux})
+    for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->mws,
+                      &c->mres, &c->mspans, &c->mpairs})
         if (b->p) hipFree(b->p);
-    for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1]})
+    for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage})
         if (b->p) hipHostFree(b->p);
+    if (c->mstage_ev) hipEventDestroy(c->mstage_ev);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
     return HG_OK;
@@ -380,6 +393,156 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
     if (h_blocks && nb && (r = d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block))) != HG_OK)
         return r;
     return HG_OK;
+}
+
+// ---- merge (compaction) ------------------------------------------------------------
+int hg_merge_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
+                       const uint64_t* table_off, const hg_span* const* d_spans,
+                       const uint64_t* counts, hg_pair* d_out, uint64_t cap,
+                       hg_merge_result* d_result) {
+    if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
+        return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (!c->mstage_ev && hipEventCreateWithFlags(&c->mstage_ev, hipEventDisableTiming) != hipSuccess)
+        return HG_ERR_HIP;
+    if (ntables == 0) {  // min_by_key over no candidates: the reference panics (:213)
+        hg_merge_result r{0, HG_ERR_EMPTY_MERGE, 0, 0};
+        if (ensure_pin(c->mstage, 4096) != HG_OK) return HG_ERR_HIP;
+        if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_ERR_HIP;
+        memcpy(c->mstage.p, &r, sizeof r);
+        if (hipMemcpyAsync(d_result, c->mstage.p, sizeof r, hipMemcpyHostToDevice, c->stream) !=
+            hipSuccess)
+            return HG_ERR_HIP;
+    } else {
+        uint64_t n = 0;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            if (counts[t] && !d_spans[t]) return HG_ERR_INVALID_ARG;
+            n += counts[t];
+        }
+        int r = ensure(c, c->mws, hgk_merge_workspace_bytes(ntables, n) +
+                                      hgk_merge_staging_bytes(ntables) + 4096);
+        if (r != HG_OK) return r;
+        // the previous call's argument copy must have left the pinned staging
+        if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_ERR_HIP;
+        if (ensure_pin(c->mstage, hgk_merge_staging_bytes(ntables) + 4096) != HG_OK)
+            return HG_ERR_HIP;
+        r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
+                             d_result, c->mws.p, c->mstage.p, c->stream);
+        if (r != HG_OK) return r;
+    }
+    if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_ERR_HIP;
+    c->mstage_busy = true;
+    return HG_OK;
+}
+
+int hg_merge_dev(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
+                 const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
+                 hg_pair* d_out, uint64_t cap, hg_merge_result* result) {
+    if (!c) return HG_ERR_INVALID_ARG;
+    if (ensure(c, c->mres, 64) != HG_OK) return HG_ERR_HIP;
+    hg_merge_result* dres_m = static_cast<hg_merge_result*>(c->mres.p);
+    int r = hg_merge_dev_async(c, ntables, d_arena, arena_len, table_off, d_spans, counts, d_out,
+                               cap, dres_m);
+    if (r != HG_OK) return r;
+    if (hipMemcpyAsync(c->hres.p, dres_m, sizeof(hg_merge_result), hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return HG_ERR_HIP;
+    const hg_merge_result res = *static_cast<hg_merge_result*>(c->hres.p);
+    if (result) *result = res;
+    if (res.kind != HG_OK) return res.kind;
+    return res.n_out > cap ? HG_ERR_CAPACITY : HG_OK;
+}
+
+int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
+                    const uint64_t* lens, uint8_t* h_out, uint64_t cap, uint64_t* out_len,
+                    uint32_t block_stride, hg_block* h_blocks, hg_merge_result* result) {
+    if (!c || (ntables && (!h_tables || !lens)) || (cap && !h_out)) return HG_ERR_INVALID_ARG;
+    if (h_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    hg_merge_result res{0, HG_OK, 0, 0};
+    if (out_len) *out_len = 0;
+    // 1. all tables into one device arena (8-byte aligned starts), spans per table
+    uint64_t total = 0, span_cap = 0;
+    uint64_t* toff = new (std::nothrow) uint64_t[ntables + 1];
+    uint64_t* sofs = new (std::nothrow) uint64_t[ntables + 1];
+    uint64_t* counts = new (std::nothrow) uint64_t[ntables + 1];
+    const hg_span** sp = new (std::nothrow) const hg_span*[ntables + 1];
+    int r = (toff && sofs && counts && sp) ? HG_OK : HG_ERR_INTERNAL;
+    for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
+        if (lens[t] && !h_tables[t]) r = HG_ERR_INVALID_ARG;
+        if (lens[t] >= kMaxLen) r = HG_ERR_TOO_LARGE;
+        toff[t] = total;
+        total += (lens[t] + 7) & ~7ull;
+        sofs[t] = span_cap;
+        span_cap += lens[t] / 16;
+    }
+    if (r == HG_OK) r = ensure(c, c->d_in, total ? total : 1);
+    if (r == HG_OK) r = ensure(c, c->mspans, (span_cap ? span_cap : 1) * sizeof(hg_span));
+    char* arena = static_cast<char*>(c->d_in.p);
+    hg_span* spans = static_cast<hg_span*>(c->mspans.p);
+    for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
+        sp[t] = spans + sofs[t];
+        counts[t] = 0;
+        if (!lens[t]) continue;
+        r = h2d_pipelined(c, arena + toff[t], h_tables[t], lens[t]);
+        if (r != HG_OK) break;
+        hg_err e{};
+        uint64_t nrec = 0;
+        r = hg_decode_dev(c, reinterpret_cast<const uint8_t*>(arena + toff[t]), lens[t],
+                          spans + sofs[t], lens[t] / 16, &nrec, &e);
+        if (e.kind != HG_OK) {  // the reference's read_all unwrap (storage.rs:64-66)
+            res = hg_merge_result{0, e.kind, t, e.offset};
+            r = e.kind;
+            break;
+        }
+        if (r != HG_OK) break;
+        counts[t] = nrec;
+    }
+    // 2. merge -> pairs into the arena
+    uint64_t nm = 0;
+    if (r == HG_OK) {
+        for (uint32_t t = 0; t < ntables; ++t) nm += counts[t];
+        r = ensure(c, c->mpairs, (nm ? nm : 1) * sizeof(hg_pair));
+    }
+    if (r == HG_OK) {
+        r = hg_merge_dev(c, ntables, reinterpret_cast<const uint8_t*>(arena), total, toff, sp,
+                         counts, static_cast<hg_pair*>(c->mpairs.p), nm, &res);
+    }
+    // 3. encode the merged records (+ index blocks) and copy them out
+    if (r == HG_OK) {
+        const uint64_t n = res.n_out;
+        uint64_t enc = 0;
+        // encoded size = sum of the selected records' sizes (from the pairs)
+        const uint64_t nb = h_blocks ? hg_block_count(n, block_stride) : 0;
+        r = ensure(c, c->d_aux, n * sizeof(uint64_t) + nb * sizeof(hg_block) + 64);
+        hg_block* d_blk = h_blocks ? reinterpret_cast<hg_block*>(static_cast<char*>(c->d_aux.p) +
+                                                                  n * sizeof(uint64_t))
+                                   : nullptr;
+        // out size is only known after the merge: upper bound = input bytes
+        if (r == HG_OK) r = ensure(c, c->d_out, total ? total : 1);
+        if (r == HG_OK)
+            r = hg_encode_dev(c, reinterpret_cast<const uint8_t*>(arena),
+                              static_cast<const hg_pair*>(c->mpairs.p), n,
+                              static_cast<uint8_t*>(c->d_out.p), total,
+                              static_cast<uint64_t*>(c->d_aux.p), block_stride, d_blk, &enc);
+        if (r == HG_OK) {
+            if (out_len) *out_len = enc;
+            if (enc > cap) {
+                r = HG_ERR_CAPACITY;
+            } else {
+                if (enc) r = d2h_pipelined(c, h_out, c->d_out.p, enc);
+                if (r == HG_OK && h_blocks && nb)
+                    r = d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block));
+            }
+        }
+    }
+    if (result) *result = res;
+    delete[] toff;
+    delete[] sofs;
+    delete[] counts;
+    delete[] sp;
+    return r;
 }
 
 }  // extern "C"

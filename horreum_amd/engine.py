@@ -10,11 +10,13 @@ from collections import namedtuple
 
 import numpy as np
 
-from .abi import (BLOCK_DTYPE, PAIR_DTYPE, SPAN_DTYPE, HgErr, HorreumGpuError, Status, check,
-                  load_library)
+from .abi import (BLOCK_DTYPE, PAIR_DTYPE, SPAN_DTYPE, HgErr, HgMergeResult, HorreumGpuError,
+                  Status, check, load_library)
 
 DecodeOut = namedtuple("DecodeOut", "spans n kind offset")
 EncodeOut = namedtuple("EncodeOut", "data rec_off blocks out_len")
+MergeOut = namedtuple("MergeOut", "status n kind table index")
+CompactOut = namedtuple("CompactOut", "status data blocks n kind table index")
 
 
 def _torch():
@@ -162,6 +164,57 @@ class Engine:
         check(rc, "hg_encode_host")
         return EncodeOut(out[:total], rec_off[:n] if rec_off is not None else None,
                          blocks[:nb] if blocks is not None else None, out_len.value)
+
+
+    # ---- merge / compaction -----------------------------------------------------------
+    def merge_dev(self, arena, table_off, spans, counts, out, cap):
+        """k-way merge of decoded tables living in device tensor `arena`.
+        table_off: byte offset of each table in the arena; spans: device
+        tensors of hg_span records (offsets relative to each table); counts:
+        records per table.  Priority order: index 0 wins equal keys.  Writes
+        hg_pair records (offsets into the arena) to device tensor `out`."""
+        k = len(counts)
+        toff = (ctypes.c_uint64 * max(k, 1))(*[int(x) for x in table_off])
+        sp = (ctypes.c_void_p * max(k, 1))(*[s.data_ptr() if s is not None else 0 for s in spans])
+        cnt = (ctypes.c_uint64 * max(k, 1))(*[int(x) for x in counts])
+        res = HgMergeResult()
+        rc = self.lib.hg_merge_dev(self.ctx, k, _ptr(arena), arena.numel() if arena is not None
+                                   else 0, ctypes.cast(toff, ctypes.c_void_p),
+                                   ctypes.cast(sp, ctypes.c_void_p),
+                                   ctypes.cast(cnt, ctypes.c_void_p), _ptr(out), int(cap),
+                                   ctypes.byref(res))
+        if rc in (Status.HIP, Status.INVALID_ARG, Status.INTERNAL):
+            raise HorreumGpuError(rc, "hg_merge_dev")
+        return MergeOut(rc, res.n_out, res.kind, res.table, res.index)
+
+    def compact_host(self, tables, block_stride=0):
+        """SSTableManager::compact's byte work (src/sstable/manager.rs:137-159)
+        on host bytes: `tables` (bytes-like, priority order: newest first) ->
+        the compacted SSTable bytes (+ index blocks)."""
+        bufs = [np.ascontiguousarray(np.frombuffer(memoryview(t).cast("B"), dtype=np.uint8))
+                for t in tables]
+        k = len(bufs)
+        ptrs = (ctypes.c_void_p * max(k, 1))(*[b.ctypes.data if b.size else 0 for b in bufs])
+        lens = (ctypes.c_uint64 * max(k, 1))(*[b.size for b in bufs])
+        cap = max(sum(b.size for b in bufs), 1)
+        out = np.empty(cap, dtype=np.uint8)
+        n_hint = sum(b.size for b in bufs) // 16
+        nb = int(self.lib.hg_block_count(n_hint, block_stride)) if block_stride else 0
+        blocks = np.empty(max(nb, 1), dtype=BLOCK_DTYPE) if block_stride else None
+        out_len = ctypes.c_uint64()
+        res = HgMergeResult()
+        rc = self.lib.hg_compact_host(self.ctx, k, ctypes.cast(ptrs, ctypes.c_void_p),
+                                      ctypes.cast(lens, ctypes.c_void_p),
+                                      out.ctypes.data_as(ctypes.c_void_p), cap,
+                                      ctypes.byref(out_len), int(block_stride),
+                                      blocks.ctypes.data_as(ctypes.c_void_p)
+                                      if blocks is not None else ctypes.c_void_p(0),
+                                      ctypes.byref(res))
+        if rc in (Status.HIP, Status.INVALID_ARG, Status.INTERNAL, Status.TOO_LARGE):
+            raise HorreumGpuError(rc, "hg_compact_host")
+        nbo = int(self.lib.hg_block_count(res.n_out, block_stride)) if block_stride else 0
+        return CompactOut(rc, out[:out_len.value], blocks[:nbo] if blocks is not None else None,
+                          res.n_out, res.kind, res.table, res.index)
 
 
 _default = None

@@ -58,6 +58,18 @@ class Index:
                                int(nxt[i] - pos[i])))
         return cls(items)
 
+    @classmethod
+    def from_encoded(cls, data, blocks):
+        """Blocks of freshly encoded table bytes (hg_block records): the first
+        key of a block is read from the record at its position."""
+        mv = memoryview(data).cast("B")
+        items = []
+        for b in blocks:
+            pos, ln = int(b["position"]), int(b["length"])
+            klen = int.from_bytes(mv[pos:pos + 8], "little")
+            items.append(Block(bytes(mv[pos + 16:pos + 16 + klen]), pos, ln))
+        return cls(items)
+
     def get(self, key):
         """src/sstable/index.rs:72-78: exact first-key match -> that block;
         otherwise the block before the insertion point; None before the

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 1
+#define HG_ABI_VERSION 2
 
 /* Status codes: return values, and the `kind` field of hg_err / results. */
 enum hg_status {
@@ -58,7 +58,11 @@ enum hg_status {
     HG_ERR_HIP = -2,
     HG_ERR_TOO_LARGE = -3,  /* input length >= 2^40 bytes (engine limit) */
     HG_ERR_INTERNAL = -4,   /* e.g. a bounded device spin timed out */
-    HG_ERR_EMPTY_MERGE = -5 /* merge of zero records; the reference panics (src/sstable/manager.rs:213) */
+    HG_ERR_EMPTY_MERGE = -5, /* merge of zero records; the reference panics (src/sstable/manager.rs:213) */
+    /* A merge input table is not strictly increasing by key.  Every table
+     * horreum writes is (BTreeMap flush, compaction output); the device
+     * merge requires it and reports the first offending record. */
+    HG_ERR_UNSORTED = -6
 };
 
 /* One decoded record: key at off+16, value at off+16+klen.
@@ -108,6 +112,16 @@ typedef struct hg_encode_result {
     int32_t kind;     /* HG_OK or HG_ERR_CAPACITY */
     uint32_t reserved;
 } hg_encode_result;
+
+/* Result of a merge / compaction.  kind: HG_OK, HG_ERR_CAPACITY,
+ * HG_ERR_EMPTY_MERGE, HG_ERR_UNSORTED (table, index = offending record), or
+ * a decode error of an input table (table, index = failing byte offset). */
+typedef struct hg_merge_result {
+    uint64_t n_out;  /* merged records (tombstones included) */
+    int32_t kind;
+    uint32_t table;
+    uint64_t index;
+} hg_merge_result;
 
 typedef struct hg_ctx hg_ctx;
 
@@ -177,6 +191,40 @@ int hg_encode_host(hg_ctx* ctx, const uint8_t* h_arena, uint64_t arena_len,
                    const hg_pair* h_pairs, uint64_t n, uint8_t* h_out,
                    uint64_t cap, uint64_t* h_rec_off, uint32_t block_stride,
                    hg_block* h_blocks, uint64_t* out_len);
+
+/* ---- merge (compaction) ------------------------------------------------
+ * Replaces SSTableManager::compact_inner (src/sstable/manager.rs:199-234),
+ * the k-way merge of SSTableManager::compact (:137-159).  ntables tables of
+ * decoded records live in one device arena: table t's bytes start at
+ * table_off[t] and its spans (offsets relative to that start) are
+ * d_spans[t][0..counts[t]).  Tables are in priority order: on equal keys the
+ * lowest t wins (compact() passes them newest first, :146-149).  Output:
+ * one hg_pair per distinct key, ascending, pointing into the arena
+ * (key_off/val_off relative to d_arena), tombstones kept -- ready for
+ * hg_encode_* to write the compacted table.  table_off, d_spans (an array of
+ * device pointers) and counts are host arrays.  Every table must be strictly
+ * increasing (else HG_ERR_UNSORTED); all tables empty is HG_ERR_EMPTY_MERGE
+ * (the reference panics). */
+int hg_merge_dev(hg_ctx* ctx, uint32_t ntables, const uint8_t* d_arena,
+                 uint64_t arena_len, const uint64_t* table_off,
+                 const hg_span* const* d_spans, const uint64_t* counts,
+                 hg_pair* d_out, uint64_t cap, hg_merge_result* result);
+int hg_merge_dev_async(hg_ctx* ctx, uint32_t ntables, const uint8_t* d_arena,
+                       uint64_t arena_len, const uint64_t* table_off,
+                       const hg_span* const* d_spans, const uint64_t* counts,
+                       hg_pair* d_out, uint64_t cap,
+                       hg_merge_result* d_result);
+/* The byte work of SSTableManager::compact (manager.rs:137-159) from host
+ * buffers: decode every table, merge (as hg_merge_dev), encode the merged
+ * records into h_out (the compacted SSTable, byte-identical to the
+ * reference's serialize_flatten of compact_inner's output) and its index
+ * blocks (optional, as hg_encode_host).  *out_len = encoded bytes; the
+ * compacted table's payload size (table.rs:36-45) is
+ * *out_len - 16 * result->n_out. */
+int hg_compact_host(hg_ctx* ctx, uint32_t ntables, const uint8_t* const* h_tables,
+                    const uint64_t* lens, uint8_t* h_out, uint64_t cap,
+                    uint64_t* out_len, uint32_t block_stride, hg_block* h_blocks,
+                    hg_merge_result* result);
 
 /* Number of blocks Index::new produces for n pairs: ceil(n / stride). */
 uint64_t hg_block_count(uint64_t n, uint32_t block_stride);

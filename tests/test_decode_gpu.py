@@ -175,6 +175,21 @@ def test_fake_headers_in_values(engine, fake):
         assert_same(engine, data[:cut])
 
 
+@pytest.mark.parametrize("split_mb", [1, 3])
+def test_stride_then_mixed(engine, split_mb):
+    """Uniform 16/100 records, then mixed sizes: the stride pre-pass resolves
+    (and predicts spans for) the head, the general engine the rest; spans the
+    pre-pass wrote at predicted indices past the break must be repaired."""
+    n1 = (split_mb << 20) // 132
+    arena1, pairs1 = corpus.fixed(n1, 16, 100, seed=41)
+    arena2, pairs2 = corpus.mixed(30000, 24, 300, seed=42)
+    d1, _, _, _ = oracle.encode(arena1, pairs1)
+    d2, _, _, _ = oracle.encode(arena2, pairs2)
+    tail = oracle.encode(*corpus.fixed(20000, 8, 56, seed=43))[0]  # stride again, other R
+    assert_same(engine, np.concatenate([d1, d2, tail]))
+    assert_same(engine, np.concatenate([d2, d1]))
+
+
 def test_many_chunks_mixed(engine):
     """~12 MiB of mixed records: thousands of chunks, look-back over many windows."""
     arena, pairs = corpus.mixed(200000, 24, 96, seed=31)

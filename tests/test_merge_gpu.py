@@ -1,0 +1,207 @@
+"""GPU parity: the device k-way merge (hg_merge_dev) and the host compaction
+entry point (hg_compact_host) vs the oracle restatement of
+SSTableManager::compact_inner (src/sstable/manager.rs:199-234): same records,
+same order, newest (lowest index) wins, tombstones kept.  Integer/byte work:
+bit-exact."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def sorted_tables(k, n_universe, frac, seed, long_prefix=False):
+    """k tables of sorted unique keys drawn from one universe (overlapping),
+    random values, ~10 % tombstones.  long_prefix: many keys share their
+    first 16+ bytes (exercises the byte-wise tail compare)."""
+    rng = np.random.default_rng(seed)
+    keys = set()
+    while len(keys) < n_universe:
+        if long_prefix and rng.random() < 0.5:
+            base = b"user/profile/000" + bytes([rng.integers(0, 4)]) * int(rng.integers(0, 3))
+            key = base + rng.integers(0, 256, size=int(rng.integers(0, 12)),
+                                      dtype=np.uint8).tobytes()
+        else:
+            key = rng.integers(0, 256, size=int(rng.integers(0, 24)), dtype=np.uint8).tobytes()
+        keys.add(key)
+    universe = sorted(keys)  # bytes order == Vec<u8> Ord (shorter prefix first)
+    tables = []
+    for t in range(k):
+        pick = [key for key in universe if rng.random() < frac]
+        pairs = []
+        for key in pick:
+            if rng.random() < 0.1:
+                pairs.append((key, None))
+            else:
+                pairs.append((key, rng.integers(0, 256, size=int(rng.integers(1, 40)),
+                                                dtype=np.uint8).tobytes() + bytes([t])))
+        tables.append(pairs)
+    return tables
+
+
+def encode_tables(tables):
+    out = []
+    for pairs in tables:
+        if not pairs:
+            out.append(np.zeros(0, np.uint8))
+            continue
+        arena, rec = oracle.pack_pairs(pairs)
+        out.append(oracle.encode(arena, rec)[0])
+    return out
+
+
+def device_merge(engine, datas, cap=None):
+    """Tables into one device arena, decoded there, merged there."""
+    import torch
+    offs, total = [], 0
+    for d in datas:
+        offs.append(total)
+        total += (d.size + 7) & ~7
+    host = np.zeros(max(total, 1), np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + d.size] = d
+    arena = torch.from_numpy(host).to(engine.device)
+    spans, counts = [], []
+    for o, d in zip(offs, datas):
+        if d.size == 0:
+            spans.append(None)
+            counts.append(0)
+            continue
+        out = engine.decode_dev(arena[o:], d.size)
+        assert out.kind == 0
+        spans.append(out.spans)
+        counts.append(out.n)
+    n = sum(counts)
+    cap = n if cap is None else cap
+    pairs = engine.empty(max(cap, 1) * 24)
+    res = engine.merge_dev(arena, offs, spans, counts, pairs, cap)
+    got = pairs[: min(res.n, cap) * 24].cpu().numpy().view(oracle.PAIR_DTYPE)
+    return res, got, host, offs
+
+
+def oracle_merge_pairs(datas, offs):
+    tabs = [(d, oracle.decode(d)[0]) for d in datas]
+    refs, rc = oracle.compact(tabs)
+    want = np.zeros(len(refs), dtype=oracle.PAIR_DTYPE)
+    for i, (t, r) in enumerate(refs):
+        s = tabs[t][1][r]
+        ko = offs[t] + int(s["off"]) + 16
+        want[i] = (ko, ko + int(s["klen"]), s["klen"], s["vlen"])
+    return want, rc
+
+
+def test_golden_compaction(engine, golden):
+    """src/sstable/manager.rs:327-358 (iterator order as the test passes it)."""
+    c = golden["compaction"]
+    tables = [[(bytes.fromhex(k), None if v is None else bytes.fromhex(v)) for k, v in t]
+              for t in c["iterators"]]
+    datas = encode_tables(tables)
+    res, got, host, _ = device_merge(engine, datas)
+    assert res.status == 0 and res.kind == 0
+    merged = [(host[p["key_off"]:p["key_off"] + p["klen"]].tobytes(),
+               host[p["val_off"]:p["val_off"] + p["vlen"]].tobytes() if p["vlen"] else None)
+              for p in got]
+    want = [(bytes.fromhex(k), None if v is None else bytes.fromhex(v)) for k, v in c["expected"]]
+    assert merged == want
+
+
+@pytest.mark.parametrize("k,n_universe,frac,seed,long_prefix", [
+    (1, 3000, 0.5, 1, False),
+    (2, 5000, 0.6, 2, False),
+    (3, 8000, 0.4, 3, True),
+    (5, 4000, 0.3, 4, True),
+    (8, 20000, 0.25, 5, False),
+    (8, 3000, 0.9, 6, True),   # heavy overlap
+    (13, 6000, 0.2, 7, False),  # odd run counts in every round
+])
+def test_merge_parity(engine, k, n_universe, frac, seed, long_prefix):
+    datas = encode_tables(sorted_tables(k, n_universe, frac, seed, long_prefix))
+    res, got, _, offs = device_merge(engine, datas)
+    want, rc = oracle_merge_pairs(datas, offs)
+    assert rc == 0 and res.status == 0
+    assert res.n == want.size
+    assert np.array_equal(got, want)
+
+
+def test_merge_with_empty_tables(engine):
+    tables = sorted_tables(4, 2000, 0.5, 9)
+    tables[1] = []
+    tables[3] = []
+    datas = encode_tables(tables)
+    res, got, _, offs = device_merge(engine, datas)
+    want, _ = oracle_merge_pairs(datas, offs)
+    assert res.status == 0 and np.array_equal(got, want)
+
+
+def test_merge_large(engine):
+    """~1.2 M records over 8 tables (thousands of tiles per round)."""
+    rng = np.random.default_rng(12)
+    universe = np.unique(rng.integers(0, 1 << 40, size=400_000, dtype=np.uint64))
+    datas = []
+    for t in range(8):
+        keys = np.sort(rng.choice(universe, size=150_000, replace=False))
+        kb = keys.astype(">u8").view(np.uint8).reshape(-1, 8)
+        n = keys.size
+        pairs = np.zeros(n, dtype=oracle.PAIR_DTYPE)
+        arena = np.concatenate([kb, np.full((n, 8), t, np.uint8)], axis=1).reshape(-1)
+        pairs["key_off"] = np.arange(n) * 16
+        pairs["val_off"] = np.arange(n) * 16 + 8
+        pairs["klen"] = 8
+        pairs["vlen"] = np.where(rng.random(n) < 0.05, 0, 8)
+        datas.append(oracle.encode(arena, pairs)[0])
+    res, got, _, offs = device_merge(engine, datas)
+    want, _ = oracle_merge_pairs(datas, offs)
+    assert res.status == 0 and np.array_equal(got, want)
+
+
+def test_merge_unsorted_and_empty(engine):
+    tables = sorted_tables(3, 500, 0.6, 13)
+    bad = list(tables[1])
+    bad[5], bad[6] = bad[6], bad[5]  # out of order
+    datas = encode_tables([tables[0], bad, tables[2]])
+    res, _, _, _ = device_merge(engine, datas)
+    assert res.status == res.kind == -6 and res.table == 1 and res.index == 6
+    dup = list(tables[2])
+    dup.insert(3, dup[3])  # duplicate key: not strictly increasing
+    res, _, _, _ = device_merge(engine, encode_tables([tables[0], dup]))
+    assert res.kind == -6 and res.table == 1 and res.index == 4
+    # every table empty / no tables: the reference panics (manager.rs:213)
+    res, _, _, _ = device_merge(engine, [np.zeros(0, np.uint8)] * 3)
+    assert res.kind == -5
+    res, _, _, _ = device_merge(engine, [])
+    assert res.kind == -5
+
+
+def test_merge_capacity(engine):
+    datas = encode_tables(sorted_tables(3, 3000, 0.5, 14))
+    res_full, full, _, offs = device_merge(engine, datas)
+    res, got, _, _ = device_merge(engine, datas, cap=100)
+    assert res.status == 5 and res.n == res_full.n
+    assert np.array_equal(got, full[:100])
+
+
+@pytest.mark.parametrize("stride", [0, 10])
+def test_compact_host(engine, stride):
+    """decode -> merge -> encode from host bytes == serialize_flatten of the
+    oracle's compact_inner output, and its index blocks."""
+    tables = sorted_tables(6, 6000, 0.35, 15, long_prefix=True)
+    datas = encode_tables(tables)
+    out = engine.compact_host([d.tobytes() for d in datas], block_stride=stride)
+    assert out.status == 0 and out.kind == 0
+    tabs = [(d, oracle.decode(d)[0]) for d in datas]
+    refs, _ = oracle.compact(tabs)
+    merged = [oracle.pairs_from_spans(tabs[t][0], tabs[t][1][r:r + 1])[0] for t, r in refs]
+    arena, rec = oracle.pack_pairs(merged)
+    want, _, blocks, _ = oracle.encode(arena, rec, block_stride=stride)
+    assert out.n == len(merged)
+    assert np.array_equal(out.data, want)
+    if stride:
+        assert np.array_equal(out.blocks, blocks)
+
+
+def test_compact_host_decode_error(engine):
+    tables = sorted_tables(3, 400, 0.6, 16)
+    datas = encode_tables(tables)
+    out = engine.compact_host([datas[0].tobytes(), datas[1][:-3].tobytes(), datas[2].tobytes()])
+    assert out.kind in (1, 2) and out.status == out.kind and out.table == 1
