@@ -23,6 +23,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -41,6 +43,8 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="repeat CPU baseline passes until this much CPU time is spent")
     p.add_argument("--no-encode", action="store_true", help="skip the config-3 encode leg")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the config-4 / config-5 (scaled) legs")
     return p.parse_args(argv)
 
 
@@ -49,6 +53,17 @@ def dist_env():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     return rank, world, local
+
+
+def shard_plan(rank, world):
+    """Weak scaling: every rank decodes its own full cfg2 table (independent
+    tables, no data-path exchange); only the seed differs per rank."""
+    return dict(CFG2, seed=CFG2["seed"] + 1000 * rank, rank=rank, world=world)
+
+
+def aggregate(wall_max_s, steps, world, bytes_per_rank):
+    """Whole-job rate: the bytes all ranks decoded / the slowest rank's time."""
+    return world * bytes_per_rank / (wall_max_s / steps) / GIB
 
 
 def max_over_ranks(value, world, device=None):
@@ -147,8 +162,9 @@ def main(argv=None):
     from horreum_amd.engine import Engine
 
     eng = Engine(local)
-    n, k, v = CFG2["n"], CFG2["k"], CFG2["v"]
-    sst = synth.fixed_sst(n, k, v, seed=CFG2["seed"] + 1000 * rank, device=device)
+    plan = shard_plan(rank, world)
+    n, k, v = plan["n"], plan["k"], plan["v"]
+    sst = synth.fixed_sst(n, k, v, seed=plan["seed"], device=device)
     L = sst.numel()
     eng.reserve(L, 0)
     spans = eng.empty(n * 16)
@@ -169,7 +185,7 @@ def main(argv=None):
           and bool((sp[:, 1] == (k | (v << 32))).all()))
 
     ms_step = wall / args.steps * 1e3
-    value = world * L / (wall / args.steps) / GIB
+    value = aggregate(wall, args.steps, world, L)
     mean_launch_ms = sum(launch_ms) / len(launch_ms)
     alg_bytes = L + 16 * n
     achieved = alg_bytes / (mean_launch_ms * 1e-3) / 1e9
@@ -178,6 +194,11 @@ def main(argv=None):
     extra = {}
     if not args.no_encode:
         extra["encode_cfg3"] = encode_leg(torch, eng, device, args, world, rank)
+    if not args.no_extra:
+        del spans
+        torch.cuda.empty_cache()
+        extra["multi_table_decode_cfg4"] = multi_table_leg(torch, eng, device, args, world, rank)
+        extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank)
 
     cpu = (cpu_baseline(sst, n, args.cpu_sample_mb, args.cpu_seconds)
            if (rank == 0 and world == 1) else None)
@@ -245,6 +266,104 @@ def encode_leg(torch, eng, device, args, world, rank):
             "ms_per_step": round(wall / steps * 1e3, 4), "records": n, "out_bytes": total,
             "roofline_frac": round(alg / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "achieved_GBs": round(alg / (mean_ms * 1e-3) / 1e9, 2), "parity_ok": bool(ok)}
+
+
+def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32):
+    """BASELINE config 4, this GPU's shard: 256 tables of <= 64 MiB (16 B
+    sorted keys, values uniform in [8, 4096] B, ~5 % tombstones, seed
+    4 + table) round-robin over 8 GPUs -> 32 tables per GPU, decoded by one
+    batched call (hg_decode_batch_dev_async: tables fan out over auxiliary
+    streams; device resident)."""
+    from horreum_amd import synth
+    tabs = []
+    for i in range(tables_per_gpu):
+        t = rank + world * i if world > 1 else i
+        v = synth.mixed_table_vlens(64 << 20, 8, 4096, 0.05, seed=4 + t)
+        keys = np.arange(v.size, dtype=np.uint64) * 7 + t
+        buf, offs = synth.keyed_table(keys, v, seed=4 + t, device=device)
+        tabs.append((buf, v.size))
+    total = sum(b.numel() for b, _ in tabs)
+    spans = [eng.empty(n * 16) for _, n in tabs]
+    res = eng.empty(24 * len(tabs))
+    bufs = [b for b, _ in tabs]
+    lens = [b.numel() for b in bufs]
+    caps = [n for _, n in tabs]
+
+    def step():
+        eng.decode_batch_dev_async(bufs, lens, spans, caps, res)
+
+    steps = max(1, args.steps // 4)
+    wall, ms = time_async(torch, step, steps, 1, world, device)
+    r = res.cpu().numpy()
+    ok = all(int(r[24 * i:24 * i + 8].view("<u8")[0]) == n and
+             int(r[24 * i + 8:24 * i + 12].view("<i4")[0]) == 0 for i, (_, n) in enumerate(tabs))
+    recs = sum(n for _, n in tabs)
+    mean_ms = sum(ms) / len(ms)
+    del tabs, spans, bufs
+    torch.cuda.empty_cache()
+    return {"value": round(aggregate(wall, steps, world, total), 3), "unit": "GiB/s",
+            "tables_per_gpu": tables_per_gpu, "bytes_per_gpu": total, "records_per_gpu": recs,
+            "ms_per_step": round(wall / steps * 1e3, 4),
+            "achieved_GBs": round((total + 16 * recs) / (mean_ms * 1e-3) / 1e9, 1),
+            "parity_ok": bool(ok)}
+
+
+def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000):
+    """BASELINE config 5 scaled to one GPU's share: 8 sorted tables of 1 M
+    records (16 B keys / 100 B values, 132 MB each), 25 % of each table's keys
+    shared by all tables.  Decode all, device merge (newest wins), encode the
+    merged table; the merge needs the record counts on the host, so the leg
+    is timed end to end with its two host syncs."""
+    from horreum_amd import synth
+    rng = np.random.default_rng(5 + 1000 * rank)
+    shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64))
+    bufs, offs_b, total = [], [], 0
+    for t in range(ntab):
+        own = rng.integers(0, 1 << 40, size=per_table - shared.size, dtype=np.uint64)
+        keys = np.unique(np.concatenate([shared, own]))
+        buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=50 + t, device=device)
+        bufs.append(buf)
+    sizes = [b.numel() for b in bufs]
+    for sz in sizes:
+        offs_b.append(total)
+        total += (sz + 7) & ~7
+    arena = torch.zeros(total, dtype=torch.uint8, device=device)
+    for o, b in zip(offs_b, bufs):
+        arena[o:o + b.numel()] = b
+    del bufs
+    caps = [sz // 16 for sz in sizes]
+    span_t = [eng.empty(c * 16) for c in caps]
+    nmax = sum(caps)
+    pairs = eng.empty(nmax * 24)
+    out = eng.empty(total)
+    eng.reserve(max(sizes), nmax)
+
+    def run():
+        counts = []
+        for o, sz, sp, c in zip(offs_b, sizes, span_t, caps):
+            d = eng.decode_dev(arena[o:], sz, spans=sp, cap=c)
+            counts.append(d.n)
+        m = eng.merge_dev(arena, offs_b, span_t, counts, pairs, nmax)
+        rc, out_len = eng.encode_dev(arena, pairs, m.n, out=out, cap=total)
+        return m, out_len
+
+    run()
+    torch.cuda.synchronize(device)
+    times = []
+    for _ in range(3):
+        barrier(world, device)
+        t0 = time.perf_counter()
+        m, out_len = run()
+        torch.cuda.synchronize(device)
+        times.append(time.perf_counter() - t0)
+    wall = max_over_ranks(sorted(times)[1], world, device)
+    in_bytes = sum(sizes)
+    del arena, span_t, pairs, out
+    torch.cuda.empty_cache()
+    return {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
+            "tables": ntab, "input_bytes_per_gpu": in_bytes, "merged_records": int(m.n),
+            "merged_bytes": int(out_len), "ms": round(wall * 1e3, 3),
+            "status": int(m.status)}
 
 
 if __name__ == "__main__":

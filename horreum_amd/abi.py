@@ -94,6 +94,8 @@ _PROTOS = {
     "hg_encode_host": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, _u8p, _u64, _vp, _u32, _vp,
                                       ctypes.POINTER(_u64)]),
     "hg_block_count": (_u64, [_u64, _u32]),
+    # batch decode(ctx, n, tables**, lens*, spans**, caps*, results)
+    "hg_decode_batch_dev_async": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     # merge(ctx, ntables, arena, arena_len, table_off*, spans**, counts*, out, cap, result)
     "hg_merge_dev": (ctypes.c_int, [_vp, _u32, _u8p, _u64, _vp, _vp, _vp, _vp, _u64,
                                     ctypes.POINTER(HgMergeResult)]),

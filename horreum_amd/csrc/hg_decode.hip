@@ -55,7 +55,7 @@ constexpr uint32_t GPT = NGRAN / THREADS;         // 4 granules per thread
 // one look-back and emission tail, during which its workgroup has no loads in
 // flight), between BATCH_MIN and BATCH (the LDS arrays' size).
 constexpr uint32_t BATCH = 64;
-constexpr uint32_t BATCH_MIN = 16;
+constexpr uint32_t BATCH_MIN = 4;
 constexpr uint32_t MAX_REC_PIECE = PIECE / 16;    // records per piece (>= 16 B each)
 constexpr uint32_t WALK_LOG = PIECE / 16;         // serial-walk batch
 constexpr uint32_t MAX_ROUNDS = 24;
@@ -1365,28 +1365,27 @@ uint64_t env_or(const char* name, uint64_t dflt) {
     return dflt;
 }
 
-// Pieces per pre-pass batch: 16 (256 KiB).  Measured on cfg2 (1 GiB, tools/
-// sweep_spec.sh): 8, 16, 32 and 64 pieces at 4-8 workgroups per CU all land
-// within 0.247-0.263 ms, 16 at the low end; HG_DECODE_SBP (a power of two in
-// [SPEC_BP_MIN, SPEC_BP]) overrides.  Pieces per general batch: about one
-// round of batches over decode_kernel's resident grid, rounded up to whole
-// pre-pass batches, in [BATCH_MIN, BATCH] (HG_DECODE_BP overrides).
-uint32_t spec_pieces(uint64_t npieces, uint32_t resident) {
-    using namespace hgk;
-    (void)npieces;
-    (void)resident;
-    const uint64_t want = env_or("HG_DECODE_SBP", 16);
-    uint32_t sbp = SPEC_BP_MIN;
-    while (sbp < SPEC_BP && sbp < want) sbp <<= 1;
-    return sbp;
+// Pieces per general batch: about one round of batches over decode_kernel's
+// resident grid (each batch pays one look-back + emission tail), a power of
+// two in [BATCH_MIN, BATCH] -- small tables get small batches so they still
+// fill the GPU (HG_DECODE_BP overrides).  Pieces per pre-pass batch:
+// min(16, general), so a general batch is whole pre-pass batches.  16 was
+// measured on cfg2 (1 GiB, tools/sweep_spec.sh: 8..64 pieces at 4-8
+// workgroups per CU all land within 0.247-0.263 ms, 16 at the low end);
+// HG_DECODE_SBP overrides.
+uint32_t pow2_in(uint64_t want, uint32_t lo, uint32_t hi) {
+    uint32_t v = lo;
+    while (v < hi && v < want) v <<= 1;
+    return v;
 }
-uint32_t general_pieces(uint64_t npieces, uint32_t resident, uint32_t sbp) {
+uint32_t general_pieces(uint64_t npieces, uint32_t resident) {
     using namespace hgk;
-    uint64_t bp = env_or("HG_DECODE_BP", (npieces + resident - 1) / resident);
-    bp = (bp + sbp - 1) / sbp * sbp;
-    if (bp < BATCH_MIN) bp = (BATCH_MIN + sbp - 1) / sbp * sbp;
-    if (bp > BATCH) bp = BATCH;  // BATCH is a multiple of every sbp
-    return (uint32_t)bp;
+    return pow2_in(env_or("HG_DECODE_BP", (npieces + resident - 1) / resident), BATCH_MIN, BATCH);
+}
+uint32_t spec_pieces(uint32_t bp) {
+    using namespace hgk;
+    const uint32_t s = pow2_in(env_or("HG_DECODE_SBP", 16), SPEC_BP_MIN, SPEC_BP);
+    return s < bp ? s : bp;
 }
 }  // namespace
 
@@ -1408,15 +1407,17 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
     a.spans = d_spans;
     a.cap = cap;
     a.result = d_result;
-    a.status = static_cast<unsigned long long*>(d_ws);
-    DecodeCtl* ctl = reinterpret_cast<DecodeCtl*>(a.status + 2 * l.nbatches);
+    // [DecodeCtl (2 words) | 2 status words per general batch] -- one memset
+    DecodeCtl* ctl = static_cast<DecodeCtl*>(d_ws);
+    a.status = static_cast<unsigned long long*>(d_ws) + 2;
     a.ticket = &ctl->ticket;
     a.scratch = reinterpret_cast<hg_span*>(static_cast<char*>(d_ws) + l.scratch_off);
     const uint32_t res_spec = resident_workgroups(decode_spec_kernel, 0);
     const uint32_t res_gen = d_diag ? resident_workgroups(decode_kernel<true>, 1)
                                     : resident_workgroups(decode_kernel<false>, 2);
-    a.sbp = spec_pieces(l.npieces, res_spec);
-    a.bp = general_pieces(l.npieces, res_gen, a.sbp);
+    (void)res_spec;
+    a.bp = general_pieces(l.npieces, res_gen);
+    a.sbp = spec_pieces(a.bp);
     a.nbatches = (uint32_t)((l.npieces + a.bp - 1) / a.bp);
     a.npieces = (uint32_t)l.npieces;
     a.hz = 8 - nb;
@@ -1429,7 +1430,8 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
     a.first_bad = fb;
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
     a.q = a.bp / a.sbp;
-    if (hipMemsetAsync(d_ws, 0, l.status_words * 8, stream) != hipSuccess) return HG_ERR_HIP;
+    if (hipMemsetAsync(d_ws, 0, (2 + 2 * (size_t)a.nbatches) * 8, stream) != hipSuccess)
+        return HG_ERR_HIP;
     // 1. stride pre-pass  2. chain check + record bases  3. spans of the resolved prefix
     // HG_DECODE_SPEC_PAD: extra dynamic LDS per pre-pass workgroup (bytes) to cap
     // its occupancy (experiments).

@@ -96,15 +96,26 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
     const uint32_t t = run_of(a, g);
     const uint64_t rec = g - a.run_off[t];
     const hg_span sp = a.spans[t][rec];
-    const uint8_t* k = a.arena + a.table_off[t] + sp.off + 16;
-    uint8_t b[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) b[i] = (uint32_t)i < sp.klen ? k[i] : 0;
+    const uint64_t kofs = a.table_off[t] + sp.off + 16;
+    const uint8_t* k = a.arena + kofs;
     uint64_t w0 = 0, w1 = 0;
+    if (kofs + 16 <= a.arena_len) {
+        // two unaligned 8-byte loads (native on gfx950), then mask past klen
+        uint64_t r0, r1;
+        __builtin_memcpy(&r0, k, 8);
+        __builtin_memcpy(&r1, k + 8, 8);
+        const uint32_t kl = sp.klen;
+        if (kl < 8) r0 &= kl ? (~0ull >> (64 - 8 * kl)) : 0ull;
+        if (kl < 16) r1 &= kl <= 8 ? 0ull : (~0ull >> (64 - 8 * (kl - 8)));
+        w0 = bswap64(r0);
+        w1 = bswap64(r1);
+    } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        w0 = (w0 << 8) | b[i];
-        w1 = (w1 << 8) | b[8 + i];
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t byte = (uint32_t)i < sp.klen ? k[i] : 0;
+            if (i < 8) w0 = (w0 << 8) | byte;
+            else w1 = (w1 << 8) | byte;
+        }
     }
     MEnt m;
     m.p0 = w0;

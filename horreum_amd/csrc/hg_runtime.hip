@@ -3,6 +3,7 @@
 // and the pinned host staging pipeline.  Kernels: hg_decode.hip,
 // hg_encode.hip.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -55,6 +56,12 @@ struct hg_ctx {
     PinBuf mstage;
     hipEvent_t mstage_ev = nullptr;
     bool mstage_busy = false;
+    // batched decode: auxiliary streams (fork/join on `stream`), one workspace each
+    static constexpr int kAux = 8;
+    int naux = 0;
+    hipStream_t aux[kAux] = {};
+    DevBuf aux_ws[kAux];
+    hipEvent_t fork_ev = nullptr, join_ev[kAux] = {};
 };
 
 namespace {
@@ -146,6 +153,12 @@ int hg_ctx_destroy(hg_ctx* c) {
     for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage})
         if (b->p) hipHostFree(b->p);
     if (c->mstage_ev) hipEventDestroy(c->mstage_ev);
+    for (int i = 0; i < c->naux; ++i) {
+        if (c->aux[i]) hipStreamDestroy(c->aux[i]);
+        if (c->aux_ws[i].p) hipFree(c->aux_ws[i].p);
+        if (c->join_ev[i]) hipEventDestroy(c->join_ev[i]);
+    }
+    if (c->fork_ev) hipEventDestroy(c->fork_ev);
     if (c->own) hipStreamDestroy(c->own);
     delete c;
     return HG_OK;
@@ -220,6 +233,76 @@ int hg_decode_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* d_span
         hipStreamSynchronize(c->stream) != hipSuccess)
         return HG_ERR_HIP;
     return finish_decode(*reinterpret_cast<hg_decode_result*>(c->hres.p), cap, n_out, err);
+}
+
+// Batched decode (many independent tables, e.g. the 256 tables of BASELINE
+// config 4): tables are spread round-robin over auxiliary streams forked from
+// the context stream and joined back into it, so small tables decode
+// concurrently instead of one after another.  Asynchronous; results land in
+// d_results[i].  HG_DECODE_STREAMS (1..8, default 4) sets the fan-out.
+static int ensure_aux(hg_ctx* c, int want) {
+    if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
+        return HG_ERR_HIP;
+    while (c->naux < want) {
+        const int i = c->naux;
+        if (hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) != hipSuccess)
+            return HG_ERR_HIP;
+        ++c->naux;
+    }
+    return HG_OK;
+}
+
+int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const* d_tables,
+                              const uint64_t* lens, hg_span* const* d_spans,
+                              const uint64_t* caps, hg_decode_result* d_results) {
+    if (!c || (ntables && (!d_tables || !lens || !d_spans || !caps || !d_results)))
+        return HG_ERR_INVALID_ARG;
+    for (uint32_t i = 0; i < ntables; ++i) {
+        if ((lens[i] && !d_tables[i]) || (caps[i] && !d_spans[i])) return HG_ERR_INVALID_ARG;
+        if (lens[i] >= kMaxLen) return HG_ERR_TOO_LARGE;
+    }
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    int fan = 4;
+    if (const char* e = getenv("HG_DECODE_STREAMS")) fan = atoi(e);
+    fan = std::max(1, std::min<int>(fan, hg_ctx::kAux));
+    fan = std::min<int>(fan, std::max<uint32_t>(ntables, 1));
+    int r = ensure_aux(c, fan);
+    if (r != HG_OK) return r;
+    // size every auxiliary workspace first (growing synchronises that stream)
+    for (int s = 0; s < fan; ++s) {
+        uint64_t need = 0;
+        for (uint32_t i = s; i < ntables; i += fan)
+            need = std::max<uint64_t>(need, hgk_decode_workspace_bytes(lens[i]));
+        DevBuf& b = c->aux_ws[s];
+        if (need > b.bytes) {
+            if (hipStreamSynchronize(c->aux[s]) != hipSuccess) return HG_ERR_HIP;
+            if (b.p) hipFree(b.p);
+            b.p = nullptr;
+            b.bytes = 0;
+            if (hipMalloc(&b.p, need) != hipSuccess) return HG_ERR_HIP;
+            b.bytes = need;
+        }
+    }
+    if (hipEventRecord(c->fork_ev, c->stream) != hipSuccess) return HG_ERR_HIP;
+    for (int s = 0; s < fan; ++s)
+        if (hipStreamWaitEvent(c->aux[s], c->fork_ev, 0) != hipSuccess) return HG_ERR_HIP;
+    for (uint32_t i = 0; i < ntables; ++i) {
+        const int s = (int)(i % (uint32_t)fan);
+        if (lens[i] == 0) {
+            if (hipMemsetAsync(d_results + i, 0, sizeof(hg_decode_result), c->aux[s]) != hipSuccess)
+                return HG_ERR_HIP;
+            continue;
+        }
+        r = hgk_decode_launch(d_tables[i], lens[i], d_spans[i], caps[i], d_results + i,
+                              c->aux_ws[s].p, c->aux[s]);
+        if (r != HG_OK) return r;
+    }
+    for (int s = 0; s < fan; ++s)
+        if (hipEventRecord(c->join_ev[s], c->aux[s]) != hipSuccess ||
+            hipStreamWaitEvent(c->stream, c->join_ev[s], 0) != hipSuccess)
+            return HG_ERR_HIP;
+    return HG_OK;
 }
 
 // Host bytes in, host spans out.  The file is pushed through two pinned

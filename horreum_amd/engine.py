@@ -104,6 +104,21 @@ class Engine:
         check(self.lib.hg_decode_dev_async(self.ctx, _ptr(sst), int(length), _ptr(spans),
                                            int(cap), _ptr(result)), "hg_decode_dev_async")
 
+    def decode_batch_dev_async(self, tables, lens, spans, caps, results):
+        """Decode many device tables concurrently (fan-out over auxiliary
+        streams, joined into the context stream).  `results`: device tensor of
+        at least len(tables) * 24 bytes (hg_decode_result records)."""
+        k = len(tables)
+        tp = (ctypes.c_void_p * max(k, 1))(*[t.data_ptr() for t in tables])
+        ln = (ctypes.c_uint64 * max(k, 1))(*[int(x) for x in lens])
+        sp = (ctypes.c_void_p * max(k, 1))(*[s.data_ptr() for s in spans])
+        cp = (ctypes.c_uint64 * max(k, 1))(*[int(x) for x in caps])
+        check(self.lib.hg_decode_batch_dev_async(self.ctx, k, ctypes.cast(tp, ctypes.c_void_p),
+                                                 ctypes.cast(ln, ctypes.c_void_p),
+                                                 ctypes.cast(sp, ctypes.c_void_p),
+                                                 ctypes.cast(cp, ctypes.c_void_p), _ptr(results)),
+              "hg_decode_batch_dev_async")
+
     def decode_host(self, data, cap=None):
         """Host bytes in, numpy SPAN_DTYPE array out (through pinned staging)."""
         buf = np.ascontiguousarray(np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8))

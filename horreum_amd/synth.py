@@ -72,3 +72,37 @@ def host_fixed_sst(n, k, v, seed):
             if b < 8 else 0
     rec[:, 16 + k:] = rng.integers(0, 256, size=(n, v), dtype=np.uint8)
     return rec.reshape(-1)
+
+
+def keyed_table(key_ids, vlens, seed, device):
+    """Encoded SSTable with 16-byte big-endian keys `key_ids` (sorted uint64,
+    host) and value lengths `vlens` (host; 0 = tombstone), random value bytes
+    from the device generator.  Returns (bytes tensor, record offsets host)."""
+    torch = _torch()
+    key_ids = np.asarray(key_ids, dtype=np.uint64)
+    vlens = np.asarray(vlens, dtype=np.int64)
+    n = key_ids.size
+    sizes = 32 + vlens
+    offs = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(sizes, out=offs[1:])
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    buf = torch.randint(0, 256, (int(offs[-1]),), dtype=torch.uint8, device=device, generator=g)
+    hdr = np.zeros((n, 32), dtype=np.uint8)
+    hdr[:, 0] = 16
+    hdr[:, 8:16] = vlens.astype("<u8").view(np.uint8).reshape(n, 8)
+    hdr[:, 24:32] = key_ids.astype(">u8").view(np.uint8).reshape(n, 8)
+    idx = torch.from_numpy(offs[:-1]).to(device)[:, None] + torch.arange(32, device=device)
+    buf[idx.view(-1)] = torch.from_numpy(hdr).to(device).view(-1)
+    return buf, offs
+
+
+def mixed_table_vlens(max_bytes, vmin, vmax, tomb_frac, seed):
+    """Value lengths of a table filled to <= max_bytes with 16-byte keys and
+    values uniform in [vmin, vmax] (tomb_frac of them tombstones)."""
+    rng = np.random.default_rng(seed)
+    est = int(max_bytes / (32 + (vmin + vmax) / 2 * (1 - tomb_frac))) + 64
+    v = rng.integers(vmin, vmax + 1, size=est)
+    v[rng.random(est) < tomb_frac] = 0
+    c = np.cumsum(32 + v)
+    return v[: int(np.searchsorted(c, max_bytes, side="right"))]

@@ -161,6 +161,17 @@ int hg_decode_dev(hg_ctx* ctx, const uint8_t* d_sst, uint64_t len,
 int hg_decode_dev_async(hg_ctx* ctx, const uint8_t* d_sst, uint64_t len,
                         hg_span* d_spans, uint64_t cap,
                         hg_decode_result* d_result);
+/* Many independent tables at once (the batched multi-table decode of
+ * BASELINE config 4; SSTableManager::new opens every table of a directory,
+ * src/sstable/manager.rs:47-55).  Table i: d_tables[i] (device), lens[i]
+ * bytes, spans to d_spans[i] (capacity caps[i]), result to d_results[i]
+ * (device array).  The host arrays are read during the call.  Tables decode
+ * concurrently on auxiliary streams forked from and joined back into the
+ * context stream; nothing is synchronised. */
+int hg_decode_batch_dev_async(hg_ctx* ctx, uint32_t ntables,
+                              const uint8_t* const* d_tables, const uint64_t* lens,
+                              hg_span* const* d_spans, const uint64_t* caps,
+                              hg_decode_result* d_results);
 /* Host-memory in and out (pinned staging, H2D -> decode -> D2H). */
 int hg_decode_host(hg_ctx* ctx, const uint8_t* h_sst, uint64_t len,
                    hg_span* h_spans, uint64_t cap,

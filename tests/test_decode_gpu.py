@@ -190,6 +190,31 @@ def test_stride_then_mixed(engine, split_mb):
     assert_same(engine, np.concatenate([d2, d1]))
 
 
+def test_batch_decode(engine):
+    """hg_decode_batch_dev_async: several tables (incl. empty and broken ones)
+    decoded concurrently on fanned-out streams; each equals its oracle."""
+    import torch
+    names = ["fixed_16_100", "mixed_small", "tiny", "large_values", "mixed_4k", "zero_values"]
+    datas = [corpus.make(nm)[2] for nm in names]
+    datas.append(np.zeros(0, np.uint8))
+    datas.append(datas[1][:-5])  # truncated
+    dev = [engine.to_device(d) for d in datas]
+    caps = [max(d.size // 16, 1) for d in datas]
+    spans = [engine.empty(c * 16) for c in caps]
+    res = engine.empty(24 * len(datas))
+    engine.decode_batch_dev_async(dev, [d.size for d in datas], spans, caps, res)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy()
+    for i, d in enumerate(datas):
+        ws, wn, wk, wo, _ = oracle.decode(d)
+        n = int(r[24 * i:24 * i + 8].view("<u8")[0])
+        kind = int(r[24 * i + 8:24 * i + 12].view("<i4")[0])
+        off = int(r[24 * i + 16:24 * i + 24].view("<u8")[0])
+        assert (n, kind, off if kind else 0) == (wn, wk, wo if wk else 0), names[i % len(names)]
+        got = engine.spans_to_numpy(spans[i], min(n, caps[i]))
+        assert np.array_equal(got, ws)
+
+
 def test_many_chunks_mixed(engine):
     """~12 MiB of mixed records: thousands of chunks, look-back over many windows."""
     arena, pairs = corpus.mixed(200000, 24, 96, seed=31)
