@@ -47,6 +47,8 @@ BLOCK_DTYPE = np.dtype([("first_rec", "<u8"), ("position", "<u8"), ("length", "<
 DECODE_RESULT_DTYPE = np.dtype([("n_records", "<u8"), ("kind", "<i4"), ("reserved", "<u4"),
                                 ("err_offset", "<u8")])
 ENCODE_RESULT_DTYPE = np.dtype([("out_len", "<u8"), ("kind", "<i4"), ("reserved", "<u4")])
+KEY_DTYPE = np.dtype([("off", "<u8"), ("len", "<u4"), ("reserved", "<u4")])
+LOOKUP_DTYPE = np.dtype([("rec", "<u8"), ("val_off", "<u8"), ("vlen", "<u4"), ("found", "<i4")])
 MERGE_RESULT_DTYPE = np.dtype([("n_out", "<u8"), ("kind", "<i4"), ("table", "<u4"),
                                ("index", "<u8")])
 
@@ -94,6 +96,10 @@ _PROTOS = {
     "hg_encode_host": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, _u8p, _u64, _vp, _u32, _vp,
                                       ctypes.POINTER(_u64)]),
     "hg_block_count": (_u64, [_u64, _u32]),
+    "hg_keyindex_bytes": (_u64, [_u64]),
+    "hg_keyindex_build_dev_async": (ctypes.c_int, [_vp, _u8p, _u64, _vp, _u64, _vp]),
+    "hg_lookup_dev_async": (ctypes.c_int, [_vp, _u8p, _vp, _vp, _u64, _u8p, _vp, _u64, _vp]),
+    "hg_lookup_host": (ctypes.c_int, [_vp, _u8p, _u64, _u8p, _u64, _vp, _u64, _vp]),
     # batch decode(ctx, n, tables**, lens*, spans**, caps*, results)
     "hg_decode_batch_dev_async": (ctypes.c_int, [_vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     # merge(ctx, ntables, arena, arena_len, table_off*, spans**, counts*, out, cap, result)

@@ -55,7 +55,10 @@ constexpr uint32_t GPT = NGRAN / THREADS;         // 4 granules per thread
 // one look-back and emission tail, during which its workgroup has no loads in
 // flight), between BATCH_MIN and BATCH (the LDS arrays' size).
 constexpr uint32_t BATCH = 64;
-constexpr uint32_t BATCH_MIN = 4;
+// Floor 16: with 4-piece batches a 64 MiB table has 1024 batches whose
+// speculative passes all end together, and each look-back then walks ~16
+// windows to the nearest INCL (cfg 4 measured 8.2 ms vs 4.7 ms at 16).
+constexpr uint32_t BATCH_MIN = 16;
 constexpr uint32_t MAX_REC_PIECE = PIECE / 16;    // records per piece (>= 16 B each)
 constexpr uint32_t WALK_LOG = PIECE / 16;         // serial-walk batch
 constexpr uint32_t MAX_ROUNDS = 24;
@@ -1367,8 +1370,7 @@ uint64_t env_or(const char* name, uint64_t dflt) {
 
 // Pieces per general batch: about one round of batches over decode_kernel's
 // resident grid (each batch pays one look-back + emission tail), a power of
-// two in [BATCH_MIN, BATCH] -- small tables get small batches so they still
-// fill the GPU (HG_DECODE_BP overrides).  Pieces per pre-pass batch:
+// two in [BATCH_MIN, BATCH] (HG_DECODE_BP overrides).  Pieces per pre-pass batch:
 // min(16, general), so a general batch is whole pre-pass batches.  16 was
 // measured on cfg2 (1 GiB, tools/sweep_spec.sh: 8..64 pieces at 4-8
 // workgroups per CU all land within 0.247-0.263 ms, 16 at the low end);

@@ -18,6 +18,12 @@ extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8
                                  uint64_t*, uint32_t, hg_block*, hg_encode_result*,
                                  unsigned long long*, hipStream_t);
 extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t);
+extern "C" uint64_t hgk_keyindex_bytes(uint64_t);
+extern "C" int hgk_keyindex_launch(const uint8_t*, uint64_t, const hg_span*, uint64_t, void*,
+                                   hipStream_t);
+extern "C" int hgk_lookup_launch(const uint8_t*, const hg_span*, const void*, uint64_t,
+                                 const uint8_t*, const hg_key*, uint64_t, hg_lookup_result*,
+                                 hipStream_t);
 extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
@@ -53,6 +59,7 @@ struct hg_ctx {
     PinBuf h_stage[2];
     // merge: workspace, result, pinned argument staging and its reuse event
     DevBuf mws, mres, mspans, mpairs;
+    DevBuf lk_index, lk_keys, lk_res;  // host lookup path
     PinBuf mstage;
     hipEvent_t mstage_ev = nullptr;
     bool mstage_busy = false;
@@ -148,7 +155,7 @@ int hg_ctx_destroy(hg_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->mws,
-                      &c->mres, &c->mspans, &c->mpairs})
+                      &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res})
         if (b->p) hipFree(b->p);
     for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage})
         if (b->p) hipHostFree(b->p);
@@ -626,6 +633,68 @@ int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
     delete[] counts;
     delete[] sp;
     return r;
+}
+
+// ---- point lookups -----------------------------------------------------------------
+uint64_t hg_keyindex_bytes(uint64_t n) { return hgk_keyindex_bytes(n); }
+
+int hg_keyindex_build_dev_async(hg_ctx* c, const uint8_t* d_table, uint64_t len,
+                                const hg_span* d_spans, uint64_t n, void* d_index) {
+    if (!c || (n && (!d_table || !d_spans || !d_index))) return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    return hgk_keyindex_launch(d_table, len, d_spans, n, d_index, c->stream);
+}
+
+int hg_lookup_dev_async(hg_ctx* c, const uint8_t* d_table, const hg_span* d_spans,
+                        const void* d_index, uint64_t n, const uint8_t* d_keys,
+                        const hg_key* d_queries, uint64_t nq, hg_lookup_result* d_results) {
+    if (!c || (nq && (!d_queries || !d_results)) || (n && nq && (!d_table || !d_spans || !d_index)))
+        return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    return hgk_lookup_launch(d_table, d_spans, d_index, n, d_keys, d_queries, nq, d_results,
+                             c->stream);
+}
+
+int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, const uint8_t* h_keys,
+                   uint64_t keys_len, const hg_key* h_queries, uint64_t nq,
+                   hg_lookup_result* h_results) {
+    if (!c || (len && !h_table) || (nq && (!h_queries || !h_results)) || (keys_len && !h_keys))
+        return HG_ERR_INVALID_ARG;
+    if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    for (uint64_t i = 0; i < nq; ++i)
+        if (h_queries[i].off + h_queries[i].len > keys_len) return HG_ERR_INVALID_ARG;
+    const uint64_t cap = len / 16;
+    int r;
+    if ((r = ensure(c, c->d_in, len ? len : 1)) != HG_OK) return r;
+    if ((r = ensure(c, c->d_out, (cap ? cap : 1) * sizeof(hg_span))) != HG_OK) return r;
+    if (len && (r = h2d_pipelined(c, c->d_in.p, h_table, len)) != HG_OK) return r;
+    uint64_t n = 0;
+    hg_err e{};
+    if (len) {
+        r = hg_decode_dev(c, static_cast<const uint8_t*>(c->d_in.p), len,
+                          static_cast<hg_span*>(c->d_out.p), cap, &n, &e);
+        if (r != HG_OK) return r;  // a table that does not decode cannot be searched
+    }
+    const size_t qat = (keys_len + 63) & ~(size_t)63;
+    if ((r = ensure(c, c->lk_index, (n ? n : 1) * 32)) != HG_OK) return r;
+    if ((r = ensure(c, c->lk_keys, qat + (nq ? nq : 1) * sizeof(hg_key))) != HG_OK) return r;
+    if ((r = ensure(c, c->lk_res, (nq ? nq : 1) * sizeof(hg_lookup_result))) != HG_OK) return r;
+    char* kd = static_cast<char*>(c->lk_keys.p);
+    if (keys_len && (r = h2d_pipelined(c, kd, h_keys, keys_len)) != HG_OK) return r;
+    if (nq && (r = h2d_pipelined(c, kd + qat, h_queries, nq * sizeof(hg_key))) != HG_OK) return r;
+    r = hg_keyindex_build_dev_async(c, static_cast<const uint8_t*>(c->d_in.p), len,
+                                    static_cast<const hg_span*>(c->d_out.p), n, c->lk_index.p);
+    if (r == HG_OK)
+        r = hg_lookup_dev_async(c, static_cast<const uint8_t*>(c->d_in.p),
+                                static_cast<const hg_span*>(c->d_out.p), c->lk_index.p, n,
+                                reinterpret_cast<const uint8_t*>(kd),
+                                reinterpret_cast<const hg_key*>(kd + qat), nq,
+                                static_cast<hg_lookup_result*>(c->lk_res.p));
+    if (r != HG_OK) return r;
+    if (nq && (r = d2h_pipelined(c, h_results, c->lk_res.p, nq * sizeof(hg_lookup_result))) != HG_OK)
+        return r;
+    return HG_OK;
 }
 
 }  // extern "C"

@@ -10,8 +10,8 @@ from collections import namedtuple
 
 import numpy as np
 
-from .abi import (BLOCK_DTYPE, PAIR_DTYPE, SPAN_DTYPE, HgErr, HgMergeResult, HorreumGpuError,
-                  Status, check, load_library)
+from .abi import (BLOCK_DTYPE, KEY_DTYPE, LOOKUP_DTYPE, PAIR_DTYPE, SPAN_DTYPE, HgErr,
+                  HgMergeResult, HorreumGpuError, Status, check, load_library)
 
 DecodeOut = namedtuple("DecodeOut", "spans n kind offset")
 EncodeOut = namedtuple("EncodeOut", "data rec_off blocks out_len")
@@ -180,6 +180,45 @@ class Engine:
         return EncodeOut(out[:total], rec_off[:n] if rec_off is not None else None,
                          blocks[:nb] if blocks is not None else None, out_len.value)
 
+
+    # ---- point lookups ----------------------------------------------------------------
+    @staticmethod
+    def pack_keys(keys):
+        """[bytes] -> (key arena uint8, KEY_DTYPE descriptors)."""
+        keys = [bytes(k) for k in keys]
+        desc = np.zeros(len(keys), dtype=KEY_DTYPE)
+        off = 0
+        for i, k in enumerate(keys):
+            desc[i] = (off, len(k), 0)
+            off += len(k)
+        arena = np.frombuffer(b"".join(keys), dtype=np.uint8) if off else np.zeros(1, np.uint8)
+        return arena, desc
+
+    def lookup_host(self, table, keys):
+        """SSTable::get for many keys (src/sstable/table.rs:54-70) on host
+        table bytes -> LOOKUP_DTYPE results (found, rec, val_off, vlen)."""
+        buf = np.ascontiguousarray(np.frombuffer(memoryview(table).cast("B"), dtype=np.uint8))
+        arena, desc = self.pack_keys(keys)
+        out = np.zeros(max(len(desc), 1), dtype=LOOKUP_DTYPE)
+        check(self.lib.hg_lookup_host(self.ctx, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
+                                      arena.ctypes.data_as(ctypes.c_void_p),
+                                      int(desc["len"].sum()) if desc.size else 0,
+                                      desc.ctypes.data_as(ctypes.c_void_p), desc.size,
+                                      out.ctypes.data_as(ctypes.c_void_p)), "hg_lookup_host")
+        return out[: desc.size]
+
+    def keyindex_build(self, table, spans, n):
+        """Device key index (32 B per record) of a decoded device table."""
+        idx = self.empty(max(int(self.lib.hg_keyindex_bytes(n)), 1))
+        check(self.lib.hg_keyindex_build_dev_async(self.ctx, _ptr(table), table.numel(),
+                                                   _ptr(spans), int(n), _ptr(idx)),
+              "hg_keyindex_build_dev_async")
+        return idx
+
+    def lookup_dev_async(self, table, spans, index, n, keys, queries, nq, results):
+        check(self.lib.hg_lookup_dev_async(self.ctx, _ptr(table), _ptr(spans), _ptr(index), int(n),
+                                           _ptr(keys), _ptr(queries), int(nq), _ptr(results)),
+              "hg_lookup_dev_async")
 
     # ---- merge / compaction -----------------------------------------------------------
     def merge_dev(self, arena, table_off, spans, counts, out, cap):

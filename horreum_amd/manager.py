@@ -58,6 +58,26 @@ class SSTableManager:
                 return pair
         return None
 
+    def get_many(self, keys):
+        """get() for a batch of keys: one device lookup launch per table,
+        newest table first; a key stops at the first table that holds it
+        (tombstones included, as manager.rs:126-134)."""
+        keys = [bytes(k) for k in keys]
+        out = [None] * len(keys)
+        todo = list(range(len(keys)))
+        for table in reversed(self.tables):
+            if not todo:
+                break
+            got = table.get_many([keys[i] for i in todo], self.engine)
+            left = []
+            for i, g in zip(todo, got):
+                if g is None:
+                    left.append(i)
+                else:
+                    out[i] = g
+            todo = left
+        return out
+
     def should_compact(self):
         """manager.rs:170-194: the compacted size, or None."""
         if not self.tables:

@@ -119,6 +119,25 @@ class SSTable:
         i = bisect.bisect_left(keys, key)
         return pairs[i] if i < len(keys) and keys[i] == key else None
 
+    def get_many(self, keys, engine=None):
+        """SSTable::get for a batch of keys in one device launch (the table is
+        read once, decoded, indexed and searched on the GPU).  Returns one
+        InternalPair (tombstones included) or None per key."""
+        from .engine import default_engine
+        from .format import InternalPair
+        eng = engine or default_engine()
+        data = self.file.read_bytes()
+        res = eng.lookup_host(data, keys)
+        mv = memoryview(data)
+        out = []
+        for k, r in zip(keys, res):
+            if not r["found"]:
+                out.append(None)
+                continue
+            vo, vl = int(r["val_off"]), int(r["vlen"])
+            out.append(InternalPair(k, mv[vo:vo + vl] if vl else None))
+        return out
+
     def get_all(self, engine=None):
         """table.rs:73-75."""
         return self.file.read_all(engine)

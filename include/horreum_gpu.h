@@ -123,6 +123,23 @@ typedef struct hg_merge_result {
     uint64_t index;
 } hg_merge_result;
 
+/* A lookup key: bytes [off, off+len) of a caller key arena. */
+typedef struct hg_key {
+    uint64_t off;
+    uint32_t len;
+    uint32_t reserved;
+} hg_key;
+
+/* Result of one point lookup.  found = 1: record `rec` holds the key (value
+ * at table byte val_off, vlen bytes; vlen == 0 is a tombstone, i.e. the
+ * reference's Some(InternalPair{value: None})).  found = 0: absent. */
+typedef struct hg_lookup_result {
+    uint64_t rec;
+    uint64_t val_off;
+    uint32_t vlen;
+    int32_t found;
+} hg_lookup_result;
+
 typedef struct hg_ctx hg_ctx;
 
 /* ---- library / context ---------------------------------------------- */
@@ -236,6 +253,26 @@ int hg_compact_host(hg_ctx* ctx, uint32_t ntables, const uint8_t* const* h_table
                     const uint64_t* lens, uint8_t* h_out, uint64_t cap,
                     uint64_t* out_len, uint32_t block_stride, hg_block* h_blocks,
                     hg_merge_result* result);
+
+/* ---- point lookups ----------------------------------------------------
+ * Replaces SSTable::get (src/sstable/table.rs:54-70; Index::get,
+ * src/sstable/index.rs:72-78) for a batch of keys.  The table is decoded
+ * (d_spans, n records) and must be strictly increasing by key, as every
+ * table horreum writes is; then the record whose key equals each query is
+ * what the reference's block-index path returns.  First build the key index
+ * once per table (32 * n bytes of device memory at d_index), then look up
+ * any number of batches. */
+uint64_t hg_keyindex_bytes(uint64_t n);
+int hg_keyindex_build_dev_async(hg_ctx* ctx, const uint8_t* d_table, uint64_t len,
+                                const hg_span* d_spans, uint64_t n, void* d_index);
+int hg_lookup_dev_async(hg_ctx* ctx, const uint8_t* d_table, const hg_span* d_spans,
+                        const void* d_index, uint64_t n, const uint8_t* d_keys,
+                        const hg_key* d_queries, uint64_t nq,
+                        hg_lookup_result* d_results);
+/* Host table bytes and host keys: decode, index, look up, copy back. */
+int hg_lookup_host(hg_ctx* ctx, const uint8_t* h_table, uint64_t len,
+                   const uint8_t* h_keys, uint64_t keys_len, const hg_key* h_queries,
+                   uint64_t nq, hg_lookup_result* h_results);
 
 /* Number of blocks Index::new produces for n pairs: ceil(n / stride). */
 uint64_t hg_block_count(uint64_t n, uint32_t block_stride);

@@ -141,6 +141,42 @@ found:
     return 1;
 }
 
+/* src/sstable/table.rs:54-70 (SSTable::get) on a decoded table: the block
+ * index of Index::new (index.rs:55-67, blocks of `stride` records), its get
+ * (index.rs:72-78: exact first key -> that block, else the block before the
+ * insertion point, none before the first block), then binary_search_by_key
+ * over the block's records.  Returns 1 and the record index if found. */
+int hgo_table_get(const uint8_t* data, const hg_span* spans, uint64_t n, uint32_t stride,
+                  const uint8_t* key, uint64_t klen, uint64_t* rec) {
+    if (n == 0 || stride == 0) return 0;
+    const uint64_t nb = (n + stride - 1) / stride;
+    uint64_t lo = 0, hi = nb; /* first block whose first key >= key */
+    while (lo < hi) {
+        uint64_t mid = lo + (hi - lo) / 2;
+        const hg_span* s = &spans[mid * stride];
+        if (key_cmp(data + s->off + 16, s->klen, key, klen) < 0) lo = mid + 1;
+        else hi = mid;
+    }
+    uint64_t b;
+    if (lo < nb && key_cmp(data + spans[lo * stride].off + 16, spans[lo * stride].klen, key, klen) == 0)
+        b = lo;
+    else if (lo == 0)
+        return 0;
+    else
+        b = lo - 1;
+    /* binary_search_by_key within the block's records */
+    uint64_t r0 = b * stride, r1 = r0 + stride < n ? r0 + stride : n;
+    uint64_t l = r0, h = r1;
+    while (l < h) {
+        uint64_t mid = l + (h - l) / 2;
+        int c = key_cmp(data + spans[mid].off + 16, spans[mid].klen, key, klen);
+        if (c == 0) { if (rec) *rec = mid; return 1; }
+        if (c < 0) l = mid + 1;
+        else h = mid;
+    }
+    return 0;
+}
+
 /* src/sstable/manager.rs:199-234. */
 int hgo_compact(uint32_t ntables, const uint8_t* const* datas,
                 const hg_span* const* spans, const uint64_t* counts,

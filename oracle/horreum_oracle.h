@@ -48,6 +48,10 @@ int hgo_compact(uint32_t ntables, const uint8_t* const* datas,
                 uint64_t* n_out);
 
 /* SSTable::open size accounting: sum(klen + vlen) (src/sstable/table.rs:36-45). */
+/* src/sstable/table.rs:54-70: SSTable::get on a decoded table. */
+int hgo_table_get(const uint8_t* data, const hg_span* spans, uint64_t n, uint32_t stride,
+                  const uint8_t* key, uint64_t klen, uint64_t* rec);
+
 uint64_t hgo_payload_size(const hg_span* spans, uint64_t n);
 
 /* CPU baselines.  Decode with the reference's per-record ownership pattern

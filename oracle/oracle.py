@@ -44,6 +44,9 @@ def lib():
         L.hgo_compact.argtypes = [u32, vp, vp, vp, vp, vp, u64, ctypes.POINTER(u64)]
         L.hgo_payload_size.argtypes = [vp, u64]
         L.hgo_payload_size.restype = u64
+        L.hgo_table_get.argtypes = [vp, vp, u64, ctypes.c_uint32, vp, u64,
+                                    ctypes.POINTER(u64)]
+        L.hgo_table_get.restype = ctypes.c_int
         L.hgo_bench_decode_owned.argtypes = [vp, u64, ctypes.POINTER(ctypes.c_double)]
         L.hgo_bench_decode_owned.restype = u64
         L.hgo_bench_encode_owned.argtypes = [vp, vp, u64, ctypes.POINTER(ctypes.c_double)]
@@ -137,6 +140,18 @@ def compact(tables_newest_first):
     rc = lib().hgo_compact(T, ctypes.cast(dptr, ctypes.c_void_p), ctypes.cast(sptr, ctypes.c_void_p),
                            _p(counts), _p(ot), _p(orr), cap, ctypes.byref(n))
     return list(zip(ot[: n.value].tolist(), orr[: n.value].tolist())), rc
+
+
+def table_get(data, spans, stride, key):
+    """SSTable::get (src/sstable/table.rs:54-70) on a decoded table: the
+    record index holding `key`, or None."""
+    buf = _u8(data)
+    spans = np.ascontiguousarray(spans, dtype=SPAN_DTYPE)
+    kb = np.frombuffer(bytes(key) or b"\0", dtype=np.uint8)
+    rec = ctypes.c_uint64()
+    hit = lib().hgo_table_get(_p(buf), _p(spans), spans.size, stride, _p(kb), len(key),
+                              ctypes.byref(rec))
+    return rec.value if hit else None
 
 
 def payload_size(spans):

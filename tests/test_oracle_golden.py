@@ -137,3 +137,19 @@ def test_payload_size(golden):
         _, _, data, _, _ = _encode(lst)
         spans, *_ = oracle.decode(data)
         assert oracle.payload_size(spans) == want
+
+
+def test_oracle_table_get(golden):
+    """src/sstable/table.rs:110-144 through the oracle's SSTable::get."""
+    c = golden["table_search"]
+    pairs = [(bytes.fromhex(k), None if v is None else bytes.fromhex(v)) for k, v in c["pairs"]]
+    arena, rec = oracle.pack_pairs(pairs)
+    data = oracle.encode(arena, rec)[0]
+    spans = oracle.decode(data)[0]
+    for key, want in c["gets"]:
+        r = oracle.table_get(data, spans, c["stride"], bytes.fromhex(key))
+        if want is None:
+            assert r is None
+        else:
+            got = oracle.pairs_from_spans(data, spans[r:r + 1])[0]
+            assert got == (bytes.fromhex(want[0]), None if want[1] is None else bytes.fromhex(want[1]))
