@@ -108,6 +108,18 @@ class SSTableManager:
         self.tables.append(SSTable(f, Index.from_encoded(data, out.blocks), size))
         return True
 
+    def flush_arena(self, arena, desc, size):
+        """The Flush command fed by MemTable.flush: one encode writes the new
+        table and its index straight from the memtable arena, then maybe
+        compact (manager.rs:104-114)."""
+        eng = self.engine or default_engine()
+        out = eng.encode_host(arena, desc, block_stride=self.block_stride)
+        data = out.data.tobytes()
+        f = PersistedFile(self._new_table_path())
+        f.write_bytes(data)
+        self.tables.append(SSTable(f, Index.from_encoded(data, out.blocks), size))
+        self.compact()
+
     def flush(self, pairs, size):
         """The Flush command (manager.rs:104-114): create, then maybe compact."""
         self.create(pairs, size)

@@ -1,0 +1,123 @@
+"""MemTable bookkeeping and flush path (reference src/memtable/mod.rs): the
+reference's own tests, size-accounting parity with the oracle restatement
+over random operation sequences (including the usize wrap of a shorter
+re-put), the arena snapshot, and -- on the GPU -- flush -> encode -> table."""
+import numpy as np
+import pytest
+
+from horreum_amd.memtable import MemTable
+from oracle import oracle
+from oracle.memtable import RefMemTable
+
+MEMTABLE_SIZE = 128  # mod.rs:163
+
+
+def test_put_and_get():
+    """mod.rs:165-180."""
+    t = MemTable(MEMTABLE_SIZE)
+    assert t.put(b"abc", b"def") is None
+    assert t.put(b"xyz", b"xxx") is None
+    assert t.put(b"xyz", b"qwerty") == b"xxx"
+    assert t.get(b"abc") == b"def"
+    assert t.get(b"xyz") == b"qwerty"
+
+
+def test_delete():
+    """mod.rs:182-195."""
+    t = MemTable(MEMTABLE_SIZE)
+    t.put(b"abc", b"def")
+    t.put(b"xyz", b"xxx")
+    assert t.delete(b"abc") == b"def"
+    assert t.delete(b"abcdef") is None
+    assert t.get(b"abc") is None
+    assert t.get(b"111") is None
+    assert t.get(b"xyz") == b"xxx"
+
+
+def test_delete_non_existing():
+    """mod.rs:197-204."""
+    t = MemTable(MEMTABLE_SIZE)
+    assert t.delete(b"abc") is None
+    assert t.get(b"abc") is None
+
+
+def _ops(seed, n=3000):
+    rng = np.random.default_rng(seed)
+    keys = [bytes([97 + i % 26]) * int(1 + i % 5) + bytes([i]) for i in range(60)]
+    ops = []
+    for _ in range(n):
+        k = keys[int(rng.integers(0, len(keys)))]
+        if rng.random() < 0.25:
+            ops.append(("del", k, None))
+        else:
+            ops.append(("put", k, bytes(int(rng.integers(0, 40)))))
+    return ops
+
+
+@pytest.mark.parametrize("seed,limit", [(1, 128), (2, 256), (3, 700)])
+def test_size_accounting_parity(seed, limit):
+    flushed = []
+    t = MemTable(limit, on_flush=lambda arena, desc, size: flushed.append((arena, desc, size)))
+    ref = RefMemTable(limit)
+    for op, k, v in _ops(seed):
+        if op == "put":
+            assert t.put(k, v) == ref.put(k, v)
+        else:
+            assert t.delete(k) == ref.delete(k)
+        assert t.actual_size == ref.actual_size
+    assert len(flushed) == len(ref.flushes) > 0
+    for (arena, desc, size), (pairs, rsize) in zip(flushed, ref.flushes):
+        assert size == rsize
+        got = [(arena[p["key_off"]:p["key_off"] + p["klen"]].tobytes(),
+                arena[p["val_off"]:p["val_off"] + p["vlen"]].tobytes() if p["vlen"] else None)
+               for p in desc]
+        # Some(b"") and None are the same record on the wire (src/format.rs:29-33)
+        assert got == [(k, v if v else None) for k, v in pairs]
+
+
+def test_delete_created_key_never_counts_its_key():
+    """A key first written by delete() is inserted as a tombstone without
+    counting (mod.rs:113-118); a later put over it adds only the value length
+    (mod.rs:88-90), so its key length is never counted."""
+    t, ref = MemTable(10 ** 6), RefMemTable(10 ** 6)
+    for m in (t, ref):
+        m.delete(b"ghost-key")
+        m.put(b"ghost-key", b"12345")
+        m.put(b"k", b"vv")
+    assert t.actual_size == ref.actual_size == 5 + 1 + 2
+    for m in (t, ref):
+        m.put(b"k", b"v")  # shorter re-put: += 1 - 2 (usize arithmetic)
+    assert t.actual_size == ref.actual_size == 7
+
+
+@pytest.mark.gpu
+def test_flush_to_table(engine, tmp_path):
+    """Memtable flush -> one device encode -> SSTable file == the oracle's
+    serialize_flatten of the sorted pairs; index blocks from the same launch."""
+    from horreum_amd.manager import SSTableManager
+    m = SSTableManager(tmp_path, 3, 10 ** 6, engine)
+    t = MemTable(300, on_flush=m.flush_arena)
+    ref = RefMemTable(300)
+    for op, k, v in _ops(7, 800):
+        if op == "put":
+            t.put(k, v)
+            ref.put(k, v)
+        else:
+            t.delete(k)
+            ref.delete(k)
+    assert len(m.tables) == len(ref.flushes) > 1
+    for table, (pairs, size) in zip(m.tables, ref.flushes):
+        arena, rec = oracle.pack_pairs(pairs)
+        want, _, blocks, _ = oracle.encode(arena, rec, block_stride=3)
+        assert open(table.file.path, "rb").read() == want.tobytes()
+        assert table.get_size() == size
+        assert [(b.position, b.length) for b in table.index.items] == \
+            [(int(b["position"]), int(b["length"])) for b in blocks]
+    # newest flush wins for a key flushed twice
+    last = {}
+    for pairs, _ in ref.flushes:
+        for k, v in pairs:
+            last[k] = v
+    for k, v in list(last.items())[:50]:
+        got = m.get(k)
+        assert got is not None and got.key == k and got.value == (v if v else None)
