@@ -12,8 +12,9 @@ Prints ONE JSON line (rank 0).  `roofline` prices one decode call against
 HBM: algorithmic bytes = L + 16 n (read the table once, write 16-byte spans),
 divided by the call's duration measured with HIP events on the stream its
 kernels run on.  A decode call is a short pipeline (status memset,
-decode_spec_kernel, decode_scan_kernel, decode_emit_kernel, decode_kernel);
-the stride pre-pass dominates (profiles/).  `cpu_baseline` times the oracle
+decode_spec_kernel, decode_kernel -- the latter writes the spans of the
+pre-pass's resolved prefix and runs the general engine on the rest); the
+stride pre-pass dominates (profiles/).  `cpu_baseline` times the oracle
 (the C restatement of the reference's Rust decode, with its per-record
 ownership pattern) on one host core over the same bytes.
 """
@@ -86,8 +87,7 @@ def barrier(world, device=None):
             dist.barrier()
 
 
-DECODE_KERNELS = ("decode_spec_kernel", "decode_scan_kernel", "decode_emit_kernel",
-                  "decode_kernel")
+DECODE_KERNELS = ("decode_spec_kernel", "decode_kernel")
 
 
 def load_traffic(kernels):
@@ -225,7 +225,7 @@ def main(argv=None):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "kernel": "decode call: status memset + decode_spec_kernel (dominant) + "
-                                   "decode_scan_kernel + decode_emit_kernel + decode_kernel",
+                                   "decode_kernel (prefix spans + general engine)",
                          "alg_bytes_per_launch": alg_bytes,
                          "mean_launch_ms": round(mean_launch_ms, 5)},
             "cpu_baseline": cpu,

@@ -84,10 +84,13 @@ struct DecodeArgs {
     uint32_t hz;                 // zero high bytes required in klen/vlen
     uint32_t bp;                 // pieces per batch (BATCH_MIN..BATCH)
     uint32_t* diag;              // DIAG builds only: DIAG_WORDS per batch
-    // Stride pre-pass results (decode_spec/scan kernels): batches of SPEC_BP
-    // pieces [0, *first_bad) are resolved and emitted already.
-    const struct SpecBatch* sbatch;
-    const uint32_t* first_bad;
+    // Stride pre-pass results (decode_spec_kernel): batches of SPEC_BP
+    // pieces [0, first_bad) are resolved; decode_kernel writes their spans.
+    struct SpecBatch* sbatch;
+    const struct SpecPiece* spiece;
+    struct DecodeCtl* ctl;
+    unsigned long long* gsum;    // records per group of SPEC_GROUP pre-pass batches
+    unsigned long long* link;    // per adjacent pre-pass batch pair: arrivals | exit - x0
     uint32_t nspec;              // stride pre-pass batches
     uint32_t sbp;                // pieces per pre-pass batch (SPEC_BP_MIN..SPEC_BP)
     uint32_t q;                  // pre-pass batches per general batch (bp / sbp)
@@ -101,16 +104,19 @@ struct SpecBatch {                // one per pre-pass batch
     uint64_t exit;                // first record start at or after the batch end
     uint32_t count;               // records starting in the batch
     uint32_t ok;                  // every piece verified as a stride run from x0
-    uint64_t gbase;               // record index of x0 (scan; valid below first_bad)
+    uint64_t pad;
 };
 
 // Control words of a decode call (zeroed with the statuses before launch).
 struct DecodeCtl {
     uint32_t ticket;              // decode_kernel batch tickets
-    uint32_t reserved;
-    uint32_t first_bad;           // first pre-pass batch not resolved (scan)
-    uint32_t reserved2;
+    uint32_t bad_rev;             // max over unresolved pre-pass batches b of nspec - b
+    uint32_t reserved[2];
 };
+constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
+__device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
+    return nspec - c->bad_rev;       // bad_rev 0 (nothing bad) -> nspec
+}
 struct SpecPiece {                // one per piece of an ok pre-pass batch
     uint64_t x, R;
     uint32_t kl, vl, count, pad;
@@ -893,6 +899,37 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
 }
 
 // ---- kernel ------------------------------------------------------------------------
+// The pre-pass batch's link check: batch j is good iff it verified and its
+// guessed entry is its predecessor's exit (batch 0: entry 0).  Both batches of
+// a pair add into one 64-bit word -- an arrival in the top byte, exit resp.
+// -x0 mod 2^48 below -- so whichever arrives second sees the whole sum in the
+// value its atomic returns.  No fences: an agent-scope release on gfx950
+// writes back and invalidates the XCD's L2, which stalls the streaming
+// workgroups around it (measured: 205 -> 755 us for the pre-pass).  Offsets
+// are < 2^40 (HG_ERR_TOO_LARGE), so the 48-bit sum is exact.
+constexpr uint64_t LINK_ONE = 1ull << 56, LINK_MASK = (1ull << 48) - 1;
+__device__ __forceinline__ void mark_bad(DecodeCtl* c, uint32_t nspec, uint32_t j) {
+    atomicMax(&c->bad_rev, nspec - j);
+}
+__device__ __forceinline__ void link_arrive(const DecodeArgs& a, uint32_t j, uint64_t v) {
+    const unsigned long long add = LINK_ONE | (v & LINK_MASK);
+    const unsigned long long old = atomicAdd(&a.link[j], add);
+    if ((old >> 56) == 1 && ((old + add) & LINK_MASK) != 0) mark_bad(a.ctl, a.nspec, j);
+}
+
+// Record base of pre-pass batch e (all batches below e resolved): the group
+// sums before e's group plus the counts before e inside it.  One wave, one
+// round of independent loads (plus one per 64 further groups).
+__device__ uint64_t spec_base(const DecodeArgs& a, uint32_t e) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t g = e / SPEC_GROUP;
+    uint64_t v = 0;
+    for (uint32_t k = lane; k < g; k += 64) v += a.gsum[k];
+    const uint32_t j = g * SPEC_GROUP + lane;
+    if (j < e) v += a.sbatch[j].count;
+    return wave_sum<uint64_t>(v);
+}
+
 template <bool DIAG>
 __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
     __shared__ DecodeSmem s;
@@ -904,19 +941,60 @@ __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
         if (DIAG && tid == 0) dg[slot] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start); \
     } while (0)
 
-    const uint32_t fb = *a.first_bad;
-    if (fb >= a.nspec) return;  // the stride pre-pass resolved the whole file
+    // ---- spans of the pre-pass's resolved prefix (workgroup e = batch e) ----------
+    const uint32_t fb = first_bad(a.ctl, a.nspec);
+    if (blockIdx.x < fb) {
+        const uint32_t e = blockIdx.x;
+        const uint32_t ep0 = e * a.sbp;
+        const uint32_t enp = min(a.sbp, a.npieces - ep0);
+        SpecPiece* pc = reinterpret_cast<SpecPiece*>(s.data64);            // LDS scratch
+        uint64_t* pbase = reinterpret_cast<uint64_t*>(pc + SPEC_BP);
+        if (tid < enp) pc[tid] = a.spiece[ep0 + tid];
+        if (tid < 64) {
+            const uint64_t base = spec_base(a, e);
+            if (tid == 0) s.xk = base;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            uint64_t g = s.xk;
+            for (uint32_t i = 0; i < enp; ++i) {
+                pbase[i] = g;
+                g += pc[i].count;
+            }
+            if (e == a.nspec - 1) {  // the whole file resolved: report it
+                hg_decode_result r;
+                r.n_records = g;
+                r.kind = HG_OK;
+                r.reserved = 0;
+                r.err_offset = 0;
+                *a.result = r;
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = 0; i < enp; ++i) {
+            const uint64_t g = uni(pbase[i]);
+            const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
+            const uint32_t kl = uni(pc[i].kl), vl = uni(pc[i].vl), cnt = uni(pc[i].count);
+            for (uint32_t t = tid; t < cnt; t += THREADS)
+                if (g + t < a.cap) write_span(a.spans, g + t, x + t * R, kl, vl);
+        }
+        __syncthreads();
+    }
+    if (fb >= a.nspec || blockIdx.x >= a.nbatches) return;  // nothing left for the general engine
     if (tid == 0) s.batch = atomicAdd(a.ticket, 1u);
     __syncthreads();
     if (min((s.batch + 1) * a.q, a.nspec) <= fb) {
-        // Resolved and emitted by the pre-pass: publish its INCL and stop.
-        if (tid == 0) {
-            const SpecBatch& sb = a.sbatch[min((s.batch + 1) * a.q, a.nspec) - 1];
+        // Resolved by the pre-pass (spans written above): publish its INCL.
+        if (tid < 64) {
             const uint32_t b0 = s.batch;
-            const uint64_t gend = sb.gbase + sb.count;
-            const uint64_t g0 = a.sbatch[b0 * a.q].gbase;
-            st_agent(&a.status[2 * b0 + 1], pack_status(ST_INCL, 0, gend));
-            st_agent(&a.status[2 * b0], pack_status(ST_INCL, (uint32_t)(gend - g0), sb.exit));
+            const uint32_t e1 = min((b0 + 1) * a.q, a.nspec);  // first batch after it
+            const uint64_t gend = spec_base(a, e1);
+            const uint64_t g0 = spec_base(a, b0 * a.q);
+            if (tid == 0) {
+                const uint64_t ex = a.sbatch[e1 - 1].exit;
+                st_agent(&a.status[2 * b0 + 1], pack_status(ST_INCL, 0, gend));
+                st_agent(&a.status[2 * b0], pack_status(ST_INCL, (uint32_t)(gend - g0), ex));
+            }
         }
         return;
     }
@@ -1189,130 +1267,19 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
         X = ps.kind == PK_EMPTY ? X : X + (uint64_t)ps.count * ps.R;
     }
     if (tid == 0) {
+        // publish (read by decode_kernel after the kernel boundary), count the
+        // records per group, then settle the two links this batch is part of
         SpecBatch o;
         o.x0 = X0;
         o.exit = X;
         o.count = (uint32_t)total;
         o.ok = ok ? 1u : 0u;
-        o.gbase = 0;
+        o.pad = 0;
         sb[b] = o;
-    }
-}
-
-// decode_scan_kernel (one workgroup of SCAN_THREADS): the longest prefix
-// of pre-pass batches that chains exactly (batch 0 enters at 0, every later
-// batch's guessed entry is its predecessor's exit, all verified) and the
-// record base of each.  Writes ctl->first_bad; when the prefix is the whole
-// file it also writes the decode result.  Chunks of SCAN_THREADS x SCAN_PER batches,
-// each thread's SCAN_PER loads issued together.
-constexpr uint32_t SCAN_THREADS = 1024, SCAN_PER = 4, SNW = SCAN_THREADS / 64;
-__global__ __launch_bounds__(SCAN_THREADS) void decode_scan_kernel(SpecBatch* sb, uint32_t n,
-                                                                    DecodeCtl* ctl,
-                                                                    hg_decode_result* result) {
-    __shared__ uint64_t wtot[SNW];
-    __shared__ uint32_t wbad[SNW];
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    uint64_t carry = 0;  // records before this chunk
-    uint32_t m = n;      // first bad batch
-    for (uint32_t c0 = 0; c0 < n; c0 += SCAN_THREADS * SCAN_PER) {
-        const uint32_t j0 = c0 + tid * SCAN_PER;
-        uint64_t x0[SCAN_PER], ex[SCAN_PER];
-        uint32_t cnt[SCAN_PER], ok[SCAN_PER];
-#pragma unroll
-        for (uint32_t k = 0; k < SCAN_PER; ++k) {
-            const uint32_t j = min(j0 + k, n - 1);
-            x0[k] = sb[j].x0;
-            ex[k] = sb[j].exit;
-            cnt[k] = sb[j].count;
-            ok[k] = sb[j].ok;
-        }
-        const uint64_t prev_exit = (j0 == 0 || j0 > n) ? 0 : sb[min(j0, n) - 1].exit;
-        uint32_t mybad = n;
-        uint64_t sum = 0;
-#pragma unroll
-        for (uint32_t k = 0; k < SCAN_PER; ++k) {
-            const uint32_t j = j0 + k;
-            const uint64_t want = k == 0 ? prev_exit : ex[k - 1];
-            if (j < n && mybad == n) {
-                if (!ok[k] || x0[k] != want) mybad = j;
-                else sum += cnt[k];
-            }
-        }
-        uint32_t bm = mybad;
-        for (int d = 32; d >= 1; d >>= 1) bm = min(bm, (uint32_t)__shfl_xor((int)bm, d, 64));
-        if (lane == 0) wbad[wid] = bm;
-        __syncthreads();
-        bm = m;
-        for (uint32_t w = 0; w < SNW; ++w) bm = min(bm, wbad[w]);
-        if (j0 >= bm) sum = 0;  // only batches below the first bad one count
-        uint64_t incl = sum;
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint64_t o = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += o;
-        }
-        if (lane == 63) wtot[wid] = incl;
-        __syncthreads();
-        uint64_t base = carry + incl - sum, chunk = 0;
-        for (uint32_t w = 0; w < SNW; ++w) {
-            if (w < wid) base += wtot[w];
-            chunk += wtot[w];
-        }
-#pragma unroll
-        for (uint32_t k = 0; k < SCAN_PER; ++k) {
-            const uint32_t j = j0 + k;
-            if (j < min(n, bm)) {
-                sb[j].gbase = base;
-                base += cnt[k];
-            }
-        }
-        carry += chunk;
-        m = bm;
-        __syncthreads();
-        if (m < n) break;
-    }
-    if (tid == 0) {
-        ctl->first_bad = m;
-        if (m == n) {
-            hg_decode_result r;
-            r.n_records = carry;
-            r.kind = HG_OK;
-            r.reserved = 0;
-            r.err_offset = 0;
-            *result = r;
-        }
-    }
-}
-
-// decode_emit_kernel: spans of the resolved pre-pass batches (pure writes;
-// the batch's piece records are staged in LDS first, one load per thread).
-// A separate pass: writing the spans from inside the pre-pass, interleaved
-// with its read stream, measured 262 us against 205 + 25 us.
-__global__ __launch_bounds__(THREADS) void decode_emit_kernel(DecodeArgs a, const SpecBatch* sb,
-                                                              const SpecPiece* sp,
-                                                              const DecodeCtl* ctl) {
-    __shared__ SpecPiece pc[SPEC_BP];
-    __shared__ uint64_t pbase[SPEC_BP];
-    const uint32_t b = blockIdx.x;
-    if (b >= ctl->first_bad) return;
-    const uint32_t p0 = b * a.sbp;
-    const uint32_t np = min(a.sbp, a.npieces - p0);
-    const uint32_t tid = threadIdx.x;
-    if (tid < np) pc[tid] = sp[p0 + tid];
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t g = sb[b].gbase;
-        for (uint32_t i = 0; i < np; ++i) {
-            pbase[i] = g;
-            g += pc[i].count;
-        }
-    }
-    __syncthreads();
-    for (uint32_t i = 0; i < np; ++i) {
-        const uint64_t g = uni(pbase[i]);
-        const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
-        const uint32_t kl = uni(pc[i].kl), vl = uni(pc[i].vl), cnt = uni(pc[i].count);
-        for (uint32_t t = tid; t < cnt; t += THREADS)
-            if (g + t < a.cap) write_span(a.spans, g + t, x + t * R, kl, vl);
+        atomicAdd(&a.gsum[b / SPEC_GROUP], (unsigned long long)total);
+        if (!ok || (b == 0 && X0 != 0)) mark_bad(a.ctl, a.nspec, b);
+        if (b > 0) link_arrive(a, b, 0 - X0);
+        if (b + 1 < a.nspec) link_arrive(a, b + 1, X);
     }
 }
 
@@ -1321,15 +1288,21 @@ __global__ __launch_bounds__(THREADS) void decode_emit_kernel(DecodeArgs a, cons
 namespace {
 struct DecodeLayout {
     uint64_t npieces, nbatches, status_words, scratch_off, nspec, sbatch_off, spiece_off, bytes;
+    uint64_t gsum_off, link_off, status_off;
 };
 DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
     DecodeLayout l;
     l.npieces = (len + PIECE - 1) / PIECE;
     l.nbatches = (l.npieces + BATCH_MIN - 1) / BATCH_MIN;  // most batches any launch uses
-    l.status_words = 2 * l.nbatches + 2;                    // + DecodeCtl
-    l.scratch_off = (l.status_words * 8 + 255) & ~255ull;
+    // [DecodeCtl | group sums | pair links | statuses] are zeroed per call
+    // (up to the statuses in use), then the scratch and pre-pass records.
     l.nspec = (l.npieces + SPEC_BP_MIN - 1) / SPEC_BP_MIN;  // most pre-pass batches
+    l.gsum_off = sizeof(DecodeCtl);
+    l.link_off = l.gsum_off + ((l.nspec + SPEC_GROUP - 1) / SPEC_GROUP) * 8;
+    l.status_off = (l.link_off + l.nspec * 8 + 255) & ~255ull;
+    l.status_words = 2 * l.nbatches;
+    l.scratch_off = (l.status_off + l.status_words * 8 + 255) & ~255ull;
     l.sbatch_off = l.scratch_off + l.npieces * MAX_REC_PIECE * sizeof(hg_span);
     l.spiece_off = l.sbatch_off + ((l.nspec * sizeof(SpecBatch) + 255) & ~255ull);
     l.bytes = l.spiece_off + ((l.npieces * sizeof(SpecPiece) + 255) & ~255ull);
@@ -1409,9 +1382,12 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
     a.spans = d_spans;
     a.cap = cap;
     a.result = d_result;
-    // [DecodeCtl (2 words) | 2 status words per general batch] -- one memset
+    char* ws = static_cast<char*>(d_ws);
     DecodeCtl* ctl = static_cast<DecodeCtl*>(d_ws);
-    a.status = static_cast<unsigned long long*>(d_ws) + 2;
+    a.ctl = ctl;
+    a.gsum = reinterpret_cast<unsigned long long*>(ws + l.gsum_off);
+    a.link = reinterpret_cast<unsigned long long*>(ws + l.link_off);
+    a.status = reinterpret_cast<unsigned long long*>(ws + l.status_off);
     a.ticket = &ctl->ticket;
     a.scratch = reinterpret_cast<hg_span*>(static_cast<char*>(d_ws) + l.scratch_off);
     const uint32_t res_spec = resident_workgroups(decode_spec_kernel, 0);
@@ -1424,32 +1400,28 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
     a.npieces = (uint32_t)l.npieces;
     a.hz = 8 - nb;
     a.diag = d_diag;
-    char* ws = static_cast<char*>(d_ws);
     SpecBatch* sb = reinterpret_cast<SpecBatch*>(ws + l.sbatch_off);
     SpecPiece* sp = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
-    uint32_t* fb = &ctl->first_bad;
     a.sbatch = sb;
-    a.first_bad = fb;
+    a.spiece = sp;
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
     a.q = a.bp / a.sbp;
-    if (hipMemsetAsync(d_ws, 0, (2 + 2 * (size_t)a.nbatches) * 8, stream) != hipSuccess)
+    if (hipMemsetAsync(d_ws, 0, l.status_off + 2 * (size_t)a.nbatches * 8, stream) != hipSuccess)
         return HG_ERR_HIP;
-    // 1. stride pre-pass  2. chain check + record bases  3. spans of the resolved prefix
+    // 1. stride pre-pass: verifies, links neighbours, sums records per group
+    // 2. decode_kernel: spans of the resolved prefix, then the general engine
+    //    from the first unresolved batch on (exits at once if there is none)
     // HG_DECODE_SPEC_PAD: extra dynamic LDS per pre-pass workgroup (bytes) to cap
     // its occupancy (experiments).
     const size_t spec_pad = (size_t)env_or("HG_DECODE_SPEC_PAD", 0) > 65536 ? 0
                           : (size_t)env_or("HG_DECODE_SPEC_PAD", 0);
     hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), spec_pad, stream, a, sb,
                        sp);
-    hipLaunchKernelGGL(decode_scan_kernel, dim3(1), dim3(SCAN_THREADS), 0, stream, sb, a.nspec, ctl,
-                       d_result);
-    hipLaunchKernelGGL(decode_emit_kernel, dim3(a.nspec), dim3(THREADS), 0, stream, a,
-                       (const SpecBatch*)sb, (const SpecPiece*)sp, (const DecodeCtl*)ctl);
-    // 4. the general engine from the first unresolved batch on (exits at once if none)
+    const uint32_t grid = a.nbatches > a.nspec ? a.nbatches : a.nspec;
     if (d_diag)
-        hipLaunchKernelGGL(decode_kernel<true>, dim3(a.nbatches), dim3(THREADS), 0, stream, a);
+        hipLaunchKernelGGL(decode_kernel<true>, dim3(grid), dim3(THREADS), 0, stream, a);
     else
-        hipLaunchKernelGGL(decode_kernel<false>, dim3(a.nbatches), dim3(THREADS), 0, stream, a);
+        hipLaunchKernelGGL(decode_kernel<false>, dim3(grid), dim3(THREADS), 0, stream, a);
     return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 

@@ -8,6 +8,6 @@ out=$root/build_exp/$name
 mkdir -p "$out"
 cd "$root/horreum_amd/csrc"
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-value -Wno-unused-result $defs"
-for f in hg_decode hg_encode hg_runtime; do /opt/rocm/bin/hipcc $F -c $f.hip -o "$out/$f.o" & done; wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/libhorreum_gpu.so" "$out"/hg_decode.o "$out"/hg_encode.o "$out"/hg_runtime.o
+for f in hg_decode hg_encode hg_merge hg_lookup hg_runtime; do /opt/rocm/bin/hipcc $F -c $f.hip -o "$out/$f.o" & done; wait
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/libhorreum_gpu.so" "$out"/*.o
 echo "$out/libhorreum_gpu.so"

@@ -1,0 +1,129 @@
+// HBM read-order probe (not part of the product): does the ORDER in which
+// workgroups sweep a 1 GiB buffer set the streaming ceiling?  Each workgroup
+// (256 threads) stages 16 KiB pieces through LDS with the next piece in flight
+// in registers, exactly like decode_spec_kernel, and reads pieces in one of
+// two orders:
+//   contiguous: ticket b reads pieces [b*ppb, (b+1)*ppb) (the decode today);
+//   interleave: ticket b reads pieces b, b+G, b+2G, ... (G = grid): at any
+//               moment the chip reads one contiguous window of the buffer.
+// A register-only grid-stride sweep gives the plain read ceiling.
+// Prints GB/s per configuration.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define CHECK(x)                                                                          \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__);              \
+            exit(1);                                                                      \
+        }                                                                                 \
+    } while (0)
+
+constexpr uint32_t GPT = 4, PIECE = GPT * 256 * 16;
+
+template <int MODE, int PAD_KB>
+__global__ __launch_bounds__(256) void sweep_kernel(const uint8_t* src, uint32_t ppb, uint32_t grid,
+                                                    uint32_t* ticket, unsigned long long* out) {
+    __shared__ u32x4 lds[PIECE / 16 + PAD_KB * 64];
+    __shared__ uint32_t sb;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0) sb = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t b = sb;
+    auto piece_addr = [&](uint32_t k) -> uint64_t {
+        const uint64_t p = MODE == 1 ? (uint64_t)k * grid + b : (uint64_t)b * ppb + k;
+        return p * PIECE;
+    };
+    u32x4 v[GPT];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < (int)GPT; ++i)
+        v[i] = *reinterpret_cast<const u32x4*>(src + piece_addr(0) + (i * 256 + tid) * 16);
+    for (uint32_t k = 0; k < ppb; ++k) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < (int)GPT; ++i) lds[i * 256 + tid] = v[i];
+        __syncthreads();
+        const uint64_t nb = piece_addr(min(k + 1, ppb - 1));
+#pragma unroll
+        for (int i = 0; i < (int)GPT; ++i)
+            v[i] = *reinterpret_cast<const u32x4*>(src + nb + (i * 256 + tid) * 16);
+        const u32x4 a = lds[(tid * 7 + k) % (PIECE / 16)];
+        acc ^= a.x ^ a.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// Register-only grid-stride sweep (the 'float4 copy' shape without the write).
+__global__ __launch_bounds__(256) void flat_kernel(const u32x4* src, uint64_t n, unsigned long long* out) {
+    uint32_t acc = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 * 4 + threadIdx.x; i < n; i += stride) {
+        u32x4 a = src[i], b2 = src[i + 256], c = src[i + 512], d = src[i + 768];
+        acc ^= a.x ^ b2.y ^ c.z ^ d.w;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int MODE, int PAD_KB>
+void run(const uint8_t* d, uint64_t len, uint32_t ppb, uint32_t* ticket, unsigned long long* out,
+         const char* name) {
+    const uint32_t npieces = (uint32_t)(len / PIECE);
+    const uint32_t grid = npieces / ppb;
+    int occ = 0;
+    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, sweep_kernel<MODE, PAD_KB>, 256, 0));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    float best = 1e9f;
+    for (int r = 0; r < 8; ++r) {
+        CHECK(hipMemset(ticket, 0, 4));
+        CHECK(hipEventRecord(e0));
+        sweep_kernel<MODE, PAD_KB><<<grid, 256>>>(d, ppb, grid, ticket, out);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0 && ms < best) best = ms;
+    }
+    printf("%-26s ppb=%3u grid=%6u occ/CU=%2d  %.4f ms  %.0f GB/s\n", name, ppb, grid, occ, best,
+           (double)grid * ppb * PIECE / best / 1e6);
+}
+
+int main() {
+    const uint64_t len = 1ull << 30;
+    uint8_t* d;
+    uint32_t* ticket;
+    unsigned long long* out;
+    CHECK(hipMalloc(&d, len + PIECE));
+    CHECK(hipMalloc(&ticket, 4));
+    CHECK(hipMalloc(&out, 8));
+    CHECK(hipMemset(d, 1, len + PIECE));
+    for (int g : {1024, 2048, 4096, 8192}) {
+        hipEvent_t e0, e1;
+        CHECK(hipEventCreate(&e0));
+        CHECK(hipEventCreate(&e1));
+        float best = 1e9f;
+        for (int r = 0; r < 8; ++r) {
+            CHECK(hipEventRecord(e0));
+            flat_kernel<<<g, 256>>>(reinterpret_cast<const u32x4*>(d), len / 16, out);
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            if (r > 0 && ms < best) best = ms;
+        }
+        printf("flat grid-stride           grid=%6d  %.4f ms  %.0f GB/s\n", g, best, len / best / 1e6);
+    }
+    for (uint32_t ppb : {4u, 16u, 64u}) {
+        run<0, 0>(d, len, ppb, ticket, out, "contiguous pad0");
+        run<1, 0>(d, len, ppb, ticket, out, "interleave pad0");
+        run<0, 24>(d, len, ppb, ticket, out, "contiguous pad24");
+        run<1, 24>(d, len, ppb, ticket, out, "interleave pad24");
+    }
+    return 0;
+}

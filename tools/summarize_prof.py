@@ -61,6 +61,13 @@ def main():
                 "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
                 "min_ns": float(r["MinNs"]), "max_ns": float(r["MaxNs"]),
                 "pct": float(r["Percentage"])}
+    legs = find(os.path.join(out_dir, "prof_legs"), "*kernel_stats.csv")
+    if legs:  # every bench leg (encode, cfg4 batched decode, compaction)
+        rows = list(csv.DictReader(open(legs[0])))
+        with open(os.path.join(prof, f"{tag}_legs_kernel_stats.csv"), "w") as f:
+            w = csv.DictWriter(f, fieldnames=rows[0].keys())
+            w.writeheader()
+            w.writerows(rows)
     fetch = counters(os.path.join(out_dir, "prof_fetch"))
     write = counters(os.path.join(out_dir, "prof_write"))
     pmc = {}
