@@ -46,6 +46,8 @@ def parse(argv=None):
     p.add_argument("--no-encode", action="store_true", help="skip the config-3 encode leg")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the config-4 / config-5 (scaled) legs")
+    p.add_argument("--no-host", action="store_true",
+                   help="skip the host-inclusive (H2D + kernel + D2H) legs")
     return p.parse_args(argv)
 
 
@@ -200,6 +202,9 @@ def main(argv=None):
         extra["multi_table_decode_cfg4"] = multi_table_leg(torch, eng, device, args, world, rank)
         extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank)
 
+    if not args.no_host and world == 1:
+        extra["host_inclusive"] = host_leg(torch, eng, sst, n, world)
+
     cpu = (cpu_baseline(sst, n, args.cpu_sample_mb, args.cpu_seconds)
            if (rank == 0 and world == 1) else None)
     if rank == 0:
@@ -266,6 +271,100 @@ def encode_leg(torch, eng, device, args, world, rank):
             "ms_per_step": round(wall / steps * 1e3, 4), "records": n, "out_bytes": total,
             "roofline_frac": round(alg / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "achieved_GBs": round(alg / (mean_ms * 1e-3) / 1e9, 2), "parity_ok": bool(ok)}
+
+
+def host_leg(torch, eng, sst, n, world, reps=3):
+    """Host-inclusive rates (north_star: the path starts and ends in host
+    memory): hg_decode_host of the cfg2 table (1 GiB in, 130 MB of spans
+    out) and hg_encode_host of the cfg3 arena (2.88 GB + 240 MB of pairs
+    in, 3.04 GB out), each from pageable buffers (threaded copies through
+    pinned staging) and from page-locked ones (direct DMA).  Median of
+    `reps` calls, wall clock around the synchronous ABI call."""
+    import ctypes
+    from horreum_amd import synth
+    from horreum_amd.abi import HgErr
+    lib, ctx = eng.lib, eng.ctx
+
+    def vp(a):
+        return ctypes.c_void_p(a.ctypes.data)
+
+    def med(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]
+
+    out = {"threads": int(os.environ.get("HG_HOST_COPY_THREADS", "8")), "reps": reps}
+    L = sst.numel()
+    for mode in ("pageable", "pinned"):
+        if mode == "pinned":
+            h_t = torch.empty(L, dtype=torch.uint8).pin_memory()
+            h_t.copy_(sst)
+            sp_t = torch.empty(n * 16, dtype=torch.uint8).pin_memory()
+            h, sp = h_t.numpy(), sp_t.numpy()
+        else:
+            h = sst.cpu().numpy().copy()
+            sp = np.empty(n * 16, dtype=np.uint8)
+        nn, err = ctypes.c_uint64(), HgErr()
+
+        def dec():
+            rc = lib.hg_decode_host(ctx, vp(h), L, vp(sp), n, ctypes.byref(nn), ctypes.byref(err))
+            assert rc == 0 and nn.value == n, (rc, nn.value)
+
+        t = med(dec)
+        ok = bool(np.array_equal(sp.view("<u8")[0:2 * n:2][:1000],
+                                 np.arange(1000, dtype=np.uint64) * 132))
+        out[f"decode_cfg2_{mode}"] = {"GiB_s": round(L / t / GIB, 3), "ms": round(t * 1e3, 2),
+                                      "parity_spot": ok}
+        del h, sp
+        if mode == "pinned":
+            del h_t, sp_t
+    torch.cuda.empty_cache()
+    # encode: cfg3 arena -> SSTable bytes
+    nE, k, v = 10_000_000, 32, 256
+    arena_d, pairs_d = synth.fixed_arena(nE, k, v, seed=3, device=sst.device)
+    total = nE * (16 + k + v)
+    for mode in ("pageable", "pinned"):
+        if mode == "pinned":
+            a_t = torch.empty(arena_d.numel(), dtype=torch.uint8).pin_memory()
+            a_t.copy_(arena_d)
+            p_t = torch.empty(pairs_d.numel(), dtype=torch.uint8).pin_memory()
+            p_t.copy_(pairs_d)
+            o_t = torch.empty(total, dtype=torch.uint8).pin_memory()
+            ha, hp, ho = a_t.numpy(), p_t.numpy(), o_t.numpy()
+        else:
+            ha, hp = arena_d.cpu().numpy().copy(), pairs_d.cpu().numpy().copy()
+            ho = np.empty(total, dtype=np.uint8)
+        ol = ctypes.c_uint64()
+
+        def enc():
+            rc = lib.hg_encode_host(ctx, vp(ha), ha.size, vp(hp), nE, vp(ho), total,
+                                    ctypes.c_void_p(0), 0, ctypes.c_void_p(0), ctypes.byref(ol))
+            assert rc == 0 and ol.value == total, (rc, ol.value)
+
+        t = med(enc)
+        ok = bool(np.array_equal(ho[16:16 + k + v], ha[:k + v]))
+        out[f"encode_cfg3_{mode}"] = {"GiB_s": round(total / t / GIB, 3), "ms": round(t * 1e3, 2),
+                                      "parity_spot": ok}
+        del ha, hp, ho
+        if mode == "pinned":
+            del a_t, p_t, o_t
+    del arena_d, pairs_d
+    torch.cuda.empty_cache()
+    # raw pinned DMA rates for reference
+    hb = torch.empty(1 << 30, dtype=torch.uint8).pin_memory()
+    db = torch.empty(1 << 30, dtype=torch.uint8, device=sst.device)
+    torch.cuda.synchronize()
+    t = med(lambda: (db.copy_(hb, non_blocking=True), torch.cuda.synchronize()))
+    out["h2d_pinned_GiB_s"] = round(1 / t, 2)
+    t = med(lambda: (hb.copy_(db, non_blocking=True), torch.cuda.synchronize()))
+    out["d2h_pinned_GiB_s"] = round(1 / t, 2)
+    del hb, db
+    torch.cuda.empty_cache()
+    return out
 
 
 def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32):

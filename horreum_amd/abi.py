@@ -107,6 +107,9 @@ _PROTOS = {
                                     ctypes.POINTER(HgMergeResult)]),
     "hg_merge_dev_async": (ctypes.c_int, [_vp, _u32, _u8p, _u64, _vp, _vp, _vp, _vp, _u64, _vp]),
     # compact(ctx, ntables, tables**, lens*, out, cap, out_len*, stride, blocks, result*)
+    "hg_host_register": (ctypes.c_int, [_vp, _u64]),
+    "hg_host_unregister": (ctypes.c_int, [_vp]),
+    "hg_host_is_pinned": (ctypes.c_int, [_vp]),
     "hg_compact_host": (ctypes.c_int, [_vp, _u32, _vp, _vp, _u8p, _u64, ctypes.POINTER(_u64),
                                        _u32, _vp, ctypes.POINTER(HgMergeResult)]),
 }

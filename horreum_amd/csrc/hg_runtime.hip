@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <new>
+#include <thread>
 
 #include "../../include/horreum_gpu.h"
 
@@ -312,12 +313,70 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
     return HG_OK;
 }
 
-// Host bytes in, host spans out.  The file is pushed through two pinned
-// staging buffers (CPU memcpy of piece i+1 overlaps the DMA of piece i), the
-// decode runs on the device copy, and the spans come back the same way.
+// Host bytes in, host spans out.  Host buffers move in 64 MiB pieces:
+//  - pinned (hipHostMalloc'd, or registered with hg_host_register, e.g. an
+//    mmap'd SSTable file kept registered by the caller): DMA straight from /
+//    to the caller's pages, no CPU copy;
+//  - pageable: two pinned staging buffers; the CPU copy of piece i+1 (split
+//    over up to kCopyThreads host threads) overlaps the DMA of piece i.
+// The decode runs on the device copy; the spans come back the same way.
 static constexpr size_t kStage = 64ull << 20;
+static constexpr unsigned kCopyThreads = 8;     // default (HG_HOST_COPY_THREADS overrides)
+static constexpr unsigned kMaxCopyThreads = 32;
+
+// True if `p` lies in page-locked host memory the DMA engines can address.
+static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    const hipError_t e = hipPointerGetAttributes(&a, p);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory reports an error: not sticky for us
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+static unsigned copy_threads() {
+    unsigned t = kCopyThreads;
+    if (const char* e = getenv("HG_HOST_COPY_THREADS")) t = (unsigned)std::max(1, atoi(e));
+    const unsigned hw = std::thread::hardware_concurrency();
+    return std::max(1u, std::min({t, hw ? hw : 1u, kMaxCopyThreads}));
+}
+
+// memcpy split over host threads in 2 MiB-aligned slices (pageable <-> pinned).
+static void par_memcpy(void* dst, const void* src, size_t n) {
+    const unsigned nt = copy_threads();
+    const size_t grain = 2ull << 20;
+    if (nt <= 1 || n < 2 * grain) {
+        memcpy(dst, src, n);
+        return;
+    }
+    const size_t slices = (n + grain - 1) / grain;
+    const unsigned use = (unsigned)std::min<size_t>(nt, slices);
+    const size_t per = (slices + use - 1) / use * grain;
+    std::thread th[kMaxCopyThreads];
+    unsigned started = 0;
+    for (unsigned t = 1; t < use; ++t) {
+        const size_t o = t * per;
+        if (o >= n) break;
+        const size_t m = std::min(per, n - o);
+        th[started++] = std::thread([=] {
+            memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, m);
+        });
+    }
+    memcpy(dst, src, std::min(per, n));
+    for (unsigned t = 0; t < started; ++t) th[t].join();
+}
+
+static int copy_direct(hg_ctx* c, void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    for (size_t off = 0; off < bytes; off += kStage)
+        if (hipMemcpyAsync(static_cast<char*>(dst) + off, static_cast<const char*>(src) + off,
+                           std::min(kStage, bytes - off), kind, c->stream) != hipSuccess)
+            return HG_ERR_HIP;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
 
 static int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (host_pinned(src)) return copy_direct(c, dst, src, bytes, hipMemcpyHostToDevice);
     if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
         return HG_ERR_HIP;
     hipEvent_t ev[2];
@@ -329,7 +388,7 @@ static int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
         const size_t n = std::min(kStage, bytes - off);
         const int b = (int)(i & 1);
         if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
-        memcpy(c->h_stage[b].p, static_cast<const char*>(src) + off, n);
+        par_memcpy(c->h_stage[b].p, static_cast<const char*>(src) + off, n);
         if (hipMemcpyAsync(static_cast<char*>(dst) + off, c->h_stage[b].p, n,
                            hipMemcpyHostToDevice, c->stream) != hipSuccess ||
             hipEventRecord(ev[b], c->stream) != hipSuccess) {
@@ -345,6 +404,7 @@ static int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
 }
 
 static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (host_pinned(dst)) return copy_direct(c, dst, src, bytes, hipMemcpyDeviceToHost);
     if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
         return HG_ERR_HIP;
     hipEvent_t ev[2];
@@ -359,7 +419,7 @@ static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
         const int b = (int)(i & 1);
         if (used[b]) {  // drain the previous use of this buffer
             if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
-            memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
+            par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
         }
         if (hipMemcpyAsync(c->h_stage[b].p, static_cast<const char*>(src) + off, n,
                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -375,7 +435,7 @@ static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
         const int b = (int)((i + k) & 1);
         if (!used[b]) continue;
         if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
-        memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
+        par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
         used[b] = false;
     }
     hipStreamSynchronize(c->stream);
@@ -383,6 +443,28 @@ static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
     hipEventDestroy(ev[1]);
     return rc;
 }
+
+int hg_host_register(const void* h_ptr, uint64_t len) {
+    if (!h_ptr || !len) return HG_ERR_INVALID_ARG;
+    const hipError_t e = hipHostRegister(const_cast<void*>(h_ptr), len, hipHostRegisterDefault);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return HG_ERR_HIP;
+    }
+    return HG_OK;
+}
+
+int hg_host_unregister(const void* h_ptr) {
+    if (!h_ptr) return HG_ERR_INVALID_ARG;
+    const hipError_t e = hipHostUnregister(const_cast<void*>(h_ptr));
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        return HG_ERR_HIP;
+    }
+    return HG_OK;
+}
+
+int hg_host_is_pinned(const void* h_ptr) { return h_ptr && host_pinned(h_ptr) ? 1 : 0; }
 
 int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spans, uint64_t cap,
                    uint64_t* n_out, hg_err* err) {

@@ -119,11 +119,18 @@ class Engine:
                                                  ctypes.cast(cp, ctypes.c_void_p), _ptr(results)),
               "hg_decode_batch_dev_async")
 
-    def decode_host(self, data, cap=None):
-        """Host bytes in, numpy SPAN_DTYPE array out (through pinned staging)."""
+    def decode_host(self, data, cap=None, out=None):
+        """Host bytes in, numpy SPAN_DTYPE array out.  Page-locked buffers
+        (pinned, or registered with host_register) are DMA'd directly;
+        pageable ones go through the pinned staging pipeline.  `out`: an
+        optional preallocated SPAN_DTYPE array (e.g. a pinned one)."""
         buf = np.ascontiguousarray(np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8))
-        cap = buf.size // 16 if cap is None else int(cap)
-        spans = np.zeros(max(cap, 1), dtype=SPAN_DTYPE)
+        if out is not None:
+            spans = out
+            cap = spans.size if cap is None else min(int(cap), spans.size)
+        else:
+            cap = buf.size // 16 if cap is None else int(cap)
+            spans = np.zeros(max(cap, 1), dtype=SPAN_DTYPE)
         n = ctypes.c_uint64()
         err = HgErr()
         rc = self.lib.hg_decode_host(self.ctx, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
@@ -132,6 +139,19 @@ class Engine:
         if rc < 0:
             raise HorreumGpuError(rc, "hg_decode_host")
         return DecodeOut(spans[: min(n.value, cap)], n.value, err.kind, err.offset)
+
+    # ---- host memory ---------------------------------------------------------------
+    def host_register(self, array):
+        """Page-lock a host numpy buffer for direct DMA (hipHostRegister)."""
+        check(self.lib.hg_host_register(ctypes.c_void_p(array.ctypes.data), array.nbytes),
+              "hg_host_register")
+
+    def host_unregister(self, array):
+        check(self.lib.hg_host_unregister(ctypes.c_void_p(array.ctypes.data)),
+              "hg_host_unregister")
+
+    def host_is_pinned(self, array):
+        return bool(self.lib.hg_host_is_pinned(ctypes.c_void_p(array.ctypes.data)))
 
     @staticmethod
     def spans_to_numpy(spans, n):

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 2
+#define HG_ABI_VERSION 3
 
 /* Status codes: return values, and the `kind` field of hg_err / results. */
 enum hg_status {
@@ -273,6 +273,19 @@ int hg_lookup_dev_async(hg_ctx* ctx, const uint8_t* d_table, const hg_span* d_sp
 int hg_lookup_host(hg_ctx* ctx, const uint8_t* h_table, uint64_t len,
                    const uint8_t* h_keys, uint64_t keys_len, const hg_key* h_queries,
                    uint64_t nq, hg_lookup_result* h_results);
+
+/* ---- host memory ------------------------------------------------------
+ * The `_host` entry points DMA straight from / to page-locked host memory
+ * and stage pageable memory through two pinned 64 MiB buffers (CPU copies
+ * split over host threads, overlapped with the DMA).  A caller that keeps an
+ * SSTable file mmap'd (PersistedFile, src/sstable/storage.rs:21-67) or a
+ * memtable arena alive registers it once so every later call skips the CPU
+ * copy.  hg_host_register pins [h_ptr, h_ptr+len) (hipHostRegister);
+ * hg_host_unregister takes the base pointer passed to register;
+ * hg_host_is_pinned returns 1 for page-locked host memory, else 0. */
+int hg_host_register(const void* h_ptr, uint64_t len);
+int hg_host_unregister(const void* h_ptr);
+int hg_host_is_pinned(const void* h_ptr);
 
 /* Number of blocks Index::new produces for n pairs: ceil(n / stride). */
 uint64_t hg_block_count(uint64_t n, uint32_t block_stride);

@@ -69,6 +69,36 @@ def test_host_path_parity(engine, name):
     assert np.array_equal(out.spans, ws)
 
 
+def test_host_path_pinned_registered_pageable(engine):
+    """The three host-memory routes of hg_decode_host agree bit-exactly:
+    pageable (threaded staging copies), registered (hipHostRegister) and
+    pinned (torch pin_memory) -- on an ~80 MB table (two 64 MiB staging
+    pieces, each copied by several host threads)."""
+    import torch
+    from horreum_amd.abi import SPAN_DTYPE
+    data = corpus.make("mixed_4k")[2]
+    data = np.tile(data, (80 << 20) // data.size + 1)
+    ws, wn, wk, _, _ = oracle.decode(data)
+    assert wk == 0
+    out = engine.decode_host(data)
+    assert (out.n, out.kind) == (wn, 0) and np.array_equal(out.spans, ws)
+    assert not engine.host_is_pinned(data)
+    reg = data.copy()
+    engine.host_register(reg)
+    try:
+        assert engine.host_is_pinned(reg)
+        out = engine.decode_host(reg)
+        assert (out.n, out.kind) == (wn, 0) and np.array_equal(out.spans, ws)
+    finally:
+        engine.host_unregister(reg)
+    pin = torch.from_numpy(data).pin_memory()
+    spans_pin = torch.zeros(wn * 16, dtype=torch.uint8).pin_memory()
+    sp = spans_pin.numpy().view(SPAN_DTYPE)
+    out = engine.decode_host(pin.numpy(), out=sp)
+    assert engine.host_is_pinned(pin.numpy()) and engine.host_is_pinned(sp)
+    assert (out.n, out.kind) == (wn, 0) and np.array_equal(sp, ws)
+
+
 def test_empty_and_tiny_inputs(engine):
     for data in [b"", b"\x00", bytes(15), bytes(16), bytes(17), bytes(32), bytes(33),
                  bytes([3] + [0] * 15)]:
