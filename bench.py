@@ -224,7 +224,7 @@ def main(argv=None):
             "config": {"workload": "cfg2 single-SSTable decode (BASELINE configs[1])",
                        "records_per_gpu": n, "sst_bytes_per_gpu": L, "key_bytes": k,
                        "value_bytes": v, "decode_piece_bytes": 16384,
-                       "prepass_batch_pieces": 16,
+                       "prepass_batch_pieces": "adaptive: ~4 workgroups per CU, 64 at cfg2",
                        "parallelism": f"table-per-gpu x{world}, no collectives"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -738,12 +738,25 @@ __device__ __forceinline__ uint4 load16(const DecodeArgs& a, uint64_t off) {
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// Table bytes are read once per call: nontemporal loads (tools/probes/
+// read_probe.hip: a 1 GiB sweep reads at 7.0 TB/s nt vs 6.3 TB/s default).
+#ifndef HG_NT_LOADS
+#define HG_NT_LOADS 1
+#endif
 __device__ __forceinline__ void load_piece(const DecodeArgs& a, uint32_t p, uint4 (&v)[GPT]) {
     const uint64_t base = (uint64_t)p * PIECE;
     if (base + PIECE <= a.len) {  // uniform: plain 16-byte loads, no per-lane branch
         const uint4* src = reinterpret_cast<const uint4*>(a.sst + base) + threadIdx.x;
 #pragma unroll
-        for (uint32_t i = 0; i < GPT; ++i) v[i] = src[i * THREADS];
+        for (uint32_t i = 0; i < GPT; ++i) {
+            if (HG_NT_LOADS) {
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + i * THREADS));
+                v[i] = make_uint4(x.x, x.y, x.z, x.w);
+            } else {
+                v[i] = src[i * THREADS];
+            }
+        }
     } else {
 #pragma unroll
         for (uint32_t i = 0; i < GPT; ++i) v[i] = load16(a, base + (i * THREADS + threadIdx.x) * 16);
@@ -1204,6 +1217,42 @@ struct SpecSmem {
     uint32_t guess;
 };
 
+// Stride check of one staged piece without a barrier: the run's geometry
+// (entry, R, count) follows from the uniform header at X alone, so the exit
+// is known at once; the per-lane compares only decide whether the batch is
+// resolved and are OR-reduced by the caller (after piece 0, so a non-stride
+// table leaves after one piece, then once per batch).  Returns false when X
+// itself cannot start a run.
+__device__ __forceinline__ bool stride_geom(const uint8_t* data, uint64_t base, uint64_t len,
+                                           uint32_t clen, uint64_t X, PieceSum& ps, int& bad) {
+    ps.x = X;
+    if (X >= base + clen) {  // no record starts in this piece
+        ps.count = 0;
+        ps.R = 0;
+        ps.kl = ps.vl = 0;
+        ps.kind = PK_EMPTY;
+        return true;
+    }
+    const uint32_t xr = (uint32_t)(X - base);
+    if (X + 16 > len) return false;
+    uint64_t kl, vl;
+    lds_header(data, xr, kl, vl);
+    kl = uni(kl);
+    vl = uni(vl);
+    if (kl > ~0ull - vl || kl + vl > len - X - 16 || ((kl >> 32) | (vl >> 32))) return false;
+    const uint64_t R = 16 + kl + vl;
+    const uint32_t m = (uint32_t)((clen - xr + R - 1) / R);  // records starting in [xr, clen)
+    if (X + m * R > len) return false;                       // the last one would not fit
+    for (uint32_t t = 1 + threadIdx.x; t < m; t += THREADS)
+        bad |= !hdr_eq(data, xr + (uint32_t)(t * R), kl, vl);
+    ps.count = m;
+    ps.R = R;
+    ps.kl = (uint32_t)kl;
+    ps.vl = (uint32_t)vl;
+    ps.kind = PK_STRIDE;
+    return true;
+}
+
 __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
                                                               SpecPiece* sp) {
     __shared__ SpecSmem s;
@@ -1218,23 +1267,25 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
     if (tid < np) h = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
     uint64_t X = 0, X0 = 0, total = 0;
     bool ok = true;
+    int bad = 0;
+    // Two barriers per piece: (A) the previous piece is done with LDS; stage
+    // v and the halo and put the next piece's loads in flight before (B).
     for (uint32_t i = 0; i < np; ++i) {
         const uint32_t p = p0 + i;
         const uint64_t base = (uint64_t)p * PIECE;
         const uint64_t rem = a.len - base;
         const uint32_t clen = rem < PIECE ? (uint32_t)rem : PIECE;
-        __syncthreads();
+        __syncthreads();  // (A)
         if (i == 0 && tid < np) s.halo[tid] = h;
 #pragma unroll
         for (uint32_t q = 0; q < GPT; ++q)
             *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s.data64) +
                                       (q * THREADS + tid) * 16) = v[q];
-        __syncthreads();
-        if (tid < 4)
+        if (tid < 4)  // thread 0 reads back its own halo write when i == 0
             *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s.data64) + PIECE + tid * 16) =
                 tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
-        __syncthreads();
         if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
+        __syncthreads();  // (B)
         if (i == 0) {
             if (tid < 64) {
                 const uint32_t f = stride_guess(data, rem, clen, a.hz);
@@ -1249,7 +1300,11 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
             X = X0 = base + f;
         }
         PieceSum ps;
-        if (!stride_run(data, base, a.len, clen, X, ps)) {
+        if (!stride_geom(data, base, a.len, clen, X, ps, bad)) {
+            ok = false;
+            break;
+        }
+        if (i == 0 && __syncthreads_or(bad)) {  // not a stride table: leave after one piece
             ok = false;
             break;
         }
@@ -1266,6 +1321,7 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
         total += ps.count;
         X = ps.kind == PK_EMPTY ? X : X + (uint64_t)ps.count * ps.R;
     }
+    if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
     if (tid == 0) {
         // publish (read by decode_kernel after the kernel boundary), count the
         // records per group, then settle the two links this batch is part of
@@ -1343,11 +1399,12 @@ uint64_t env_or(const char* name, uint64_t dflt) {
 
 // Pieces per general batch: about one round of batches over decode_kernel's
 // resident grid (each batch pays one look-back + emission tail), a power of
-// two in [BATCH_MIN, BATCH] (HG_DECODE_BP overrides).  Pieces per pre-pass batch:
-// min(16, general), so a general batch is whole pre-pass batches.  16 was
-// measured on cfg2 (1 GiB, tools/sweep_spec.sh: 8..64 pieces at 4-8
-// workgroups per CU all land within 0.247-0.263 ms, 16 at the low end);
-// HG_DECODE_SBP overrides.
+// two in [BATCH_MIN, BATCH] (HG_DECODE_BP overrides).  Pieces per pre-pass
+// batch: long-lived streams win -- enough pieces that the pre-pass grid is
+// about 4 workgroups per CU, in [SPEC_BP_MIN, SPEC_BP] and at most the general
+// batch (a general batch is whole pre-pass batches).  Measured on cfg2 (1 GiB,
+// nontemporal loads, tools/sweep_spec.sh): 8 pieces 0.223 ms, 16: 0.218,
+// 32: 0.207, 64 (1024 workgroups): 0.197-0.200 ms.  HG_DECODE_SBP overrides.
 uint32_t pow2_in(uint64_t want, uint32_t lo, uint32_t hi) {
     uint32_t v = lo;
     while (v < hi && v < want) v <<= 1;
@@ -1357,10 +1414,24 @@ uint32_t general_pieces(uint64_t npieces, uint32_t resident) {
     using namespace hgk;
     return pow2_in(env_or("HG_DECODE_BP", (npieces + resident - 1) / resident), BATCH_MIN, BATCH);
 }
-uint32_t spec_pieces(uint32_t bp) {
+uint32_t spec_pieces(uint32_t bp, uint64_t npieces, uint32_t cus) {
     using namespace hgk;
-    const uint32_t s = pow2_in(env_or("HG_DECODE_SBP", 16), SPEC_BP_MIN, SPEC_BP);
+    const uint64_t want = (npieces + 4ull * cus - 1) / (4ull * cus);
+    const uint32_t s = pow2_in(env_or("HG_DECODE_SBP", want), SPEC_BP_MIN, SPEC_BP);
     return s < bp ? s : bp;
+}
+uint32_t device_cus() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
+    if (!cached[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 1;
+        cached[dev] = cus;
+    }
+    return (uint32_t)cached[dev];
 }
 }  // namespace
 
@@ -1395,7 +1466,7 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
                                     : resident_workgroups(decode_kernel<false>, 2);
     (void)res_spec;
     a.bp = general_pieces(l.npieces, res_gen);
-    a.sbp = spec_pieces(a.bp);
+    a.sbp = spec_pieces(a.bp, l.npieces, device_cus());
     a.nbatches = (uint32_t)((l.npieces + a.bp - 1) / a.bp);
     a.npieces = (uint32_t)l.npieces;
     a.hz = 8 - nb;

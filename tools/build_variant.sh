@@ -5,9 +5,13 @@ set -e
 name=$1; defs=$2
 root=$(cd "$(dirname "$0")/.." && pwd)
 out=$root/build_exp/$name
-mkdir -p "$out"
+rm -rf "$out"; mkdir -p "$out"
 cd "$root/horreum_amd/csrc"
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-value -Wno-unused-result $defs"
-for f in hg_decode hg_encode hg_merge hg_lookup hg_runtime; do /opt/rocm/bin/hipcc $F -c $f.hip -o "$out/$f.o" & done; wait
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$out/libhorreum_gpu.so" "$out"/*.o
+pids=()
+for f in hg_decode hg_encode hg_merge hg_lookup hg_runtime; do
+  /opt/rocm/bin/hipcc $F -c $f.hip -o "$out/$f.o" & pids+=($!)
+done
+for p in "${pids[@]}"; do wait $p || { echo "compile failed" >&2; exit 1; }; done
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -Wl,--no-undefined -o "$out/libhorreum_gpu.so" "$out"/*.o
 echo "$out/libhorreum_gpu.so"

@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(const uint8_t* src, uint32_t
     uint32_t acc = 0;
 #pragma unroll
     for (int i = 0; i < (int)GPT; ++i)
-        v[i] = *reinterpret_cast<const u32x4*>(src + piece_addr(0) + (i * 256 + tid) * 16);
+        v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + piece_addr(0) + (i * 256 + tid) * 16));
     for (uint32_t k = 0; k < ppb; ++k) {
         __syncthreads();
 #pragma unroll
@@ -51,7 +51,7 @@ __global__ __launch_bounds__(256) void sweep_kernel(const uint8_t* src, uint32_t
         const uint64_t nb = piece_addr(min(k + 1, ppb - 1));
 #pragma unroll
         for (int i = 0; i < (int)GPT; ++i)
-            v[i] = *reinterpret_cast<const u32x4*>(src + nb + (i * 256 + tid) * 16);
+            v[i] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + nb + (i * 256 + tid) * 16));
         const u32x4 a = lds[(tid * 7 + k) % (PIECE / 16)];
         acc ^= a.x ^ a.w;
     }
@@ -63,7 +63,7 @@ __global__ __launch_bounds__(256) void flat_kernel(const u32x4* src, uint64_t n,
     uint32_t acc = 0;
     const uint64_t stride = (uint64_t)gridDim.x * 256 * 4;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 * 4 + threadIdx.x; i < n; i += stride) {
-        u32x4 a = src[i], b2 = src[i + 256], c = src[i + 512], d = src[i + 768];
+        u32x4 a = __builtin_nontemporal_load(src + i), b2 = __builtin_nontemporal_load(src + i + 256), c = __builtin_nontemporal_load(src + i + 512), d = __builtin_nontemporal_load(src + i + 768);
         acc ^= a.x ^ b2.y ^ c.z ^ d.w;
     }
     if (acc == 0x12345678u) out[0] = acc;
