@@ -119,8 +119,11 @@ __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec
 }
 struct SpecPiece {                // one per piece of an ok pre-pass batch
     uint64_t x, R;
-    uint32_t kl, vl, count, pad;
+    uint32_t kl, vl, count, pad;  // pad: SP_STRIDE, or SP_HOP (count spans in scratch)
 };
+enum : uint32_t { SP_STRIDE = 0, SP_HOP = 1 };
+// SpecBatch.pad (diagnostics, tools/spec_diag.py): how the pre-pass batch went
+enum : uint32_t { SB_STRIDE = 1, SB_STRIDE_BROKE = 2, SB_HOP_SMALL = 3, SB_HOP_DEAD = 4, SB_HOP = 5 };
 
 // Diagnostic record per batch (tools/decode_diag.py).
 constexpr uint32_t DIAG_WORDS = 24;
@@ -943,8 +946,47 @@ __device__ uint64_t spec_base(const DecodeArgs& a, uint32_t e) {
     return wave_sum<uint64_t>(v);
 }
 
+// Spans of pieces [q0, q0 + n) (n <= SPEC_BP) from their pre-pass summaries
+// (stride arithmetic, or the hop walk's scratch), record base g0.  All
+// threads; returns the record index after the last piece.
+__device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t q0, uint32_t n,
+                                    uint64_t g0) {
+    const uint32_t tid = threadIdx.x;
+    SpecPiece* pc = reinterpret_cast<SpecPiece*>(s.data64);  // LDS scratch
+    uint64_t* pbase = reinterpret_cast<uint64_t*>(pc + SPEC_BP);
+    __syncthreads();
+    if (tid < n) pc[tid] = a.spiece[q0 + tid];
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t g = g0;
+        for (uint32_t i = 0; i < n; ++i) {
+            pbase[i] = g;
+            g += pc[i].count;
+        }
+        pbase[SPEC_BP] = g;
+    }
+    __syncthreads();
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint64_t g = uni(pbase[i]);
+        const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
+        const uint32_t kl = uni(pc[i].kl), vl = uni(pc[i].vl), cnt = uni(pc[i].count);
+        if (uni(pc[i].pad) == SP_HOP) {  // hop segment: spans were walked into scratch
+            const uint4* src =
+                reinterpret_cast<const uint4*>(a.scratch + (size_t)(q0 + i) * MAX_REC_PIECE);
+            for (uint32_t t = tid; t < cnt; t += THREADS)
+                if (g + t < a.cap) *reinterpret_cast<uint4*>(a.spans + g + t) = src[t];
+        } else {
+            for (uint32_t t = tid; t < cnt; t += THREADS)
+                if (g + t < a.cap) write_span(a.spans, g + t, x + t * R, kl, vl);
+        }
+    }
+    const uint64_t end = uni(pbase[SPEC_BP]);
+    __syncthreads();
+    return end;
+}
+
 template <bool DIAG>
-__global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
+__device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
     __shared__ DecodeSmem s;
     const uint32_t tid = threadIdx.x;
     uint64_t t_start = 0;
@@ -956,44 +998,29 @@ __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
 
     // ---- spans of the pre-pass's resolved prefix (workgroup e = batch e) ----------
     const uint32_t fb = first_bad(a.ctl, a.nspec);
-    if (blockIdx.x < fb) {
-        const uint32_t e = blockIdx.x;
+    // Only batches whose whole general batch is resolved: the general engine
+    // redoes a general batch that holds an unresolved pre-pass batch (and
+    // reuses the scratch spans of its pieces meanwhile).
+    if (blk < fb && min((blk / a.q + 1) * a.q, a.nspec) <= fb) {
+        const uint32_t e = blk;
         const uint32_t ep0 = e * a.sbp;
         const uint32_t enp = min(a.sbp, a.npieces - ep0);
-        SpecPiece* pc = reinterpret_cast<SpecPiece*>(s.data64);            // LDS scratch
-        uint64_t* pbase = reinterpret_cast<uint64_t*>(pc + SPEC_BP);
-        if (tid < enp) pc[tid] = a.spiece[ep0 + tid];
         if (tid < 64) {
             const uint64_t base = spec_base(a, e);
             if (tid == 0) s.xk = base;
         }
         __syncthreads();
-        if (tid == 0) {
-            uint64_t g = s.xk;
-            for (uint32_t i = 0; i < enp; ++i) {
-                pbase[i] = g;
-                g += pc[i].count;
-            }
-            if (e == a.nspec - 1) {  // the whole file resolved: report it
-                hg_decode_result r;
-                r.n_records = g;
-                r.kind = HG_OK;
-                r.reserved = 0;
-                r.err_offset = 0;
-                *a.result = r;
-            }
+        const uint64_t g = emit_spec_range(s, a, ep0, enp, uni(s.xk));
+        if (tid == 0 && e == a.nspec - 1) {  // the whole file resolved: report it
+            hg_decode_result r;
+            r.n_records = g;
+            r.kind = HG_OK;
+            r.reserved = 0;
+            r.err_offset = 0;
+            *a.result = r;
         }
-        __syncthreads();
-        for (uint32_t i = 0; i < enp; ++i) {
-            const uint64_t g = uni(pbase[i]);
-            const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
-            const uint32_t kl = uni(pc[i].kl), vl = uni(pc[i].vl), cnt = uni(pc[i].count);
-            for (uint32_t t = tid; t < cnt; t += THREADS)
-                if (g + t < a.cap) write_span(a.spans, g + t, x + t * R, kl, vl);
-        }
-        __syncthreads();
     }
-    if (fb >= a.nspec || blockIdx.x >= a.nbatches) return;  // nothing left for the general engine
+    if (fb >= a.nspec || blk >= a.nbatches) return;  // nothing left for the general engine
     if (tid == 0) s.batch = atomicAdd(a.ticket, 1u);
     __syncthreads();
     if (min((s.batch + 1) * a.q, a.nspec) <= fb) {
@@ -1017,6 +1044,73 @@ __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
     if (DIAG) {
         t_start = __builtin_amdgcn_s_memtime();
         dg = a.diag + (size_t)b * DIAG_WORDS;
+    }
+    // Pre-resolved: every pre-pass batch in this general batch verified and
+    // chained to its neighbour (the pre-pass resolves batches past the first
+    // unresolved one too).  Publish that result at once, look back, and if the
+    // looked-back entry is the pre-pass entry emit from the summaries -- no
+    // table bytes are read.  Otherwise the general engine below runs from the
+    // exact entry.
+    uint64_t x_exact = X_UNKNOWN;
+    {
+        const uint32_t e0 = b * a.q, e1 = min((b + 1) * a.q, a.nspec);
+        if (tid < 64) {
+            bool good = true;
+            uint64_t cnt = 0;
+            if (tid < e1 - e0) {
+                const SpecBatch sbe = a.sbatch[e0 + tid];
+                good = sbe.ok && (tid == 0 || sbe.x0 == a.sbatch[e0 + tid - 1].exit);
+                cnt = sbe.count;
+            }
+            good = __all(good);
+            cnt = wave_sum<uint64_t>(cnt);
+            if (tid == 0) {
+                s.pred_ok = good;
+                s.gk = cnt;
+                s.xk = a.sbatch[e0].x0;
+                s.exitk = a.sbatch[e1 - 1].exit;
+            }
+        }
+        __syncthreads();
+        if (uni(s.pred_ok)) {
+            const uint64_t P0 = uni(s.xk), ptot = uni(s.gk), pex = uni(s.exitk);
+            const uint64_t bb = (uint64_t)p0 * PIECE;
+            if (tid == 0) {
+                const uint32_t xrel = P0 < bb + (uint64_t)np * PIECE ? (uint32_t)(P0 - bb) : NONE_REL;
+                st_agent(&a.status[2 * b + 1], pack_status(ST_AGG, xrel, 0));
+                st_agent(&a.status[2 * b], pack_status(ST_AGG, (uint32_t)ptot, pex));
+            }
+            __syncthreads();
+            if (tid < 64) {
+                uint32_t spins = 0;
+                LookbackOut lb = lookback(a, b, spins);
+                if (tid == 0) {
+                    s.xk = lb.x;
+                    s.gk = lb.g;
+                    s.err_kind = lb.err;
+                }
+            }
+            __syncthreads();
+            const uint64_t xk0 = uni(s.xk), gk0 = uni(s.gk);
+            if (uni(s.err_kind) == HG_OK && xk0 == P0) {
+                if (tid == 0) {
+                    st_agent(&a.status[2 * b + 1], pack_status(ST_INCL, 0, gk0 + ptot));
+                    st_agent(&a.status[2 * b], pack_status(ST_INCL, (uint32_t)ptot, pex));
+                    if (b == a.nbatches - 1) {
+                        hg_decode_result r;
+                        r.n_records = gk0 + ptot;
+                        r.kind = HG_OK;
+                        r.reserved = 0;
+                        r.err_offset = 0;
+                        *a.result = r;
+                    }
+                }
+                emit_spec_range(s, a, p0, np, gk0);
+                return;
+            }
+            if (uni(s.err_kind) == HG_OK) x_exact = xk0;  // wrong entry: decode from the exact one
+        }
+        __syncthreads();  // s.pred_ok / s.xk are reused below
     }
     uint4 v[GPT];
     load_piece(a, p0, v);
@@ -1054,6 +1148,7 @@ __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
     uint32_t rounds_acc = 0;
     __syncthreads();
     if (uni(s.pred_ok)) x = uni(s.pred_exit);
+    if (x_exact != X_UNKNOWN) x = x_exact;
 #pragma nounroll
     for (uint32_t pass = 0;; ++pass) {
         gi = gk;
@@ -1205,17 +1300,276 @@ __global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
     }
 }
 
+template <bool DIAG>
+__global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
+    decode_body<DIAG>(a, blockIdx.x);
+}
+
 // ---- stride pre-pass ---------------------------------------------------------------
 // decode_spec_kernel: one workgroup per SPEC_BP pieces, no inter-workgroup
 // communication: guesses the batch entry (stride_guess), verifies every piece
 // as a stride run from the previous piece's exit and records per-piece
 // summaries.  Pure streaming (register prefetch of the next piece).  A batch
 // that is not one verified chain of stride runs is left to decode_kernel.
+// ---- hop mode (large records): read headers, not tables ---------------------------
+// A batch whose first piece has no stride run but whose records are large
+// (few header candidates in the first piece: HOP_MAX_CAND) is
+// decoded by hopping from header to header in HBM: decode output depends on
+// the 16-byte headers alone, so with ~2 KiB records (BASELINE cfg 4) only
+// ~1 cache line per record is touched instead of the whole table
+// (tools/probes/read_probe.hip: header-only reads of 1 KiB records take
+// 1/8 of the full sweep).  The batch is cut into 64 KiB segments:
+//   A. one wave per segment stages a HOP_WIN-byte window at the segment start,
+//      finds header candidates (zero-mask filter) and takes the first one whose
+//      next HOP_CHECK headers (read from HBM) are readable records;
+//   B. one lane per segment walks from its guess to the segment end, writing
+//      spans to the segment's scratch (one dependent 16-byte load per record);
+//   C. thread 0 stitches: a segment whose guess is not its predecessor's exit
+//      (a wrong guess, or no record starts in its window) is re-walked from
+//      that exit.  So the batch's spans are exact given its entry, like a
+//      stride batch's, and the pre-pass links check the entries as usual.
+constexpr uint32_t HOP_SEG_PIECES = 4;                    // 64 KiB segments
+constexpr uint32_t HOP_SEGS = SPEC_BP / HOP_SEG_PIECES;   // per pre-pass batch, at most
+constexpr uint32_t HOP_WIN = 4096;                        // guess window (bytes)
+constexpr uint32_t HOP_CHECK = 3;                         // hops a guess must survive
+constexpr uint32_t HOP_MAX_CAND = 384;                    // large-record test on piece 0
+constexpr uint32_t HOP_MAX_RECS = 128;  // a segment walk gives up past this (small records)
+constexpr uint32_t HOP_MAX_REDO = 2;    // stitch re-walks per batch before giving up
+constexpr uint32_t HOP_TRIES = 8;                         // candidates tried per lane
+constexpr uint64_t NO_HOP = ~0ull;
+
 struct SpecSmem {
-    uint64_t data64[(PIECE + 64) / 8];
+    uint64_t data64[(PIECE + 64) / 8];  // a piece, or four HOP_WIN + 16 byte windows
     uint4 halo[SPEC_BP];
     uint32_t guess;
+    uint64_t hg[HOP_SEGS];    // guessed segment entries (NO_HOP: none)
+    uint64_t hd[HOP_SEGS];    // HOP_CHECK-record span of the guess
+    uint64_t hexit[HOP_SEGS];
+    uint32_t hcnt[HOP_SEGS];
+    uint32_t hdead[HOP_SEGS];
+    uint32_t hok;
+    uint64_t hx, ht;          // batch exit and records after stitching
+    uint32_t hcode;           // SpecBatch.pad: how the batch went (SB_*)
 };
+
+__device__ __forceinline__ bool rec_ok(uint64_t q, uint64_t len, uint64_t kl, uint64_t vl) {
+    return kl <= ~0ull - vl && kl + vl <= len - q - 16 && !((kl >> 32) | (vl >> 32));
+}
+
+// Header at absolute q (q + 16 <= len) straight from HBM.
+__device__ __forceinline__ void hbm_header(const DecodeArgs& a, uint64_t q, uint64_t& kl,
+                                           uint64_t& vl) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(a.sst + q);
+    kl = p[0];
+    vl = p[1];
+}
+
+// Span of the HOP_CHECK records after the (valid) record at p, or 0 if one
+// of them cannot be read.  Reaching the end of the file exactly passes.
+__device__ uint64_t hop_check(const DecodeArgs& a, uint64_t p, uint64_t kl, uint64_t vl) {
+    uint64_t q = p + 16 + kl + vl;
+    for (uint32_t h = 0; h < HOP_CHECK; ++h) {
+        if (q == a.len) return q - p;
+        if (q + 16 > a.len) return 0;
+        hbm_header(a, q, kl, vl);
+        if (!rec_ok(q, a.len, kl, vl)) return 0;
+        q += 16 + kl + vl;
+    }
+    return q - p;
+}
+
+// Exact walk of [x, end) through HBM headers: spans to out[0..), count,
+// exit (first start >= end) and whether a record cannot be read or the
+// segment holds more than HOP_MAX_RECS records (dead: the batch is left to
+// the general engine, which reads the table instead).
+__device__ void hop_walk(const DecodeArgs& a, uint64_t x, uint64_t end, hg_span* out,
+                         uint32_t& cnt, uint64_t& exit, uint32_t& dead) {
+    uint32_t n = 0;
+    uint64_t cur = x;
+    dead = 0;
+    while (cur < end) {
+        if (n == HOP_MAX_RECS) {
+            dead = 1;
+            break;
+        }
+        uint64_t kl, vl;
+        if (cur + 16 > a.len) {
+            dead = 1;
+            break;
+        }
+        hbm_header(a, cur, kl, vl);
+        if (!rec_ok(cur, a.len, kl, vl)) {
+            dead = 1;
+            break;
+        }
+        write_span(out, n, cur, kl, vl);
+        ++n;
+        cur += 16 + kl + vl;
+    }
+    cnt = n;
+    exit = cur;
+}
+
+// Phase A for segment starting at S (absolute), by one wave, window staged in
+// w (HOP_WIN + 16 bytes).  Returns (guess, span) in every lane.
+__device__ void hop_guess(const DecodeArgs& a, const uint8_t* w, uint64_t S, uint64_t& guess,
+                          uint64_t& span) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint64_t rem = a.len - S;
+    const bool any_valid = rem >= 16;
+    const uint64_t plim64 = any_valid ? rem - 16 : 0;
+    const uint32_t plim = plim64 < 0xFFFFFFFFull ? (uint32_t)plim64 : 0xFFFFFFFFu;
+    const uint32_t clen = rem < HOP_WIN ? (uint32_t)rem : HOP_WIN;
+    unsigned long long best = ~0ull;  // (position << 40) | span
+    uint32_t tries = 0;
+#pragma unroll 1
+    for (uint32_t j = 0; j < 4 && best == ~0ull && tries < HOP_TRIES; ++j) {
+        const uint32_t gi = lane * 4 + j;
+        uint32_t c = filter_bits(w, gi, a.hz, clen, plim, any_valid);
+        while (c && tries < HOP_TRIES) {
+            const uint32_t bpos = __ffs(c) - 1;
+            c &= c - 1;
+            ++tries;
+            const uint32_t p = gi * 16 + bpos;
+            uint64_t kl, vl;
+            lds_header(w, p, kl, vl);
+            if (!rec_ok(S + p, a.len, kl, vl)) continue;
+            const uint64_t d = hop_check(a, S + p, kl, vl);
+            if (d) {
+                best = ((unsigned long long)p << 40) | (d < V40 ? d : V40);
+                break;
+            }
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const unsigned long long o = __shfl_xor(best, d, 64);
+        best = o < best ? o : best;
+    }
+    guess = best == ~0ull ? NO_HOP : S + (best >> 40);
+    span = best == ~0ull ? 0 : (best & V40);
+}
+
+// The hop-mode batch [p0, p0 + np): all threads call it.  On success fills
+// sp[] (SP_HOP pieces: segment entry and count on its first piece) and
+// returns true with X0 = entry, X = exit, total = records.
+__device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_t np,
+                          SpecPiece* sp, uint64_t& X0, uint64_t& X, uint64_t& total) {
+    const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
+    const uint32_t nseg = (np + HOP_SEG_PIECES - 1) / HOP_SEG_PIECES;
+    const uint64_t bend = min((uint64_t)(p0 + np) * PIECE, a.len);
+    // Large records?  Piece 0 is still staged: count its header candidates
+    // (a record start and its shifts pass the zero-byte filter, ~4 per record
+    // for short keys/values).  At most HOP_MAX_CAND (~512 B per record) -> hop.
+    {
+        const uint64_t base = (uint64_t)p0 * PIECE;
+        const uint64_t rem = a.len - base;
+        const bool any_valid = rem >= 16;
+        const uint64_t plim64 = any_valid ? rem - 16 : 0;
+        const uint32_t plim = plim64 < 0xFFFFFFFFull ? (uint32_t)plim64 : 0xFFFFFFFFu;
+        const uint32_t clen = rem < PIECE ? (uint32_t)rem : PIECE;
+        const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
+        uint32_t nc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < GPT; ++j)
+            nc += __popc(filter_bits(data, tid * GPT + j, a.hz, clen, plim, any_valid));
+        nc = wave_sum<uint32_t>(nc);
+        if (tid == 0) s.hcnt[0] = 0;
+        __syncthreads();
+        if (lane == 0) atomicAdd(&s.hcnt[0], nc);
+        __syncthreads();
+        if (s.hcnt[0] > HOP_MAX_CAND) {
+            s.hcode = SB_HOP_SMALL;
+            return false;
+        }
+    }
+    uint8_t* w = reinterpret_cast<uint8_t*>(s.data64) + wid * (HOP_WIN + 16);
+    // A: guesses, four segments per round (one per wave)
+    for (uint32_t r = 0; r * NW < nseg; ++r) {
+        const uint32_t k = r * NW + wid;
+        const uint64_t S = (uint64_t)(p0 + k * HOP_SEG_PIECES) * PIECE;
+        __syncthreads();
+        if (k < nseg) {
+#pragma unroll
+            for (uint32_t j = 0; j < 4; ++j)
+                *reinterpret_cast<uint4*>(w + (j * 64 + lane) * 16) =
+                    load16(a, S + (j * 64 + lane) * 16);
+            if (lane == 0) *reinterpret_cast<uint4*>(w + HOP_WIN) = load16(a, S + HOP_WIN);
+        }
+        __syncthreads();
+        if (k < nseg) {
+            uint64_t g, d;
+            hop_guess(a, w, S, g, d);
+            if (lane == 0) {
+                s.hg[k] = g;
+                s.hd[k] = d;
+            }
+        }
+    }
+    __syncthreads();
+    if (s.hg[0] == NO_HOP) {  // no entry for the batch: the general engine takes it
+        s.hcode = SB_HOP_DEAD;
+        return false;
+    }
+    // B: one lane per segment walks it into scratch
+    if (tid < nseg && s.hg[tid] != NO_HOP) {
+        const uint64_t S1 = (uint64_t)(p0 + (tid + 1) * HOP_SEG_PIECES) * PIECE;
+        uint32_t c, dd;
+        uint64_t ex;
+        hop_walk(a, s.hg[tid], min(S1, bend),
+                 a.scratch + (size_t)(p0 + tid * HOP_SEG_PIECES) * MAX_REC_PIECE, c, ex, dd);
+        s.hcnt[tid] = c;
+        s.hexit[tid] = ex;
+        s.hdead[tid] = dd;
+    }
+    __syncthreads();
+    // C: stitch in segment order (re-walk a segment entered off its guess)
+    if (tid == 0) {
+        uint32_t ok = s.hdead[0] == 0, redo = 0;
+        uint64_t x = s.hexit[0], t = s.hcnt[0];
+        for (uint32_t k = 1; k < nseg && ok; ++k) {
+            if (s.hg[k] != x) {
+                if (++redo > HOP_MAX_REDO) {
+                    ok = 0;
+                    break;
+                }
+                const uint64_t S1 = (uint64_t)(p0 + (k + 1) * HOP_SEG_PIECES) * PIECE;
+                uint32_t c, dd;
+                uint64_t ex;
+                hop_walk(a, x, min(S1, bend),
+                         a.scratch + (size_t)(p0 + k * HOP_SEG_PIECES) * MAX_REC_PIECE, c, ex, dd);
+                s.hg[k] = x;
+                s.hcnt[k] = c;
+                s.hexit[k] = ex;
+                s.hdead[k] = dd;
+            }
+            ok = s.hdead[k] == 0;
+            x = s.hexit[k];
+            t += s.hcnt[k];
+        }
+        s.hok = ok;
+        s.hx = x;
+        s.ht = t;
+        s.hcode = ok ? SB_HOP : SB_HOP_DEAD;
+    }
+    __syncthreads();
+    if (!s.hok) return false;
+    if (tid < np) {
+        const uint32_t k = tid / HOP_SEG_PIECES;
+        const bool first = tid % HOP_SEG_PIECES == 0;
+        SpecPiece o;
+        o.x = first ? s.hg[k] : 0;
+        o.R = 0;
+        o.kl = o.vl = 0;
+        o.count = first ? s.hcnt[k] : 0;
+        o.pad = SP_HOP;
+        sp[p0 + tid] = o;
+    }
+    X0 = s.hg[0];
+    X = s.hx;
+    total = s.ht;
+    return true;
+}
 
 // Stride check of one staged piece without a barrier: the run's geometry
 // (entry, R, count) follows from the uniform header at X alone, so the exit
@@ -1253,12 +1607,11 @@ __device__ __forceinline__ bool stride_geom(const uint8_t* data, uint64_t base, 
     return true;
 }
 
-__global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
-                                                              SpecPiece* sp) {
+__device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
     __shared__ SpecSmem s;
     const uint32_t tid = threadIdx.x;
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
-    const uint32_t b = blockIdx.x;
+    const uint32_t b = blk;
     const uint32_t p0 = b * a.sbp;
     const uint32_t np = min(a.sbp, a.npieces - p0);
     uint4 v[GPT];
@@ -1266,7 +1619,7 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
     uint4 h = make_uint4(0, 0, 0, 0);
     if (tid < np) h = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
     uint64_t X = 0, X0 = 0, total = 0;
-    bool ok = true;
+    bool ok = true, hop = false;
     int bad = 0;
     // Two barriers per piece: (A) the previous piece is done with LDS; stage
     // v and the halo and put the next piece's loads in flight before (B).
@@ -1293,8 +1646,8 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
             }
             __syncthreads();
             const uint32_t f = uni(s.guess);
-            if (f == NO_GUESS) {
-                ok = false;
+            if (f == NO_GUESS) {  // no stride run: large records are hopped, others left
+                hop = true;
                 break;
             }
             X = X0 = base + f;
@@ -1305,7 +1658,7 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
             break;
         }
         if (i == 0 && __syncthreads_or(bad)) {  // not a stride table: leave after one piece
-            ok = false;
+            hop = true;
             break;
         }
         if (tid == 0) {
@@ -1321,6 +1674,10 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
         total += ps.count;
         X = ps.kind == PK_EMPTY ? X : X + (uint64_t)ps.count * ps.R;
     }
+    if (hop) {
+        bad = 0;
+        ok = hop_batch(s, a, p0, np, sp, X0, X, total);
+    }
     if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
     if (tid == 0) {
         // publish (read by decode_kernel after the kernel boundary), count the
@@ -1330,13 +1687,66 @@ __global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, Spec
         o.exit = X;
         o.count = (uint32_t)total;
         o.ok = ok ? 1u : 0u;
-        o.pad = 0;
+        o.pad = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
         sb[b] = o;
         atomicAdd(&a.gsum[b / SPEC_GROUP], (unsigned long long)total);
         if (!ok || (b == 0 && X0 != 0)) mark_bad(a.ctl, a.nspec, b);
         if (b > 0) link_arrive(a, b, 0 - X0);
         if (b + 1 < a.nspec) link_arrive(a, b + 1, X);
     }
+}
+
+__global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
+                                                              SpecPiece* sp) {
+    spec_body(a, sb, sp, blockIdx.x);
+}
+
+// ---- many tables in one launch ---------------------------------------------------
+// hg_decode_batch_dev_async: every table keeps its own DecodeArgs (own
+// workspace slice: controls, statuses, scratch, pre-pass records) and the
+// single-table code runs unchanged on it; a workgroup finds its table from
+// the prefix sums of the per-table grids (binary search over <= ntab + 1
+// words).  Tickets and look-backs are per table, so the ordering argument of
+// the single-table decode holds inside each table.
+__device__ __forceinline__ uint32_t find_table(const uint32_t* pre, uint32_t ntab, uint32_t blk) {
+    uint32_t lo = 0, hi = ntab;  // pre[lo] <= blk < pre[hi]
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= blk) lo = mid; else hi = mid;
+    }
+    return uni(lo);
+}
+
+// Zero every table's control region; empty tables get their (empty) result.
+__global__ __launch_bounds__(THREADS) void decode_zero_multi(const DecodeArgs* tabs,
+                                                             const uint64_t* zero_bytes,
+                                                             uint32_t ntab) {
+    const uint32_t t = blockIdx.x;
+    if (t >= ntab) return;
+    unsigned long long* w = reinterpret_cast<unsigned long long*>(tabs[t].ctl);
+    const uint64_t n = zero_bytes[t] / 8;
+    for (uint64_t i = threadIdx.x; i < n; i += THREADS) w[i] = 0;
+    if (tabs[t].len == 0 && threadIdx.x == 0) {
+        hg_decode_result r;
+        r.n_records = 0;
+        r.kind = HG_OK;
+        r.reserved = 0;
+        r.err_offset = 0;
+        *tabs[t].result = r;
+    }
+}
+
+__global__ __launch_bounds__(THREADS) void decode_spec_multi(const DecodeArgs* tabs,
+                                                             const uint32_t* pre, uint32_t ntab) {
+    const uint32_t t = find_table(pre, ntab, blockIdx.x);
+    const DecodeArgs& a = tabs[t];
+    spec_body(a, a.sbatch, const_cast<SpecPiece*>(a.spiece), blockIdx.x - pre[t]);
+}
+
+__global__ __launch_bounds__(THREADS) void decode_multi(const DecodeArgs* tabs, const uint32_t* pre,
+                                                        uint32_t ntab) {
+    const uint32_t t = find_table(pre, ntab, blockIdx.x);
+    decode_body<false>(tabs[t], blockIdx.x - pre[t]);
 }
 
 }  // namespace hgk
@@ -1367,6 +1777,12 @@ DecodeLayout decode_layout(uint64_t len) {
 }  // namespace
 
 extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) { return decode_layout(len).bytes; }
+
+// Diagnostics (tools/spec_diag.py): geometry of the last launch.
+static uint64_t g_last_launch[8];
+extern "C" void hgk_decode_last_layout(uint64_t* out) {
+    for (int i = 0; i < 8; ++i) out[i] = g_last_launch[i];
+}
 
 namespace {
 // Workgroups of `kernel` (256 threads) resident at once on the current device.
@@ -1435,12 +1851,12 @@ uint32_t device_cus() {
 }
 }  // namespace
 
-// d_ws must hold hgk_decode_workspace_bytes(len) bytes.  The launcher zeroes
-// the statuses and the ticket (the scratch area needs no initialisation).
-// len == 0 is handled by the caller (no launch).
-extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
-                                      uint64_t cap, hg_decode_result* d_result, void* d_ws,
-                                      uint32_t* d_diag, hipStream_t stream) {
+namespace {
+// DecodeArgs of one table with the given batch geometry (bp pieces per
+// general batch, sbp per pre-pass batch); zero_bytes = control region to zero.
+hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t cap,
+                          hg_decode_result* d_result, void* d_ws, uint32_t* d_diag, uint32_t bp,
+                          uint32_t sbp, uint64_t& zero_bytes) {
     using namespace hgk;
     const DecodeLayout l = decode_layout(len);
     // Zero high bytes every genuine length field must have: any record fits
@@ -1460,34 +1876,50 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
     a.link = reinterpret_cast<unsigned long long*>(ws + l.link_off);
     a.status = reinterpret_cast<unsigned long long*>(ws + l.status_off);
     a.ticket = &ctl->ticket;
-    a.scratch = reinterpret_cast<hg_span*>(static_cast<char*>(d_ws) + l.scratch_off);
-    const uint32_t res_spec = resident_workgroups(decode_spec_kernel, 0);
-    const uint32_t res_gen = d_diag ? resident_workgroups(decode_kernel<true>, 1)
-                                    : resident_workgroups(decode_kernel<false>, 2);
-    (void)res_spec;
-    a.bp = general_pieces(l.npieces, res_gen);
-    a.sbp = spec_pieces(a.bp, l.npieces, device_cus());
+    a.scratch = reinterpret_cast<hg_span*>(ws + l.scratch_off);
+    a.bp = bp;
+    a.sbp = sbp < bp ? sbp : bp;
     a.nbatches = (uint32_t)((l.npieces + a.bp - 1) / a.bp);
     a.npieces = (uint32_t)l.npieces;
     a.hz = 8 - nb;
     a.diag = d_diag;
-    SpecBatch* sb = reinterpret_cast<SpecBatch*>(ws + l.sbatch_off);
-    SpecPiece* sp = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
-    a.sbatch = sb;
-    a.spiece = sp;
+    a.sbatch = reinterpret_cast<SpecBatch*>(ws + l.sbatch_off);
+    a.spiece = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
     a.q = a.bp / a.sbp;
-    if (hipMemsetAsync(d_ws, 0, l.status_off + 2 * (size_t)a.nbatches * 8, stream) != hipSuccess)
-        return HG_ERR_HIP;
-    // 1. stride pre-pass: verifies, links neighbours, sums records per group
+    zero_bytes = (l.status_off + 2 * (uint64_t)a.nbatches * 8 + 7) & ~7ull;
+    const uint64_t ll[8] = {l.sbatch_off, l.spiece_off, a.nspec, a.sbp, a.bp, a.nbatches,
+                            l.status_off, 0};
+    for (int i = 0; i < 8; ++i) g_last_launch[i] = ll[i];
+    return a;
+}
+}  // namespace
+
+// d_ws must hold hgk_decode_workspace_bytes(len) bytes.  The launcher zeroes
+// the statuses and the ticket (the scratch area needs no initialisation).
+// len == 0 is handled by the caller (no launch).
+extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
+                                      uint64_t cap, hg_decode_result* d_result, void* d_ws,
+                                      uint32_t* d_diag, hipStream_t stream) {
+    using namespace hgk;
+    const uint64_t npieces = (len + PIECE - 1) / PIECE;
+    const uint32_t res_gen = d_diag ? resident_workgroups(decode_kernel<true>, 1)
+                                    : resident_workgroups(decode_kernel<false>, 2);
+    const uint32_t bp = general_pieces(npieces, res_gen);
+    const uint32_t sbp = spec_pieces(bp, npieces, device_cus());
+    uint64_t zero_bytes = 0;
+    const DecodeArgs a = make_args(d_sst, len, d_spans, cap, d_result, d_ws, d_diag, bp, sbp,
+                                   zero_bytes);
+    if (hipMemsetAsync(d_ws, 0, zero_bytes, stream) != hipSuccess) return HG_ERR_HIP;
+    // 1. pre-pass (stride runs, hop walks): verifies, links neighbours, sums records per group
     // 2. decode_kernel: spans of the resolved prefix, then the general engine
     //    from the first unresolved batch on (exits at once if there is none)
     // HG_DECODE_SPEC_PAD: extra dynamic LDS per pre-pass workgroup (bytes) to cap
     // its occupancy (experiments).
     const size_t spec_pad = (size_t)env_or("HG_DECODE_SPEC_PAD", 0) > 65536 ? 0
                           : (size_t)env_or("HG_DECODE_SPEC_PAD", 0);
-    hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), spec_pad, stream, a, sb,
-                       sp);
+    hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), spec_pad, stream, a,
+                       a.sbatch, const_cast<SpecPiece*>(a.spiece));
     const uint32_t grid = a.nbatches > a.nspec ? a.nbatches : a.nspec;
     if (d_diag)
         hipLaunchKernelGGL(decode_kernel<true>, dim3(grid), dim3(THREADS), 0, stream, a);
@@ -1500,4 +1932,67 @@ extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_
                                  uint64_t cap, hg_decode_result* d_result, void* d_ws,
                                  hipStream_t stream) {
     return hgk_decode_launch_diag(d_sst, len, d_spans, cap, d_result, d_ws, nullptr, stream);
+}
+
+// Many tables, three launches in all (zero, pre-pass, decode).  Batch
+// geometry comes from the total size (the tables share the chip), so a
+// batch of small tables gets the long pre-pass batches one big table would.
+// Table i's workspace is d_ws + ws_off[i] (hgk_decode_workspace_bytes(lens[i])
+// bytes).  h_stage: pinned host memory of at least hgk_decode_multi_stage_bytes(ntab)
+// bytes, d_stage: device memory of the same size; the caller keeps h_stage
+// untouched until the stream has passed this call (the arguments are copied
+// from it asynchronously).
+extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t ntab) {
+    using namespace hgk;
+    return ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256 + ((uint64_t)ntab * 8 + 255) / 256 * 256 +
+           2 * (((uint64_t)ntab + 1) * 4 + 255) / 256 * 256;
+}
+
+extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_tables,
+                                       const uint64_t* lens, hg_span* const* d_spans,
+                                       const uint64_t* caps, hg_decode_result* d_results,
+                                       void* d_ws, const uint64_t* ws_off, void* h_stage,
+                                       void* d_stage, hipStream_t stream) {
+    using namespace hgk;
+    if (ntab == 0) return HG_OK;
+    uint64_t total_pieces = 0;
+    for (uint32_t i = 0; i < ntab; ++i) total_pieces += (lens[i] + PIECE - 1) / PIECE;
+    const uint32_t res_gen = resident_workgroups(decode_kernel<false>, 2);
+    const uint32_t bp = general_pieces(total_pieces, res_gen);
+    const uint32_t sbp = spec_pieces(bp, total_pieces, device_cus());
+    char* hs = static_cast<char*>(h_stage);
+    const uint64_t args_b = ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256;
+    const uint64_t zb_b = ((uint64_t)ntab * 8 + 255) / 256 * 256;
+    const uint64_t pre_b = (((uint64_t)ntab + 1) * 4 + 255) / 256 * 256;
+    DecodeArgs* args = reinterpret_cast<DecodeArgs*>(hs);
+    uint64_t* zb = reinterpret_cast<uint64_t*>(hs + args_b);
+    uint32_t* pre_s = reinterpret_cast<uint32_t*>(hs + args_b + zb_b);
+    uint32_t* pre_d = reinterpret_cast<uint32_t*>(hs + args_b + zb_b + pre_b);
+    pre_s[0] = pre_d[0] = 0;
+    for (uint32_t i = 0; i < ntab; ++i) {
+        args[i] = make_args(d_tables[i], lens[i], d_spans[i], caps[i], d_results + i,
+                            static_cast<char*>(d_ws) + ws_off[i], nullptr, bp, sbp, zb[i]);
+        const uint32_t gs = lens[i] ? args[i].nspec : 0;
+        const uint32_t gd = lens[i] ? (args[i].nbatches > args[i].nspec ? args[i].nbatches
+                                                                          : args[i].nspec)
+                                    : 0;
+        pre_s[i + 1] = pre_s[i] + gs;
+        pre_d[i + 1] = pre_d[i] + gd;
+    }
+    const uint64_t bytes = hgk_decode_multi_stage_bytes(ntab);
+    if (hipMemcpyAsync(d_stage, h_stage, bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
+        return HG_ERR_HIP;
+    char* ds = static_cast<char*>(d_stage);
+    const DecodeArgs* dargs = reinterpret_cast<const DecodeArgs*>(ds);
+    const uint64_t* dzb = reinterpret_cast<const uint64_t*>(ds + args_b);
+    const uint32_t* dpre_s = reinterpret_cast<const uint32_t*>(ds + args_b + zb_b);
+    const uint32_t* dpre_d = reinterpret_cast<const uint32_t*>(ds + args_b + zb_b + pre_b);
+    hipLaunchKernelGGL(decode_zero_multi, dim3(ntab), dim3(THREADS), 0, stream, dargs, dzb, ntab);
+    if (pre_s[ntab])
+        hipLaunchKernelGGL(decode_spec_multi, dim3(pre_s[ntab]), dim3(THREADS), 0, stream, dargs,
+                           dpre_s, ntab);
+    if (pre_d[ntab])
+        hipLaunchKernelGGL(decode_multi, dim3(pre_d[ntab]), dim3(THREADS), 0, stream, dargs, dpre_d,
+                           ntab);
+    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

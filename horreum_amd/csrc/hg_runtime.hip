@@ -15,6 +15,10 @@
 extern "C" int hgk_decode_launch(const uint8_t*, uint64_t, hg_span*, uint64_t, hg_decode_result*,
                                  void*, hipStream_t);
 extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t);
+extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t);
+extern "C" int hgk_decode_launch_multi(uint32_t, const uint8_t* const*, const uint64_t*,
+                                       hg_span* const*, const uint64_t*, hg_decode_result*, void*,
+                                       const uint64_t*, void*, void*, hipStream_t);
 extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
                                  uint64_t*, uint32_t, hg_block*, hg_encode_result*,
                                  unsigned long long*, hipStream_t);
@@ -70,6 +74,11 @@ struct hg_ctx {
     hipStream_t aux[kAux] = {};
     DevBuf aux_ws[kAux];
     hipEvent_t fork_ev = nullptr, join_ev[kAux] = {};
+    // batched decode in one launch: all tables' workspaces, argument staging
+    DevBuf bws, bstage_d;
+    PinBuf bstage;
+    hipEvent_t bstage_ev = nullptr;
+    bool bstage_busy = false;
 };
 
 namespace {
@@ -108,6 +117,13 @@ hg_encode_result* eres(hg_ctx* c) {
 }  // namespace
 
 extern "C" {
+
+// Diagnostics only (not in include/horreum_gpu.h): the decode workspace and a
+// blocking device->host copy, for tools/spec_diag.py.
+void* hgk_ctx_workspace(hg_ctx* c) { return c ? c->ws.p : nullptr; }
+int hgk_debug_d2h(void* dst, const void* src, uint64_t n) {
+    return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
 
 int hg_abi_version(void) { return HG_ABI_VERSION; }
 
@@ -156,11 +172,13 @@ int hg_ctx_destroy(hg_ctx* c) {
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->mws,
-                      &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res})
+                      &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
+                      &c->bws, &c->bstage_d})
         if (b->p) hipFree(b->p);
-    for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage})
+    for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage, &c->bstage})
         if (b->p) hipHostFree(b->p);
     if (c->mstage_ev) hipEventDestroy(c->mstage_ev);
+    if (c->bstage_ev) hipEventDestroy(c->bstage_ev);
     for (int i = 0; i < c->naux; ++i) {
         if (c->aux[i]) hipStreamDestroy(c->aux[i]);
         if (c->aux_ws[i].p) hipFree(c->aux_ws[i].p);
@@ -244,10 +262,13 @@ int hg_decode_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* d_span
 }
 
 // Batched decode (many independent tables, e.g. the 256 tables of BASELINE
-// config 4): tables are spread round-robin over auxiliary streams forked from
-// the context stream and joined back into it, so small tables decode
-// concurrently instead of one after another.  Asynchronous; results land in
-// d_results[i].  HG_DECODE_STREAMS (1..8, default 4) sets the fan-out.
+// config 4).  Default: ONE launch chain for all tables (hgk_decode_launch_multi:
+// every table's batches in one grid, per-table workspaces side by side), so
+// small tables fill the chip together instead of queueing launch by launch.
+// HG_DECODE_BATCH=streams selects the older fan-out: tables round-robin over
+// auxiliary streams forked from and joined back into the context stream
+// (HG_DECODE_STREAMS, 1..8, default 4).  Asynchronous; results land in
+// d_results[i].
 static int ensure_aux(hg_ctx* c, int want) {
     if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
         return HG_ERR_HIP;
@@ -271,6 +292,35 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
         if (lens[i] >= kMaxLen) return HG_ERR_TOO_LARGE;
     }
     if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    const char* mode = getenv("HG_DECODE_BATCH");
+    if (!(mode && strcmp(mode, "streams") == 0)) {
+        if (ntables == 0) return HG_OK;
+        uint64_t* off = static_cast<uint64_t*>(malloc(sizeof(uint64_t) * ntables));
+        if (!off) return HG_ERR_INTERNAL;
+        uint64_t total = 0;
+        for (uint32_t i = 0; i < ntables; ++i) {
+            off[i] = total;
+            total += (hgk_decode_workspace_bytes(lens[i]) + 255) & ~255ull;
+        }
+        const uint64_t sb = hgk_decode_multi_stage_bytes(ntables);
+        int r = ensure(c, c->bws, total ? total : 256);
+        if (r == HG_OK) r = ensure(c, c->bstage_d, sb);
+        if (r == HG_OK && !c->bstage_ev &&
+            hipEventCreateWithFlags(&c->bstage_ev, hipEventDisableTiming) != hipSuccess)
+            r = HG_ERR_HIP;
+        // the previous call's arguments may still be in flight from the pinned stage
+        if (r == HG_OK && c->bstage_busy && hipEventSynchronize(c->bstage_ev) != hipSuccess)
+            r = HG_ERR_HIP;
+        if (r == HG_OK && ensure_pin(c->bstage, sb) != HG_OK) r = HG_ERR_HIP;
+        if (r == HG_OK)
+            r = hgk_decode_launch_multi(ntables, d_tables, lens, d_spans, caps, d_results, c->bws.p,
+                                        off, c->bstage.p, c->bstage_d.p, c->stream);
+        free(off);
+        if (r != HG_OK) return r;
+        if (hipEventRecord(c->bstage_ev, c->stream) != hipSuccess) return HG_ERR_HIP;
+        c->bstage_busy = true;
+        return HG_OK;
+    }
     int fan = 4;
     if (const char* e = getenv("HG_DECODE_STREAMS")) fan = atoi(e);
     fan = std::max(1, std::min<int>(fan, hg_ctx::kAux));

@@ -220,14 +220,24 @@ def test_stride_then_mixed(engine, split_mb):
     assert_same(engine, np.concatenate([d2, d1]))
 
 
-def test_batch_decode(engine):
+@pytest.mark.parametrize("mode", ["one_launch", "streams"])
+def test_batch_decode(engine, monkeypatch, mode):
     """hg_decode_batch_dev_async: several tables (incl. empty and broken ones)
-    decoded concurrently on fanned-out streams; each equals its oracle."""
+    decoded in one launch chain (default) or on fanned-out streams; each
+    equals its oracle.  Hop-mode (large record), stride and general-engine
+    tables side by side."""
     import torch
+    if mode == "streams":
+        monkeypatch.setenv("HG_DECODE_BATCH", "streams")
     names = ["fixed_16_100", "mixed_small", "tiny", "large_values", "mixed_4k", "zero_values"]
     datas = [corpus.make(nm)[2] for nm in names]
     datas.append(np.zeros(0, np.uint8))
     datas.append(datas[1][:-5])  # truncated
+    big = oracle.encode(*_large_mixed(9000, seed=71))[0]
+    datas += [big, big[:-3], np.zeros(0, np.uint8), big[: big.size // 3]]
+    bad = big.copy()
+    bad[int(oracle.decode(big)[0]["off"][4000]) + 3] = 0x7F  # klen ~2^30: body past the end
+    datas.append(bad)
     dev = [engine.to_device(d) for d in datas]
     caps = [max(d.size // 16, 1) for d in datas]
     spans = [engine.empty(c * 16) for c in caps]
@@ -269,3 +279,78 @@ def test_cfg2_full_size(engine):
     assert torch.equal(sp[:, 1], torch.full_like(idx, 16 | (100 << 32)))
     pre = sst[: 64 << 20].cpu().numpy()
     assert_same(engine, pre)
+
+
+# ---- hop mode (large records: header-to-header walks through HBM) -----------------
+@pytest.fixture
+def hop_batches(monkeypatch):
+    """Force 64-piece pre-pass batches (16 hop segments per batch) on small tables."""
+    monkeypatch.setenv("HG_DECODE_BP", "64")
+    monkeypatch.setenv("HG_DECODE_SBP", "64")
+
+
+def _large_mixed(n, seed, vmin=8, vmax=4096, tomb=0.05):
+    arena, pairs = corpus.mixed(n, 16, vmax, seed=seed, kmin=16, vmin=vmin, tomb_frac=tomb)
+    return arena, pairs
+
+
+def _fake_chain_table(n, seed, fake_v=600, reps=4):
+    """Values of 2-4 KiB that each carry a chain of `reps` self-consistent fake
+    headers (klen 0, vlen fake_v) -- windows that start inside a value lock
+    onto the fake chain, whose 3-hop span passes the large-record test."""
+    rng = np.random.default_rng(seed)
+    arena, pairs = _large_mixed(n, seed, vmin=2048, vmax=4096, tomb=0.0)
+    hdr = np.frombuffer((0).to_bytes(8, "little") + int(fake_v).to_bytes(8, "little"), np.uint8)
+    for i in range(n):
+        vo = int(pairs["val_off"][i]) + int(rng.integers(0, 64))
+        for r in range(reps):
+            o = vo + r * (16 + fake_v)
+            arena[o:o + 16] = hdr
+    data, rec_off, _, _ = oracle.encode(arena, pairs)
+    return data, rec_off
+
+
+@pytest.mark.parametrize("batches", ["adaptive", "forced64"])
+def test_hop_mode_mixed_4k(engine, request, batches):
+    """cfg-4-shaped records (16 B keys, 8..4096 B values, 5 % tombstones):
+    the pre-pass hops headers; spans bit-exact vs the oracle, whole table
+    and cut inside / at the edges of 64 KiB hop segments."""
+    if batches == "forced64":
+        request.getfixturevalue("hop_batches")
+    arena, pairs = _large_mixed(24000, seed=61)
+    data, rec_off, _, _ = oracle.encode(arena, pairs)
+    assert data.size > 40 << 20
+    assert_same(engine, data)
+    seg = 4 * CHUNK
+    cuts = {data.size - 1, data.size - 17, int(rec_off[-1]) + 3}
+    for k in (1, 5, 16, 17, 63, 64, 65):
+        for d in (-16, -1, 0, 1, 15):
+            cuts.add(k * seg + d)
+    cuts.update(int(x) + d for x in rec_off[[100, 5000, 12345]] for d in (0, 1, 16, 17))
+    for cut in sorted(c for c in cuts if 0 < c < data.size):
+        assert_same(engine, data[:cut])
+
+
+def test_hop_mode_corrupt_and_fake_chains(engine, hop_batches):
+    """Hop batches with a corrupt length mid-table (exact error kind/offset)
+    and values carrying fake header chains (wrong segment guesses are
+    re-walked from the predecessor's exit)."""
+    arena, pairs = _large_mixed(12000, seed=62)
+    data, rec_off, _, _ = oracle.encode(arena, pairs)
+    for i in (7, 3001, 9000):
+        bad = data.copy()
+        o = int(rec_off[i])
+        bad[o + 8:o + 16] = np.frombuffer((1 << 41).to_bytes(8, "little"), np.uint8)
+        assert_same(engine, bad)
+    fake, _ = _fake_chain_table(8000, seed=63)
+    assert_same(engine, fake)
+    assert_same(engine, fake[: fake.size // 2 + 999])
+
+
+def test_hop_mode_records_larger_than_window(engine, hop_batches):
+    """Values of 5-70 KiB: many 64 KiB segments have no record start in
+    their 4 KiB window (no guess) and are entered from the stitch."""
+    arena, pairs = _large_mixed(1500, seed=64, vmin=5000, vmax=70000, tomb=0.02)
+    data, _, _, _ = oracle.encode(arena, pairs)
+    assert_same(engine, data)
+    assert_same(engine, data[: data.size - 1000])
