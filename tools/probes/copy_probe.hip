@@ -1,0 +1,103 @@
+// Device-copy probe (not part of the product): what read+write rate a plain
+// 16-byte-per-lane copy reaches on this GPU, by loads in flight per lane
+// (U), cache policy and grid shape.  Sets the practical ceiling for encode
+// (which reads and writes each byte once).  Prints GB/s (read + write bytes).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy_grid(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                 uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; i < n16; i += stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + (uint64_t)u * 256;
+            if (j < n16) v[u] = NT ? __builtin_nontemporal_load(src + j) : src[j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + (uint64_t)u * 256;
+            if (j < n16) {
+                if (NT) __builtin_nontemporal_store(v[u], dst + j);
+                else dst[j] = v[u];
+            }
+        }
+    }
+}
+
+// one tile of T x 16 B per workgroup (no grid-stride loop), like encode's tiles
+template <int T, bool NT>
+__global__ __launch_bounds__(256) void copy_tile(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                 uint64_t n16) {
+    const uint64_t b = (uint64_t)blockIdx.x * 256 * T;
+#pragma unroll 1
+    for (int t = 0; t < T; ++t) {
+        const uint64_t j = b + (uint64_t)t * 256 + threadIdx.x;
+        if (j < n16) {
+            u32x4 v = NT ? __builtin_nontemporal_load(src + j) : src[j];
+            if (NT) __builtin_nontemporal_store(v, dst + j);
+            else dst[j] = v;
+        }
+    }
+}
+
+template <typename F>
+static float time_it(F f) {
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    f();
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f, tot = 0;
+    const int reps = 7;
+    for (int r = 0; r < reps; ++r) {
+        CHECK(hipEventRecord(a));
+        f();
+        CHECK(hipEventRecord(b));
+        CHECK(hipEventSynchronize(b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        tot += ms;
+        if (ms < best) best = ms;
+    }
+    return tot / reps;
+}
+
+int main() {
+    const uint64_t bytes = 3040000000ull;
+    const uint64_t n16 = bytes / 16;
+    u32x4 *src, *dst;
+    CHECK(hipMalloc(&src, bytes));
+    CHECK(hipMalloc(&dst, bytes));
+    CHECK(hipMemset(src, 1, bytes));
+    auto rep = [&](const char* name, float ms) {
+        printf("%-34s %8.4f ms  %7.1f GB/s (r+w)\n", name, ms, 2.0 * bytes / ms / 1e6);
+        fflush(stdout);
+    };
+    rep("hipMemcpyAsync d2d", time_it([&] { CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, 0)); }));
+    for (int g : {2048, 4096, 8192}) {
+        char nm[64];
+#define G(U, NT)                                                                              \
+        snprintf(nm, sizeof nm, "grid %d U=%d nt=%d", g, U, NT);                              \
+        rep(nm, time_it([&] { copy_grid<U, NT><<<g, 256>>>(src, dst, n16); }));
+        G(1, false) G(1, true) G(2, true) G(4, true) G(4, false) G(8, true)
+#undef G
+    }
+    {
+        const uint64_t nb19 = (n16 + 256 * 19 - 1) / (256 * 19);
+        rep("tile 19x1KiB nt (encode-shaped)", time_it([&] { copy_tile<19, true><<<(uint32_t)nb19, 256>>>(src, dst, n16); }));
+        rep("tile 19x1KiB default", time_it([&] { copy_tile<19, false><<<(uint32_t)nb19, 256>>>(src, dst, n16); }));
+        const uint64_t nb76 = (n16 + 256 * 76 - 1) / (256 * 76);
+        rep("tile 76x1KiB nt", time_it([&] { copy_tile<76, true><<<(uint32_t)nb76, 256>>>(src, dst, n16); }));
+    }
+    CHECK(hipFree(src));
+    CHECK(hipFree(dst));
+    return 0;
+}
