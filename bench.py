@@ -200,7 +200,8 @@ def main(argv=None):
         del spans
         torch.cuda.empty_cache()
         extra["multi_table_decode_cfg4"] = multi_table_leg(torch, eng, device, args, world, rank)
-        extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank)
+        extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank,
+                                                         host=not args.no_host and world == 1)
 
     if not args.no_host and world == 1:
         extra["host_inclusive"] = host_leg(torch, eng, sst, n, world)
@@ -407,12 +408,15 @@ def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32):
             "parity_ok": bool(ok)}
 
 
-def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000):
+def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000, host=False):
     """BASELINE config 5 scaled to one GPU's share: 8 sorted tables of 1 M
     records (16 B keys / 100 B values, 132 MB each), 25 % of each table's keys
     shared by all tables.  Decode all, device merge (newest wins), encode the
     merged table; the merge needs the record counts on the host, so the leg
-    is timed end to end with its two host syncs."""
+    is timed end to end with its two host syncs.  With `host`, also the
+    end-to-end rate from host memory (cfg 5 asks for H2D/D2H included):
+    hg_compact_host on pageable copies of the same tables (H2D of every
+    table, decode, merge, encode, D2H of the compacted table), median of 3."""
     from horreum_amd import synth
     rng = np.random.default_rng(5 + 1000 * rank)
     shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64))
@@ -423,6 +427,7 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000)
         buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=50 + t, device=device)
         bufs.append(buf)
     sizes = [b.numel() for b in bufs]
+    hosts = [b.cpu().numpy() for b in bufs] if host else None
     for sz in sizes:
         offs_b.append(total)
         total += (sz + 7) & ~7
@@ -459,10 +464,24 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000)
     in_bytes = sum(sizes)
     del arena, span_t, pairs, out
     torch.cuda.empty_cache()
-    return {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
+    line = {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
             "tables": ntab, "input_bytes_per_gpu": in_bytes, "merged_records": int(m.n),
             "merged_bytes": int(out_len), "ms": round(wall * 1e3, 3),
             "status": int(m.status)}
+    if hosts is not None:
+        hout = np.empty(in_bytes, dtype=np.uint8)  # caller-owned output, reused
+        eng.compact_host(hosts, out=hout)  # warm-up (staging buffers, workspaces)
+        ht = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            c = eng.compact_host(hosts, out=hout)
+            ht.append(time.perf_counter() - t0)
+        t = sorted(ht)[1]
+        line["host_inclusive"] = {"ms": round(t * 1e3, 2), "GiB_s": round(in_bytes / t / GIB, 3),
+                                  "parity_spot": bool(c.status == 0 and c.n == m.n
+                                                      and c.data.size == out_len)}
+        del hosts
+    return line
 
 
 if __name__ == "__main__":

@@ -261,17 +261,23 @@ class Engine:
             raise HorreumGpuError(rc, "hg_merge_dev")
         return MergeOut(rc, res.n_out, res.kind, res.table, res.index)
 
-    def compact_host(self, tables, block_stride=0):
+    def compact_host(self, tables, block_stride=0, out=None):
         """SSTableManager::compact's byte work (src/sstable/manager.rs:137-159)
         on host bytes: `tables` (bytes-like, priority order: newest first) ->
-        the compacted SSTable bytes (+ index blocks)."""
+        the compacted SSTable bytes (+ index blocks).  `out`: optional
+        caller-owned uint8 buffer of at least the total input size (the
+        result is a view of it), so repeated calls do not fault in fresh
+        pages."""
         bufs = [np.ascontiguousarray(np.frombuffer(memoryview(t).cast("B"), dtype=np.uint8))
                 for t in tables]
         k = len(bufs)
         ptrs = (ctypes.c_void_p * max(k, 1))(*[b.ctypes.data if b.size else 0 for b in bufs])
         lens = (ctypes.c_uint64 * max(k, 1))(*[b.size for b in bufs])
         cap = max(sum(b.size for b in bufs), 1)
-        out = np.empty(cap, dtype=np.uint8)
+        if out is None:
+            out = np.empty(cap, dtype=np.uint8)
+        elif out.dtype != np.uint8 or out.size < cap or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint8 array of >= %d bytes" % cap)
         n_hint = sum(b.size for b in bufs) // 16
         nb = int(self.lib.hg_block_count(n_hint, block_stride)) if block_stride else 0
         blocks = np.empty(max(nb, 1), dtype=BLOCK_DTYPE) if block_stride else None
