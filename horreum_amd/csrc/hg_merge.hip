@@ -336,32 +336,45 @@ __global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const 
                                                              const uint64_t* tile_base,
                                                              hg_pair* out, uint64_t cap,
                                                              const unsigned long long* err) {
-    __shared__ uint32_t ws[THREADS / 64];
+    // Row-major over the tile (entry t0 + k * THREADS + tid), so every load of
+    // entries and most stores of pairs are contiguous across the wave; a
+    // live entry's rank = live entries of the rows before + its wave's prefix
+    // in the row (ballot) + the lanes before it (popcount).
+    __shared__ uint32_t wc[EPT][THREADS / 64];
     if (*err != ~0ull) return;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
-    // each thread owns EPT consecutive positions of the tile
-    const uint64_t g0 = t0 + (uint64_t)tid * EPT;
     MEnt x[EPT];
-    uint32_t live = 0;
+    uint32_t pre[EPT];
+    bool lv[EPT];
 #pragma unroll
     for (uint32_t k = 0; k < EPT; ++k) {
-        if (g0 + k < a.n) {
-            x[k] = e[g0 + k];
-            live += !(x[k].tdead & DEAD);
-        } else {
-            x[k].tdead = DEAD;
+        const uint64_t g = t0 + (uint64_t)k * THREADS + tid;
+        lv[k] = false;
+        if (g < a.n) {
+            x[k] = e[g];
+            lv[k] = !(x[k].tdead & DEAD);
         }
     }
-    uint32_t incl = hgk::wave_incl_scan(live);
-    if (lane == 63) ws[wid] = incl;
-    __syncthreads();
-    uint64_t pos = tile_base[blockIdx.x] + incl - live;
-    for (uint32_t w = 0; w < wid; ++w) pos += ws[w];
+    const unsigned long long below = (1ull << lane) - 1ull;
 #pragma unroll
     for (uint32_t k = 0; k < EPT; ++k) {
-        if (x[k].tdead & DEAD) continue;
-        if (pos < cap) {
+        const unsigned long long m = __ballot(lv[k]);
+        pre[k] = (uint32_t)__popcll(m & below);
+        if (lane == 0) wc[k][wid] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    uint64_t run = tile_base[blockIdx.x];
+#pragma unroll
+    for (uint32_t k = 0; k < EPT; ++k) {
+        uint32_t row = 0, woff = 0;
+#pragma unroll
+        for (uint32_t w = 0; w < THREADS / 64; ++w) {
+            row += wc[k][w];
+            woff += w < wid ? wc[k][w] : 0u;
+        }
+        const uint64_t pos = run + woff + pre[k];
+        if (lv[k] && pos < cap) {
             const uint32_t t = x[k].tdead;
             const hg_span sp = a.spans[t][x[k].rec];
             hg_pair p;
@@ -371,7 +384,7 @@ __global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const 
             p.vlen = sp.vlen;
             out[pos] = p;
         }
-        ++pos;
+        run += row;
     }
 }
 

@@ -703,23 +703,44 @@ int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
     if (r == HG_OK) r = ensure(c, c->mspans, (span_cap ? span_cap : 1) * sizeof(hg_span));
     char* arena = static_cast<char*>(c->d_in.p);
     hg_span* spans = static_cast<hg_span*>(c->mspans.p);
+    // every table up, then one batched decode chain for all of them and one
+    // sync for the record counts (the merge needs them on the host)
     for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
         sp[t] = spans + sofs[t];
         counts[t] = 0;
-        if (!lens[t]) continue;
-        r = h2d_pipelined(c, arena + toff[t], h_tables[t], lens[t]);
-        if (r != HG_OK) break;
-        hg_err e{};
-        uint64_t nrec = 0;
-        r = hg_decode_dev(c, reinterpret_cast<const uint8_t*>(arena + toff[t]), lens[t],
-                          spans + sofs[t], lens[t] / 16, &nrec, &e);
-        if (e.kind != HG_OK) {  // the reference's read_all unwrap (storage.rs:64-66)
-            res = hg_merge_result{0, e.kind, t, e.offset};
-            r = e.kind;
-            break;
+        if (lens[t]) r = h2d_pipelined(c, arena + toff[t], h_tables[t], lens[t]);
+    }
+    if (r == HG_OK && ntables) {
+        const uint8_t** dt = new (std::nothrow) const uint8_t*[ntables];
+        hg_span** ds = new (std::nothrow) hg_span*[ntables];
+        uint64_t* caps = new (std::nothrow) uint64_t[ntables];
+        hg_decode_result* hr = new (std::nothrow) hg_decode_result[ntables];
+        r = (dt && ds && caps && hr) ? HG_OK : HG_ERR_INTERNAL;
+        if (r == HG_OK) r = ensure(c, c->d_aux, ntables * sizeof(hg_decode_result) + 64);
+        for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
+            dt[t] = reinterpret_cast<const uint8_t*>(arena + toff[t]);
+            ds[t] = spans + sofs[t];
+            caps[t] = lens[t] / 16;
         }
-        if (r != HG_OK) break;
-        counts[t] = nrec;
+        hg_decode_result* dr = static_cast<hg_decode_result*>(c->d_aux.p);
+        if (r == HG_OK) r = hg_decode_batch_dev_async(c, ntables, dt, lens, ds, caps, dr);
+        if (r == HG_OK &&
+            (hipMemcpyAsync(hr, dr, ntables * sizeof(hg_decode_result), hipMemcpyDeviceToHost,
+                            c->stream) != hipSuccess ||
+             hipStreamSynchronize(c->stream) != hipSuccess))
+            r = HG_ERR_HIP;
+        for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
+            if (hr[t].kind != HG_OK) {  // the reference's read_all unwrap (storage.rs:64-66)
+                res = hg_merge_result{0, hr[t].kind, t, hr[t].err_offset};
+                r = hr[t].kind;
+                break;
+            }
+            counts[t] = hr[t].n_records;
+        }
+        delete[] dt;
+        delete[] ds;
+        delete[] caps;
+        delete[] hr;
     }
     // 2. merge -> pairs into the arena
     uint64_t nm = 0;

@@ -105,9 +105,10 @@ class Engine:
                                            int(cap), _ptr(result)), "hg_decode_dev_async")
 
     def decode_batch_dev_async(self, tables, lens, spans, caps, results):
-        """Decode many device tables concurrently (fan-out over auxiliary
-        streams, joined into the context stream).  `results`: device tensor of
-        at least len(tables) * 24 bytes (hg_decode_result records)."""
+        """Decode many device tables in one launch chain on the context
+        stream (every table keeps its own workspace slice).  `results`:
+        device tensor of at least len(tables) * 24 bytes (hg_decode_result
+        records)."""
         k = len(tables)
         tp = (ctypes.c_void_p * max(k, 1))(*[t.data_ptr() for t in tables])
         ln = (ctypes.c_uint64 * max(k, 1))(*[int(x) for x in lens])
