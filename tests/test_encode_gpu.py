@@ -118,3 +118,61 @@ def test_cfg3_full_size(engine):
                        torch.tensor([k, v], device=engine.device).expand(n, 2))
     assert torch.equal(r[:, 16:], arena.view(n, k + v))
     assert torch.equal(rec, torch.arange(n, device=engine.device, dtype=torch.int64) * (16 + k + v))
+
+
+_EDGE_LENS = [0, 1, 7, 15, 16, 17, 31, 33]
+
+
+def _edge_pairs(rng):
+    """Uniform tiles (256 equal records: the division fast path) of every
+    (klen, vlen) in _EDGE_LENS^2, then a tile mixing them all, in a shuffled
+    arena: straddle pieces with sources shorter and longer than one 16-byte
+    window, tails of 1..15 bytes, empty keys and tombstones."""
+    combos = [(k, v) for k in _EDGE_LENS for v in _EDGE_LENS]
+    kl, vl = [], []
+    for k, v in combos[:12]:
+        kl += [k] * 256
+        vl += [v] * 256
+    for _ in range(3):
+        order = rng.permutation(len(combos))
+        kl += [combos[i][0] for i in order]
+        vl += [combos[i][1] for i in order]
+    kl, vl = np.array(kl), np.array(vl)
+    n = kl.size
+    arena = rng.integers(0, 256, size=int((kl + vl).sum()) + 4096, dtype=np.uint8)
+    pairs = np.zeros(n, dtype=oracle.PAIR_DTYPE)
+    pairs["klen"], pairs["vlen"] = kl, vl
+    # sources anywhere (unaligned), keys and values apart
+    pairs["key_off"] = rng.integers(0, arena.size - 40, n)
+    pairs["val_off"] = rng.integers(0, arena.size - 40, n)
+    return arena, pairs
+
+
+def test_piece_assembly_edges(engine):
+    """Straddle/tail pieces assembled in registers and the uniform-tile path,
+    bit-exact vs the oracle, with record offsets and blocks."""
+    rng = np.random.default_rng(11)
+    arena, pairs = _edge_pairs(rng)
+    want, wrec, wblk, _ = oracle.encode(arena, pairs, 5)
+    data, rec, blk = gpu_encode_dev(engine, arena, pairs, 5)
+    assert np.array_equal(data, want)
+    assert np.array_equal(rec, wrec) and np.array_equal(blk, wblk)
+
+
+@pytest.mark.parametrize("cut", [1, 3, 8, 15, 16, 17, 31, 40, 77])
+def test_capacity_cut_inside_pieces(engine, cut):
+    """A capacity that ends inside a header, a straddle or a tail piece: every
+    byte before it equals the oracle's, nothing at or past it is written."""
+    rng = np.random.default_rng(12 + cut)
+    arena, pairs = _edge_pairs(rng)
+    want, _, _, _ = oracle.encode(arena, pairs)
+    total = want.size
+    cap = total - cut
+    out = engine.empty(total)
+    out.fill_(0xA5)
+    rc, out_len = engine.encode_dev(engine.to_device(arena), engine.to_device(pairs.view(np.uint8)),
+                                    pairs.size, out=out, cap=cap)
+    got = out.cpu().numpy()
+    assert rc == 5 and out_len == total
+    assert np.array_equal(got[:cap], want[:cap])
+    assert (got[cap:] == 0xA5).all()
