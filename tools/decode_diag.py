@@ -69,6 +69,10 @@ def run(eng, sst, L, label):
     d = diag.cpu().numpy().astype(np.uint32).reshape(nch, W)
     d = d[d[:, 3] != 0]  # rows of batches that ran (t_end stamped)
     out["batches"] = int(d.shape[0])
+    out["label"] = label
+    if d.shape[0] == 0:  # the pre-pass resolved the whole table: no general batches ran
+        print(json.dumps(out), flush=True)
+        return out
     stats = {}
     for i, nm in enumerate(NAMES):
         col = d[:, i].astype(np.float64)
