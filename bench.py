@@ -146,7 +146,62 @@ def cpu_baseline(sst_dev, n_records, sample_mb, seconds):
     return {"value": round(passes * host.size / total_s / GIB, 4), "unit": "GiB/s", "cores": 1,
             "kind": "port",
             "sample": f"{passes} passes over the first {nrec} records ({host.size} B) of the "
-                      f"same table, hgo_bench_decode_owned, {total_s:.2f} s"}
+                      f"same table, hgo_bench_decode_owned, {total_s:.2f} s",
+            "extra": cpu_extras(host)}
+
+
+def cpu_extras(host_sample, seconds=1.0):
+    """The rest of BASELINE.md's CPU plan, on the same host core: cfg 1 (the
+    reference's own CPU case: 100 k puts of 16 B keys / 100 B values ->
+    serialize_flatten -> full iteration with deserialize_from_bytes, owned
+    buffers as src/format.rs:23-77), the cfg 3 owned encode on a 1 M-pair
+    sample, the oracle's allocation-free span decode (a tuned single-thread
+    decode: the serial walk cannot be split across cores without the
+    speculation the GPU does) and a single-thread host memcpy of the sample
+    (the CPU's own streaming ceiling for this byte work)."""
+    from horreum_amd import synth
+    from oracle import oracle
+
+    def rep(fn):
+        tot, k = 0.0, 0
+        while k == 0 or tot < seconds:
+            tot += fn()
+            k += 1
+        return tot / k
+
+    out = {"cores": 1}
+    arena, pairs = synth.fixed_arena(100_000, 16, 100, seed=1, device="cpu")
+    a, p = arena.numpy(), pairs.numpy().view(oracle.PAIR_DTYPE)
+    table, _, _, _ = oracle.encode(a, p)
+    te = rep(lambda: oracle.bench_encode_owned(a, p)[1])
+    td = rep(lambda: oracle.bench_decode_owned(table)[1])
+    out["cfg1_100k_puts"] = {"bytes": int(table.size), "encode_ms": round(te * 1e3, 3),
+                             "iterate_ms": round(td * 1e3, 3),
+                             "encode_GiB_s": round(table.size / te / GIB, 4),
+                             "iterate_GiB_s": round(table.size / td / GIB, 4)}
+    arena, pairs = synth.fixed_arena(1_000_000, 32, 256, seed=3, device="cpu")
+    a, p = arena.numpy(), pairs.numpy().view(oracle.PAIR_DTYPE)
+    te = rep(lambda: oracle.bench_encode_owned(a, p)[1])
+    out["cfg3_encode_owned_1M"] = {"bytes": 304_000_000, "GiB_s": round(304e6 / te / GIB, 4)}
+
+    def span_decode():
+        t0 = time.perf_counter()
+        oracle.decode(host_sample)
+        return time.perf_counter() - t0
+
+    td = rep(span_decode)
+    out["cfg2_span_decode_tuned"] = {"bytes": int(host_sample.size),
+                                     "GiB_s": round(host_sample.size / td / GIB, 4)}
+    dst = np.empty_like(host_sample)
+
+    def cp():
+        t0 = time.perf_counter()
+        np.copyto(dst, host_sample)
+        return time.perf_counter() - t0
+
+    tc = rep(cp)
+    out["host_memcpy_GiB_s"] = round(host_sample.size / tc / GIB, 3)
+    return out
 
 
 def main(argv=None):
