@@ -76,6 +76,7 @@ struct EncodeArgs {
     uint8_t* out;
     uint64_t cap;
     uint64_t* rec_off;  // may be null
+    uint64_t rec_base;  // added to every record offset (chunked host encode)
     hg_encode_result* result;
     const uint64_t* tile_sum;    // output bytes of every tile (encode_sums_kernel)
     const uint64_t* group_base;  // output offset of every ENC_GROUP tiles (encode_bases_kernel)
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
     if (a.rec_off)
 #pragma unroll
         for (uint32_t i = 0; i < ENC_RPT; ++i)
-            if (r0 + i < a.n) a.rec_off[r0 + i] = tb + s.off[tid * ENC_RPT + i];
+            if (r0 + i < a.n) a.rec_off[r0 + i] = a.rec_base + tb + s.off[tid * ENC_RPT + i];
 
     // ---- 3. piece copy ----------------------------------------------------------
     // Unrolled by two with swapped roles, so the in-flight loads are never
@@ -486,14 +487,16 @@ __global__ __launch_bounds__(BASES_THREADS) void encode_bases_kernel(uint64_t* g
 }
 
 // blocks[b] = {b*stride, rec_off[b*stride], rec_off[min((b+1)*stride, n)] - pos}
+// The table's total length comes from `res` (device) or, with res null, `total`.
 __global__ void blocks_kernel(const uint64_t* rec_off, uint64_t n, uint32_t stride,
-                              const hg_encode_result* res, hg_block* blocks, uint64_t nb) {
+                              const hg_encode_result* res, uint64_t total, hg_block* blocks,
+                              uint64_t nb) {
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= nb) return;
     const uint64_t first = b * stride;
     const uint64_t nxt = first + stride;
     const uint64_t pos = rec_off[first];
-    const uint64_t end = nxt < n ? rec_off[nxt] : res->out_len;
+    const uint64_t end = nxt < n ? rec_off[nxt] : (res ? res->out_len : total);
     hg_block blk;
     blk.first_rec = first;
     blk.position = pos;
@@ -512,11 +515,13 @@ extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t n) {
 // d_status: hgk_encode_workspace_bytes(n) bytes (the tile sums / bases).
 // d_rec_off may be null unless d_blocks is requested (the runtime then passes
 // workspace).  Three launches: tile sums, their scan (+ the result), copy.
-extern "C" int hgk_encode_launch(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
-                                 uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
-                                 uint32_t block_stride, hg_block* d_blocks,
-                                 hg_encode_result* d_result, unsigned long long* d_status,
-                                 hipStream_t stream) {
+// rec_base is added to every record offset written (0 for a whole table; the
+// chunk's output offset when a host encode runs the table in chunks).
+extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                                    uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
+                                    uint64_t rec_base, uint32_t block_stride, hg_block* d_blocks,
+                                    hg_encode_result* d_result, unsigned long long* d_status,
+                                    hipStream_t stream) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
@@ -541,6 +546,7 @@ extern "C" int hgk_encode_launch(const uint8_t* d_arena, const hg_pair* d_pairs,
     a.out = d_out;
     a.cap = cap;
     a.rec_off = d_rec_off;
+    a.rec_base = rec_base;
     a.result = d_result;
     a.tile_sum = tsum;
     a.group_base = gsum;
@@ -550,8 +556,32 @@ extern "C" int hgk_encode_launch(const uint8_t* d_arena, const hg_pair* d_pairs,
         const uint64_t nb = (n + block_stride - 1) / block_stride;
         const uint32_t grid = (uint32_t)((nb + 255) / 256);
         hipLaunchKernelGGL(blocks_kernel, dim3(grid), dim3(256), 0, stream, d_rec_off, n,
-                           block_stride, d_result, d_blocks, nb);
+                           block_stride, (const hg_encode_result*)d_result, (uint64_t)0, d_blocks,
+                           nb);
         if (hipGetLastError() != hipSuccess) return HG_ERR_HIP;
     }
     return HG_OK;
+}
+
+extern "C" int hgk_encode_launch(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                                 uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
+                                 uint32_t block_stride, hg_block* d_blocks,
+                                 hg_encode_result* d_result, unsigned long long* d_status,
+                                 hipStream_t stream) {
+    return hgk_encode_launch_at(d_arena, d_pairs, n, d_out, cap, d_rec_off, 0, block_stride,
+                                d_blocks, d_result, d_status, stream);
+}
+
+// Block entries of a whole table from its (global) record offsets and total
+// length (host known): the chunked host encode runs this once at the end.
+extern "C" int hgk_encode_blocks_launch(const uint64_t* d_rec_off, uint64_t n,
+                                        uint32_t block_stride, uint64_t total, hg_block* d_blocks,
+                                        hipStream_t stream) {
+    using namespace hgk;
+    if (n == 0 || block_stride == 0) return HG_OK;
+    const uint64_t nb = (n + block_stride - 1) / block_stride;
+    const uint32_t grid = (uint32_t)((nb + 255) / 256);
+    hipLaunchKernelGGL(blocks_kernel, dim3(grid), dim3(256), 0, stream, d_rec_off, n, block_stride,
+                       (const hg_encode_result*)nullptr, total, d_blocks, nb);
+    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

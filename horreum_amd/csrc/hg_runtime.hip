@@ -7,8 +7,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <new>
 #include <thread>
+#include <vector>
 
 #include "../../include/horreum_gpu.h"
 
@@ -23,6 +26,11 @@ extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8
                                  uint64_t*, uint32_t, hg_block*, hg_encode_result*,
                                  unsigned long long*, hipStream_t);
 extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t);
+extern "C" int hgk_encode_launch_at(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
+                                    uint64_t*, uint64_t, uint32_t, hg_block*, hg_encode_result*,
+                                    unsigned long long*, hipStream_t);
+extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
+                                        hipStream_t);
 extern "C" uint64_t hgk_keyindex_bytes(uint64_t);
 extern "C" int hgk_keyindex_launch(const uint8_t*, uint64_t, const hg_span*, uint64_t, void*,
                                    hipStream_t);
@@ -577,6 +585,101 @@ int hg_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uin
     return res.kind;
 }
 
+// Host encode with page-locked buffers, in chunks of ~256 MiB of output: the
+// arena goes up in order only as far as the next chunk's sources reach
+// (running max of the source ends), each chunk is encoded as soon as its
+// bytes and pairs are up, and its output comes back on a second stream while
+// the next chunk's input goes up (PCIe is full duplex).  For a memtable arena
+// in pair order (a flush) upload and download overlap almost completely;
+// scattered sources make the first chunk wait for most of the arena, which
+// degrades gracefully to upload-then-download.  Record offsets are written
+// global (rec_base = the chunk's output offset); block entries are built once
+// at the end from them.
+static int encode_host_overlapped(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len,
+                                  const hg_pair* h_pairs, uint64_t n, uint8_t* h_out,
+                                  uint64_t total, uint64_t* h_rec_off, uint32_t block_stride,
+                                  hg_block* h_blocks) {
+    // Chunk size: measured on MI355X with cfg 3 from pinned memory (tools/host_encode.py):
+    // 64 MiB 183 ms, 128 MiB 142 ms, 192-256 MiB 76 ms, 512 MiB 82 ms, one
+    // upload-then-download pass 118 ms (smaller copies behind cross-stream
+    // waits fall off a cliff).  HG_ENC_CHUNK_MB overrides.
+    const char* env_chunk = getenv("HG_ENC_CHUNK_MB");
+    const uint64_t kChunkOut = (uint64_t)(env_chunk ? std::max(1, atoi(env_chunk)) : 256) << 20;
+    const bool tm = getenv("HG_HOST_TIMING") != nullptr;
+    auto now = [] { return std::chrono::duration<double, std::milli>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count(); };
+    const double t_start = now();
+    int r = ensure_aux(c, 1);
+    if (r != HG_OK) return r;
+    hipStream_t up = c->stream, down = c->aux[0];
+    const size_t pairs_at = (arena_len + 63) & ~(size_t)63;
+    const size_t in_bytes = pairs_at + n * sizeof(hg_pair);
+    const uint64_t nb = h_blocks ? hg_block_count(n, block_stride) : 0;
+    const bool want_rec = h_rec_off || h_blocks;
+    if ((r = ensure(c, c->d_in, in_bytes)) != HG_OK) return r;
+    if ((r = ensure(c, c->d_out, total)) != HG_OK) return r;
+    if ((r = ensure(c, c->d_aux, n * sizeof(uint64_t) + nb * sizeof(hg_block) + 64)) != HG_OK)
+        return r;
+    if ((r = ensure(c, c->ws, hgk_encode_workspace_bytes(n))) != HG_OK) return r;
+    char* din = static_cast<char*>(c->d_in.p);
+    const uint8_t* darena = reinterpret_cast<const uint8_t*>(din);
+    hg_pair* dpairs = reinterpret_cast<hg_pair*>(din + pairs_at);
+    uint8_t* dout = static_cast<uint8_t*>(c->d_out.p);
+    uint64_t* drec = static_cast<uint64_t*>(c->d_aux.p);
+    hg_block* dblk =
+        reinterpret_cast<hg_block*>(static_cast<char*>(c->d_aux.p) + n * sizeof(uint64_t));
+    unsigned long long* ws = reinterpret_cast<unsigned long long*>(c->ws.p);
+    std::vector<hipEvent_t> evs;
+    uint64_t up_arena = 0, p_lo = 0, base = 0, srcmax = 0;
+    while (r == HG_OK && p_lo < n) {
+        uint64_t p_hi = p_lo, bytes = 0;
+        while (p_hi < n && (bytes < kChunkOut || p_hi == p_lo)) {
+            const hg_pair& q = h_pairs[p_hi];
+            bytes += 16ull + q.klen + q.vlen;
+            if (q.klen) srcmax = std::max(srcmax, q.key_off + q.klen);
+            if (q.vlen) srcmax = std::max(srcmax, q.val_off + q.vlen);
+            ++p_hi;
+        }
+        const uint64_t need = std::min(srcmax, arena_len);
+        if (need > up_arena) {
+            if (hipMemcpyAsync(din + up_arena, h_arena + up_arena, need - up_arena,
+                               hipMemcpyHostToDevice, up) != hipSuccess)
+                r = HG_ERR_HIP;
+            up_arena = need;
+        }
+        if (r == HG_OK && hipMemcpyAsync(dpairs + p_lo, h_pairs + p_lo,
+                                         (p_hi - p_lo) * sizeof(hg_pair), hipMemcpyHostToDevice,
+                                         up) != hipSuccess)
+            r = HG_ERR_HIP;
+        if (r == HG_OK)
+            r = hgk_encode_launch_at(darena, dpairs + p_lo, p_hi - p_lo, dout + base, bytes,
+                                     want_rec ? drec + p_lo : nullptr, base, 0, nullptr, eres(c),
+                                     ws, up);
+        hipEvent_t ev = nullptr;
+        if (r == HG_OK && (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess ||
+                           hipEventRecord(ev, up) != hipSuccess ||
+                           hipStreamWaitEvent(down, ev, 0) != hipSuccess ||
+                           hipMemcpyAsync(h_out + base, dout + base, bytes, hipMemcpyDeviceToHost,
+                                          down) != hipSuccess))
+            r = HG_ERR_HIP;
+        if (ev) evs.push_back(ev);
+        base += bytes;
+        p_lo = p_hi;
+    }
+    if (r == HG_OK && h_blocks)
+        r = hgk_encode_blocks_launch(drec, n, block_stride, total, dblk, up);
+    const double t_issued = now();
+    if (hipStreamSynchronize(up) != hipSuccess || hipStreamSynchronize(down) != hipSuccess)
+        r = r == HG_OK ? HG_ERR_HIP : r;
+    if (tm)
+        fprintf(stderr, "[hg] encode_host_overlapped: issue %.2f ms, wait %.2f ms, %zu chunks\n",
+                t_issued - t_start, now() - t_issued, evs.size());
+    for (hipEvent_t e : evs) (void)hipEventDestroy(e);
+    if (r == HG_OK && h_rec_off) r = d2h_pipelined(c, h_rec_off, drec, n * sizeof(uint64_t));
+    if (r == HG_OK && h_blocks && nb) r = d2h_pipelined(c, h_blocks, dblk, nb * sizeof(hg_block));
+    return r;
+}
+
 int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const hg_pair* h_pairs,
                    uint64_t n, uint8_t* h_out, uint64_t cap, uint64_t* h_rec_off,
                    uint32_t block_stride, hg_block* h_blocks, uint64_t* out_len) {
@@ -588,6 +691,10 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
     for (uint64_t i = 0; i < n; ++i) total += 16ull + h_pairs[i].klen + h_pairs[i].vlen;
     if (out_len) *out_len = total;
     if (total > cap) return HG_ERR_CAPACITY;
+    if (n && total && arena_len && getenv("HG_ENCODE_HOST_SERIAL") == nullptr &&
+        host_pinned(h_arena) && host_pinned(h_pairs) && host_pinned(h_out))
+        return encode_host_overlapped(c, h_arena, arena_len, h_pairs, n, h_out, total, h_rec_off,
+                                      block_stride, h_blocks);
     const uint64_t nb = h_blocks ? hg_block_count(n, block_stride) : 0;
     // d_in: arena ++ pairs; d_out: encoded bytes; d_aux: rec_off ++ blocks
     const size_t pairs_at = (arena_len + 63) & ~(size_t)63;

@@ -179,13 +179,19 @@ class Engine:
                                            int(cap), _ptr(rec_off), int(block_stride),
                                            _ptr(blocks), _ptr(result)), "hg_encode_dev_async")
 
-    def encode_host(self, arena, pairs, block_stride=0, want_rec_off=False):
-        """numpy arena (uint8) + PAIR_DTYPE records -> EncodeOut (numpy)."""
+    def encode_host(self, arena, pairs, block_stride=0, want_rec_off=False, out=None):
+        """numpy arena (uint8) + PAIR_DTYPE records -> EncodeOut (numpy).
+        `out`: optional caller-owned uint8 buffer of >= the encoded size (e.g.
+        page-locked with host_register: with arena, pairs and out all
+        page-locked the upload and download overlap in chunks)."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8)
         pairs = np.ascontiguousarray(pairs, dtype=PAIR_DTYPE)
         n = pairs.size
         total = int((16 + pairs["klen"].astype(np.uint64) + pairs["vlen"].astype(np.uint64)).sum())
-        out = np.empty(max(total, 1), dtype=np.uint8)
+        if out is None:
+            out = np.empty(max(total, 1), dtype=np.uint8)
+        elif out.dtype != np.uint8 or out.size < total or not out.flags.c_contiguous:
+            raise ValueError("out must be a contiguous uint8 array of >= %d bytes" % total)
         rec_off = np.empty(max(n, 1), dtype=np.uint64) if want_rec_off else None
         nb = int(self.lib.hg_block_count(n, block_stride)) if block_stride else 0
         blocks = np.empty(max(nb, 1), dtype=BLOCK_DTYPE) if block_stride else None

@@ -176,3 +176,40 @@ def test_capacity_cut_inside_pieces(engine, cut):
     assert rc == 5 and out_len == total
     assert np.array_equal(got[:cap], want[:cap])
     assert (got[cap:] == 0xA5).all()
+
+
+@pytest.mark.parametrize("chunk_mb", ["16", None])
+@pytest.mark.parametrize("shuffled", [False, True])
+def test_host_encode_page_locked_chunks(engine, shuffled, chunk_mb, monkeypatch):
+    """hg_encode_host with page-locked arena, pairs and output takes the
+    chunked path (upload of chunk i+1 overlapping the download of chunk i);
+    > 64 MiB of output so several chunks run, with record offsets and blocks
+    (global across chunks); shuffled pairs make every chunk reach far into
+    the arena.  HG_ENC_CHUNK_MB=16 forces several chunks."""
+    if chunk_mb:
+        monkeypatch.setenv("HG_ENC_CHUNK_MB", chunk_mb)
+    rng = np.random.default_rng(21 + shuffled)
+    n = 400_000
+    kl = rng.integers(0, 48, n)
+    vl = rng.integers(0, 400, n)
+    vl[rng.random(n) < 0.05] = 0
+    offs = np.concatenate([[0], np.cumsum(kl + vl)])
+    arena = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    pairs = np.zeros(n, dtype=oracle.PAIR_DTYPE)
+    pairs["key_off"], pairs["val_off"] = offs[:-1], offs[:-1] + kl
+    pairs["klen"], pairs["vlen"] = kl, vl
+    if shuffled:
+        pairs = pairs[rng.permutation(n)]
+    want, wrec, wblk, _ = oracle.encode(arena, pairs, 10)
+    assert want.size > (64 << 20)  # > 4 chunks of 16 MiB
+    out = np.empty(want.size, dtype=np.uint8)
+    for a in (arena, pairs, out):
+        engine.host_register(a)
+    try:
+        got = engine.encode_host(arena, pairs, block_stride=10, want_rec_off=True, out=out)
+    finally:
+        for a in (arena, pairs, out):
+            engine.host_unregister(a)
+    assert got.out_len == want.size
+    assert np.array_equal(got.data, want)
+    assert np.array_equal(got.rec_off, wrec) and np.array_equal(got.blocks, wblk)
