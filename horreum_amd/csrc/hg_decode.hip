@@ -65,6 +65,9 @@ constexpr uint32_t MAX_ROUNDS = 24;
 constexpr uint32_t CAND_CAP = 16;                 // strong candidates examined per lane
 constexpr uint32_t SHORT_WALK = 24;               // serial pre-walk budget (large records)
 constexpr uint32_t NONE_REL = 0x3FFFFFu;          // "no record starts here"
+#ifndef HG_LEADIN
+#define HG_LEADIN 1  // general batches guess their entry from a walked lead-in piece
+#endif
 constexpr uint32_t NO_GUESS = 0xFFFFFFFFu;
 
 enum : uint32_t { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2, ST_ERR = 3 };
@@ -150,6 +153,7 @@ struct DecodeSmem {
     uint8_t tgt[THREADS];               // lane is the target of another lane's exit
     uint32_t bk[PIECE / 32];            // "backed": some strong candidate's next lands here
     uint4 halo[BATCH];                  // first 16 bytes after each piece of the batch
+    uint4 lead_halo;                    // first 16 bytes of the batch (lead-in piece's halo)
     PieceSum sum[BATCH];
     uint32_t scan_tmp[NW];
     unsigned long long best, best2;     // entry-heuristic reductions
@@ -530,6 +534,12 @@ __device__ bool stride_run(const uint8_t* data, uint64_t base, uint64_t len, uin
     const uint64_t R = 16 + kl + vl;
     const uint32_t m = (uint32_t)((clen - xr + R - 1) / R);  // records starting in [xr, clen)
     if (X + m * R > len) return false;                       // the last one would not fit
+    // fail fast without a barrier: the second record's header (block-uniform)
+    if (m > 1) {
+        uint64_t k2, v2;
+        lds_header(data, xr + (uint32_t)R, k2, v2);
+        if (uni(k2) != kl || uni(v2) != vl) return false;
+    }
     int bad = 0;
     for (uint32_t t = 1 + threadIdx.x; t < m; t += THREADS)
         bad |= !hdr_eq(data, xr + (uint32_t)(t * R), kl, vl);
@@ -767,7 +777,9 @@ __device__ __forceinline__ void load_piece(const DecodeArgs& a, uint32_t p, uint
 }
 
 // All threads: v -> LDS (after the previous piece is done with it), halo, slack.
-__device__ __forceinline__ void stage_piece(DecodeSmem& s, const uint4 (&v)[GPT], uint32_t i) {
+// lead: the batch's lead-in piece (its halo is s.lead_halo).
+__device__ __forceinline__ void stage_piece(DecodeSmem& s, const uint4 (&v)[GPT], uint32_t i,
+                                            bool lead = false) {
     uint8_t* data = reinterpret_cast<uint8_t*>(s.data64);
     __syncthreads();
 #pragma unroll
@@ -775,7 +787,7 @@ __device__ __forceinline__ void stage_piece(DecodeSmem& s, const uint4 (&v)[GPT]
         *reinterpret_cast<uint4*>(data + (q * THREADS + threadIdx.x) * 16) = v[q];
     if (threadIdx.x < 4)
         *reinterpret_cast<uint4*>(data + PIECE + threadIdx.x * 16) =
-            threadIdx.x == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
+            threadIdx.x == 0 ? (lead ? s.lead_halo : s.halo[i]) : make_uint4(0, 0, 0, 0);
     __syncthreads();
 }
 
@@ -1112,8 +1124,6 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         }
         __syncthreads();  // s.pred_ok / s.xk are reused below
     }
-    uint4 v[GPT];
-    load_piece(a, p0, v);
     if (tid < np) s.halo[tid] = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
     if (tid == 0) {  // is the predecessor batch's exit already published?
         s.pred_ok = b == 0;
@@ -1149,22 +1159,40 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
     __syncthreads();
     if (uni(s.pred_ok)) x = uni(s.pred_exit);
     if (x_exact != X_UNKNOWN) x = x_exact;
+    // Lead-in: with no published entry, pass 0 first walks the piece before
+    // the batch (its own entry guessed, spans to this batch's scratch slot 0,
+    // rewritten by piece 0) and takes its exit as the batch's guessed entry.
+    // A wrong guess there has almost always re-joined the true path by the
+    // piece end, so the batch's AGG chains and its successors need not wait
+    // for an exact redo (each redo is one serial hop of the look-back chain).
+    // Same call site as the batch's pieces: no second copy of the engine.
+    const bool lead0 = HG_LEADIN && x == X_UNKNOWN && p0 > 0;
+    if (lead0 && tid == 0) s.lead_halo = load16(a, (uint64_t)p0 * PIECE);
+    uint4 v[GPT];
+    load_piece(a, lead0 ? p0 - 1 : p0, v);
 #pragma nounroll
     for (uint32_t pass = 0;; ++pass) {
         gi = gk;
         uint32_t prev_count = 0;
         uint32_t i = 0;
+        bool lead = pass == 0 && lead0;
 #pragma nounroll
-        for (; i < np; ++i) {
-            if (pass == 1) load_piece(a, p0 + i, v);  // (rare pass: no prefetch, fewer VGPRs)
-            stage_piece(s, v, i);
-            if (pass == 0 && i + 1 < np) load_piece(a, p0 + i + 1, v);  // in flight meanwhile
+        for (; i < np;) {
+            const uint32_t pi = lead ? p0 - 1 : p0 + i;
+            if (pass == 1) load_piece(a, pi, v);  // (rare pass: no prefetch, fewer VGPRs)
+            stage_piece(s, v, i, lead);
+            if (pass == 0 && (lead || i + 1 < np)) load_piece(a, pi + 1, v);  // in flight meanwhile
             PieceSum ps;
             uint64_t ex;
             uint32_t mode = 0;
             hg_span* out = pass ? a.spans : scratch + (size_t)i * MAX_REC_PIECE;
-            const int32_t e = piece_path<DIAG>(s, a, p0 + i, x, pass == 1, prev_count <= SHORT_WALK,
+            const int32_t e = piece_path<DIAG>(s, a, pi, x, pass == 1, prev_count <= SHORT_WALK,
                                                out, pass ? a.cap : ~0ull, pass ? gi : 0, ps, ex, mode);
+            if (lead) {  // the lead-in only supplies the guessed entry
+                lead = false;
+                x = e == HG_OK ? ex : X_UNKNOWN;
+                continue;
+            }
             if (i == 0 && pass == 0) X0 = x;
             nstride += mode == 1;
             ngen += mode == 2;
@@ -1190,6 +1218,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
                 ++i;
                 break;
             }
+            ++i;
         }
         resume = pass == 0 ? 0 : i;
         gres = gi;
@@ -1301,7 +1330,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
 }
 
 template <bool DIAG>
-__global__ __launch_bounds__(THREADS) void decode_kernel(DecodeArgs a) {
+__global__ __launch_bounds__(THREADS, 4) void decode_kernel(DecodeArgs a) {
     decode_body<DIAG>(a, blockIdx.x);
 }
 
