@@ -65,6 +65,12 @@ constexpr uint32_t MAX_ROUNDS = 24;
 constexpr uint32_t CAND_CAP = 16;                 // strong candidates examined per lane
 constexpr uint32_t SHORT_WALK = 24;               // serial pre-walk budget (large records)
 constexpr uint32_t NONE_REL = 0x3FFFFFu;          // "no record starts here"
+#ifndef HG_FAR_CAND
+#define HG_FAR_CAND 8192ull  // candidate records this long are guesses only as a fallback
+#endif
+#ifndef HG_EMPTY_SPEC
+#define HG_EMPTY_SPEC 1  // a piece without a guess is speculated empty (records > a piece)
+#endif
 #ifndef HG_LEADIN
 #define HG_LEADIN 1  // general batches guess their entry from a walked lead-in piece
 #endif
@@ -604,7 +610,8 @@ __device__ uint32_t stride_guess(const uint8_t* data, uint64_t rem, uint32_t cle
 // speculative walk (see the file comment).  All threads call it.
 template <bool DIAG>
 __device__ void general_prepare(DecodeSmem& s, const uint8_t* data, uint64_t base, uint64_t len,
-                                uint64_t rem, uint32_t clen, uint32_t hz, uint32_t& g, Walk& w) {
+                                uint64_t rem, uint32_t clen, uint32_t hz, uint32_t& g, Walk& w,
+                                uint64_t far = HG_FAR_CAND) {
     const uint32_t tid = threadIdx.x;
     const bool any_valid = rem >= 16;
     const uint64_t plim64 = any_valid ? rem - 16 : 0;
@@ -631,7 +638,11 @@ __device__ void general_prepare(DecodeSmem& s, const uint8_t* data, uint64_t bas
             const uint32_t p = seg0 + j * 16 + b;
             uint64_t kl, vl;
             lds_header(data, p, kl, vl);
-            if (((kl >> 32) | (vl >> 32)) || kl + vl > rem - p - 16) continue;
+            // far candidates (a record of >= HG_FAR_CAND bytes) are not used
+            // for guesses: shifted reads of a small header decode as records
+            // 256x or 65536x longer, and genuine huge records are walked
+            // exactly anyway (speed only; every path is exact from its entry)
+            if (((kl >> 32) | (vl >> 32)) || kl + vl > rem - p - 16 || kl + vl >= far) continue;
             const uint64_t nx = (uint64_t)p + 16 + kl + vl;
             if (nx < clen) {
                 if (!((s.pc[nx >> 4] >> (nx & 15)) & 1u)) continue;  // look-ahead
@@ -857,23 +868,31 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         if (f != NO_GUESS) {
             X = base + f;
         } else {
-            general_prepare<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w);
+            // first with far candidates left out of the guesses, then (a piece
+            // of nothing but far records) with every candidate
+#pragma nounroll
+            for (uint32_t attempt = 0; attempt < 2; ++attempt) {
+                general_prepare<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w,
+                                      attempt ? ~0ull : (uint64_t)HG_FAR_CAND);
+                // Park the lane walk in LDS that is free until relax() (keeps
+                // the guess's registers off the walk's): exit -> sx[1],
+                // positions -> bk, count|dead -> tgt; g is s.sg (NO_GUESS when
+                // dead).
+                const uint32_t t = threadIdx.x;
+                s.sx[1][t] = w.exit;
+                s.bk[t] = w.p01;
+                s.bk[THREADS + t] = w.p23;
+                s.tgt[t] = (uint8_t)(w.cnt | (w.dead ? 16u : 0u));
+                X = uni(general_entry_guess(s, data, base, clen));
+                g = s.sg[t];
+                w.exit = s.sx[1][t];
+                w.p01 = s.bk[t];
+                w.p23 = s.bk[THREADS + t];
+                w.cnt = s.tgt[t] & 15u;
+                w.dead = (s.tgt[t] & 16u) != 0;
+                if (X != ~0ull || HG_FAR_CAND >= (1ull << 62)) break;
+            }
             prepared = true;
-            // Park the lane walk in LDS that is free until relax() (keeps the
-            // guess's registers off the walk's): exit -> sx[1], positions ->
-            // bk, count|dead -> tgt; g is s.sg (NO_GUESS when dead).
-            const uint32_t t = threadIdx.x;
-            s.sx[1][t] = w.exit;
-            s.bk[t] = w.p01;
-            s.bk[THREADS + t] = w.p23;
-            s.tgt[t] = (uint8_t)(w.cnt | (w.dead ? 16u : 0u));
-            X = uni(general_entry_guess(s, data, base, clen));
-            g = s.sg[t];
-            w.exit = s.sx[1][t];
-            w.p01 = s.bk[t];
-            w.p23 = s.bk[THREADS + t];
-            w.cnt = s.tgt[t] & 15u;
-            w.dead = (s.tgt[t] & 16u) != 0;
             if (X == ~0ull) {
                 X = X_UNKNOWN;
                 mode = 0;
@@ -1193,7 +1212,25 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
                 x = e == HG_OK ? ex : X_UNKNOWN;
                 continue;
             }
-            if (i == 0 && pass == 0) X0 = x;
+            if (HG_EMPTY_SPEC && pass == 0 && e == E_NO_GUESS) {
+                // No record start found in this piece and no entry known yet:
+                // speculate that it holds none (records longer than a piece
+                // leave many pieces without a start).  The batch's guessed
+                // entry becomes the first guess found in a later piece; the
+                // look-back verifies it like any other guess, and the exact
+                // pass never re-joins on these pieces (their exit is unknown).
+                ps.x = X_UNKNOWN;
+                ps.exit = X_UNKNOWN;
+                ps.R = 0;
+                ps.kl = ps.vl = 0;
+                ps.count = 0;
+                ps.kind = PK_EMPTY;
+                if (tid == 0) s.sum[i] = ps;
+                prev_count = 0;
+                ++i;
+                continue;
+            }
+            if (pass == 0 && X0 == X_UNKNOWN) X0 = x;
             nstride += mode == 1;
             ngen += mode == 2;
             nserial += mode == 3;
@@ -1767,15 +1804,19 @@ __global__ __launch_bounds__(THREADS) void decode_zero_multi(const DecodeArgs* t
 
 __global__ __launch_bounds__(THREADS) void decode_spec_multi(const DecodeArgs* tabs,
                                                              const uint32_t* pre, uint32_t ntab) {
-    const uint32_t t = find_table(pre, ntab, blockIdx.x);
-    const DecodeArgs& a = tabs[t];
-    spec_body(a, a.sbatch, const_cast<SpecPiece*>(a.spiece), blockIdx.x - pre[t]);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
+    const DecodeArgs a = tabs[t];
+    spec_body(a, a.sbatch, const_cast<SpecPiece*>(a.spiece),
+              blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
 }
 
-__global__ __launch_bounds__(THREADS) void decode_multi(const DecodeArgs* tabs, const uint32_t* pre,
-                                                        uint32_t ntab) {
-    const uint32_t t = find_table(pre, ntab, blockIdx.x);
-    decode_body<false>(tabs[t], blockIdx.x - pre[t]);
+// Same register bound as decode_kernel (4 waves/SIMD); the table index is
+// block-uniform, so its arguments are fetched with scalar loads into a copy.
+__global__ __launch_bounds__(THREADS, 4) void decode_multi(const DecodeArgs* tabs,
+                                                           const uint32_t* pre, uint32_t ntab) {
+    const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
+    const DecodeArgs a = tabs[t];
+    decode_body<false>(a, blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
 }
 
 }  // namespace hgk

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Time the decode kernel on three workload shapes in one process.
 
-cfg2 (fixed 16 B / 100 B records, 1 GiB), mixed 16 B / 8..4096 B values and
-small mixed records.  Median launch time over 7 timed launches; every run's
+cfg2 (fixed 16 B / 100 B records, 1 GiB), mixed 16 B / 8..4096 B values,
+small mixed records, medium mixed records and large values up to 16 and 64 KiB.  Median launch time over 7 timed launches; every run's
 spans are checked bit-exact against the oracle (test infrastructure)."""
 import json
 import os
@@ -24,7 +24,10 @@ def workloads(dev):
     yield "cfg2 16B/100B 1GiB", synth.fixed_sst(n, 16, 100, seed=2, device=dev)
     rng = np.random.default_rng(4)
     for label, m, kr, vr in [("mixed 16B/8..4096B", 400_000, (16, 17), (8, 4097)),
-                             ("small mixed 0..24B/0..64B", 4_000_000, (0, 24), (0, 64))]:
+                             ("small mixed 0..24B/0..64B", 4_000_000, (0, 24), (0, 64)),
+                             ("medium 8..64B/64..512B", 1_500_000, (8, 65), (64, 513)),
+                             ("large 16B/0..16KiB", 60_000, (16, 17), (0, 16385)),
+                             ("huge 16B/0..64KiB", 15_000, (16, 17), (0, 65537))]:
         kl = rng.integers(*kr, m)
         vl = rng.integers(*vr, m)
         vl[rng.random(m) < 0.05] = 0
