@@ -226,9 +226,10 @@ __device__ __forceinline__ void lane_walk(const uint8_t* data, uint64_t base, ui
             w.dead = true;
             break;
         }
-        uint64_t kl, vl;
-        lds_header(data, (uint32_t)cur, kl, vl);
-        if (kl > ~0ull - vl || kl + vl > len - abs - 16 || ((kl >> 32) | (vl >> 32))) {
+        uint32_t k0, k1, v0, v1;
+        lds_header32(data, (uint32_t)cur, k0, k1, v0, v1);
+        const uint64_t body = (uint64_t)k0 + v0;
+        if ((k1 | v1) || body > len - abs - 16) {
             w.dead = true;
             break;
         }
@@ -237,7 +238,7 @@ __device__ __forceinline__ void lane_walk(const uint8_t* data, uint64_t base, ui
         if (it == 2) w.p23 = (uint32_t)cur;
         if (it == 3) w.p23 |= (uint32_t)cur << 16;
         ++w.cnt;
-        cur += 16 + kl + vl;
+        cur += 16 + body;
     }
     w.exit = base + cur;
 }
@@ -821,11 +822,13 @@ __device__ bool short_walk(DecodeSmem& s, const uint8_t* data, uint64_t len, uin
                 break;
             }
             if (n == SHORT_WALK || cur + 16 > len) break;
-            uint64_t kl, vl;
-            lds_header(data, (uint32_t)(cur - base), kl, vl);
-            if (kl > ~0ull - vl || kl + vl > len - cur - 16 || ((kl >> 32) | (vl >> 32))) break;
-            s.pc[n++] = (uint16_t)(cur - base);
-            cur += 16 + kl + vl;
+            const uint32_t p = (uint32_t)(cur - base);
+            uint32_t k0, k1, v0, v1;
+            lds_header32(data, p, k0, k1, v0, v1);
+            const uint64_t body = (uint64_t)k0 + v0;
+            if ((k1 | v1) || body > len - cur - 16) break;
+            s.pc[n++] = (uint16_t)p;
+            cur += 16 + body;
         }
         s.walk_n = n;
         s.walk_done = ok;

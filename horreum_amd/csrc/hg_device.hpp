@@ -58,6 +58,20 @@ __device__ __forceinline__ void lds_header(const uint8_t* lds, uint32_t p, uint6
     }
 }
 
+// The same header as four 32-bit halves from five dword reads (always
+// dword-aligned) and byte funnel shifts: fewer dependent operations on the
+// serial walks' critical path than the 64-bit form (reads 20 bytes from p & ~3).
+__device__ __forceinline__ void lds_header32(const uint8_t* lds, uint32_t p, uint32_t& k0,
+                                             uint32_t& k1, uint32_t& v0, uint32_t& v1) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (p & ~3u));
+    const uint32_t a0 = w[0], a1 = w[1], a2 = w[2], a3 = w[3], a4 = w[4];
+    const uint32_t sh = p & 3u;
+    k0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
+    k1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+    v0 = __builtin_amdgcn_alignbyte(a3, a2, sh);
+    v1 = __builtin_amdgcn_alignbyte(a4, a3, sh);
+}
+
 // Wave-level inclusive scan (64 lanes).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     const uint32_t lane = threadIdx.x & 63u;

@@ -112,6 +112,19 @@ def main():
         buf[offs[:-1] + i] = hdr[:, i]
     t = torch.from_numpy(buf).to(eng.device)
     run(eng, t, t.numel(), "mixed 16B/8..4096B")
+    # medium records (8..64 B keys / 64..512 B values)
+    m = 1_500_000
+    kl = rng.integers(8, 65, m)
+    vl = rng.integers(64, 513, m)
+    sizes = 16 + kl + vl
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
+    for i in range(16):
+        buf[offs[:-1] + i] = hdr[:, i]
+    t = torch.from_numpy(buf).to(eng.device)
+    run(eng, t, t.numel(), "medium 8..64B/64..512B")
+    del t
     # small mixed records
     m = 2_000_000
     kl = rng.integers(0, 24, m)
