@@ -354,3 +354,51 @@ def test_hop_mode_records_larger_than_window(engine, hop_batches):
     data, _, _, _ = oracle.encode(arena, pairs)
     assert_same(engine, data)
     assert_same(engine, data[: data.size - 1000])
+
+
+@pytest.mark.parametrize("shape", ["medium", "huge", "small_far"])
+def test_guess_rules_shapes(engine, shape):
+    """Tables that exercise the guess rules over many general batches:
+    medium records (serial short walks of up to 64 records per piece),
+    values up to 64 KiB (pieces without any record start are speculated
+    empty), and small records whose shifted header reads decode as far
+    candidates (>= 8 KiB, guesses only as a fallback).  Each whole, cut
+    mid-record and cut at a piece edge, bit-exact vs the oracle."""
+    if shape == "medium":
+        arena, pairs = corpus.mixed(60000, 64, 512, seed=81, kmin=8, vmin=64)
+    elif shape == "huge":
+        arena, pairs = corpus.mixed(900, 16, 65536, seed=82, kmin=16, tomb_frac=0.02)
+    else:
+        arena, pairs = corpus.mixed(300000, 24, 64, seed=83)
+    data, _, _, _ = oracle.encode(arena, pairs)
+    assert data.size > 8 * (1 << 20)
+    assert_same(engine, data)
+    assert_same(engine, data[: data.size - 7])
+    assert_same(engine, data[: (data.size // CHUNK - 3) * CHUNK])
+
+
+def test_batch_decode_guess_shapes(engine):
+    """One batched launch over tables of every shape the guess rules handle
+    (stride, small, medium, 4 KiB, 64 KiB values) and truncated copies."""
+    import torch
+    specs = [corpus.fixed(30000, 16, 100, seed=91),
+             corpus.mixed(150000, 24, 64, seed=92),
+             corpus.mixed(30000, 64, 512, seed=93, kmin=8, vmin=64),
+             corpus.mixed(4000, 16, 4096, seed=94, kmin=16, vmin=8),
+             corpus.mixed(500, 16, 65536, seed=95, kmin=16)]
+    datas = [oracle.encode(a, p)[0] for a, p in specs]
+    datas += [d[: d.size - 11] for d in datas]
+    dev = [engine.to_device(d) for d in datas]
+    caps = [max(d.size // 16, 1) for d in datas]
+    spans = [engine.empty(c * 16) for c in caps]
+    res = engine.empty(24 * len(datas))
+    engine.decode_batch_dev_async(dev, [d.size for d in datas], spans, caps, res)
+    torch.cuda.synchronize()
+    r = res.cpu().numpy()
+    for i, d in enumerate(datas):
+        ws, wn, wk, wo, _ = oracle.decode(d)
+        n = int(r[24 * i:24 * i + 8].view("<u8")[0])
+        kind = int(r[24 * i + 8:24 * i + 12].view("<i4")[0])
+        off = int(r[24 * i + 16:24 * i + 24].view("<u8")[0])
+        assert (n, kind, off if kind else 0) == (wn, wk, wo if wk else 0), i
+        assert np.array_equal(engine.spans_to_numpy(spans[i], min(n, caps[i])), ws), i
