@@ -17,7 +17,8 @@
 //   2. merge_check_kernel: each table strictly increasing (else UNSORTED).
 //   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
-//      positions, finds its A/B split with a 64-ary search by one wave, stages
+//      positions, takes its A/B split from merge_split_kernel (64-ary
+//      searches by one wave per tile boundary, all boundaries at once), stages
 //      both segments in LDS and places every element by a binary search in
 //      the other segment (ties: A first).  A B element whose key also occurs
 //      in A is marked dead (newest wins).  Output runs occupy the same index
@@ -196,10 +197,49 @@ __device__ __forceinline__ uint32_t lds_bound(const MergeArgs& a, const MEnt* s,
     return lo;
 }
 
+// Pair of runs holding output position d of a round: A run index pa, the
+// pair's start o, A/B boundary amid and end oend.
+__device__ __forceinline__ void pair_of(const LevelArgs& l, uint64_t d, uint32_t& pa, uint64_t& o,
+                                        uint64_t& amid, uint64_t& oend) {
+    uint32_t lo = 0, hi = l.nruns;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (l.roff[mid] <= d) lo = mid;
+        else hi = mid;
+    }
+    pa = lo & ~1u;
+    o = l.roff[pa];
+    amid = l.roff[min(pa + 1, l.nruns)];
+    oend = l.roff[min(pa + 2, l.nruns)];
+}
+
+// A split (A elements among the merged positions before it) for every tile
+// start of a round, one wave per tile boundary, all boundaries at once: the
+// merge-path searches' dependent HBM probes overlap across the grid instead
+// of sitting at the head of every tile of the round.
+__global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, LevelArgs l,
+                                                              const MEnt* in, uint64_t* split,
+                                                              uint64_t nb_tiles,
+                                                              const unsigned long long* err) {
+    const uint64_t t = (uint64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    if (t > nb_tiles) return;
+    uint64_t i = 0;
+    if (*err == ~0ull) {
+        const uint64_t d = min(t * TILE, a.n);
+        uint32_t pa;
+        uint64_t o, amid, oend;
+        pair_of(l, d, pa, o, amid, oend);
+        const uint64_t na = amid - o, nb = oend - amid;
+        i = nb == 0 ? d - o : merge_path(a, in + o, na, in + amid, nb, d - o);
+    }
+    if ((threadIdx.x & 63u) == 0) split[t] = i;
+}
+
 // err: the order check's result; merging unsorted runs is meaningless (and
 // their merge paths are not monotone), so every round skips work once set.
 __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, LevelArgs l,
                                                               const MEnt* in, MEnt* out,
+                                                              const uint64_t* split,
                                                               unsigned long long* err) {
     __shared__ LevelSmem s;
     const uint32_t tid = threadIdx.x;
@@ -210,16 +250,9 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
     uint64_t d0 = t0;
     while (d0 < t1) {
         // pair containing output position d0
-        uint32_t lo = 0, hi = l.nruns;
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (l.roff[mid] <= d0) lo = mid;
-            else hi = mid;
-        }
-        const uint32_t pa = lo & ~1u;  // A run of the pair
-        const uint64_t o = l.roff[pa];
-        const uint64_t amid = l.roff[min(pa + 1, l.nruns)];
-        const uint64_t oend = l.roff[min(pa + 2, l.nruns)];
+        uint32_t pa;
+        uint64_t o, amid, oend;
+        pair_of(l, d0, pa, o, amid, oend);
         const uint64_t d1 = min(t1, oend);
         const MEnt* A = in + o;
         const MEnt* B = in + amid;
@@ -230,15 +263,13 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
             __syncthreads();
             continue;
         }
-        if (tid < 64) {
-            const uint64_t i0 = merge_path(a, A, na, B, nb, d0 - o);
-            const uint64_t i1 = merge_path(a, A, na, B, nb, d1 - o);
-            if (tid == 0) {
-                s.i0 = i0;
-                s.i1 = i1;
-                s.has_prev = i0 > 0;
-                if (i0 > 0) s.aprev = A[i0 - 1];
-            }
+        if (tid == 0) {  // splits from merge_split_kernel (pair edges are 0 / na)
+            const uint64_t i0 = d0 == t0 ? split[blockIdx.x] : 0;
+            const uint64_t i1 = d1 == oend ? na : split[blockIdx.x + 1];
+            s.i0 = i0;
+            s.i1 = i1;
+            s.has_prev = i0 > 0;
+            if (i0 > 0 && i0 <= na) s.aprev = A[i0 - 1];
         }
         __syncthreads();
         const uint64_t i0 = s.i0, i1 = s.i1;
@@ -502,8 +533,12 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         LevelArgs l;
         l.roff = roff;
         l.nruns = (uint32_t)nruns;
+        // tile_base is free until the final count/scan: the round's splits
+        const uint32_t gs = (uint32_t)((ntiles + 1 + THREADS / 64 - 1) / (THREADS / 64));
+        hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
+                           (const MEnt*)cur, tile_base, ntiles, (const unsigned long long*)err);
         hipLaunchKernelGGL(merge_level_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
-                           l, (const MEnt*)cur, nxt, err);
+                           l, (const MEnt*)cur, nxt, (const uint64_t*)tile_base, err);
         roff += nruns + 1;
         nruns = (nruns + 1) / 2;
         MEnt* t = cur;
