@@ -96,15 +96,20 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
     if (g >= a.n) return;
     const uint32_t t = run_of(a, g);
     const uint64_t rec = g - a.run_off[t];
-    const hg_span sp = a.spans[t][rec];
+    // spans and key bytes are read once: nontemporal 16-byte loads
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 spv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.spans[t] + rec));
+    hg_span sp;
+    sp.off = ((uint64_t)spv.y << 32) | spv.x;
+    sp.klen = spv.z;
+    sp.vlen = spv.w;
     const uint64_t kofs = a.table_off[t] + sp.off + 16;
     const uint8_t* k = a.arena + kofs;
     uint64_t w0 = 0, w1 = 0;
     if (kofs + 16 <= a.arena_len) {
-        // two unaligned 8-byte loads (native on gfx950), then mask past klen
-        uint64_t r0, r1;
-        __builtin_memcpy(&r0, k, 8);
-        __builtin_memcpy(&r1, k + 8, 8);
+        // one unaligned 16-byte load (native on gfx950), then mask past klen
+        const u32x4 kv = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(k));
+        uint64_t r0 = ((uint64_t)kv.y << 32) | kv.x, r1 = ((uint64_t)kv.w << 32) | kv.z;
         const uint32_t kl = sp.klen;
         if (kl < 8) r0 &= kl ? (~0ull >> (64 - 8 * kl)) : 0ull;
         if (kl < 16) r1 &= kl <= 8 ? 0ull : (~0ull >> (64 - 8 * (kl - 8)));
