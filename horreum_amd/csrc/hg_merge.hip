@@ -222,11 +222,14 @@ __device__ __forceinline__ void pair_of(const LevelArgs& l, uint64_t d, uint32_t
 // start of a round, one wave per tile boundary, all boundaries at once: the
 // merge-path searches' dependent HBM probes overlap across the grid instead
 // of sitting at the head of every tile of the round.
+// One lane per boundary, a plain binary search (~20 dependent probes of two
+// entries): the 64-ary wave search moved ~12x the bytes for the same answer
+// and, with every boundary searched at once, was bound by those bytes.
 __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, LevelArgs l,
                                                               const MEnt* in, uint64_t* split,
                                                               uint64_t nb_tiles,
                                                               const unsigned long long* err) {
-    const uint64_t t = (uint64_t)blockIdx.x * (THREADS / 64) + (threadIdx.x >> 6);
+    const uint64_t t = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
     if (t > nb_tiles) return;
     uint64_t i = 0;
     if (*err == ~0ull) {
@@ -234,10 +237,22 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
         uint32_t pa;
         uint64_t o, amid, oend;
         pair_of(l, d, pa, o, amid, oend);
-        const uint64_t na = amid - o, nb = oend - amid;
-        i = nb == 0 ? d - o : merge_path(a, in + o, na, in + amid, nb, d - o);
+        const uint64_t na = amid - o, nb = oend - amid, dd = d - o;
+        if (nb == 0) {
+            i = dd;
+        } else {  // first c in [lo, hi) with A[c] > B[dd-c-1] (A[c] not among the first dd)
+            const MEnt* A = in + o;
+            const MEnt* B = in + amid;
+            uint64_t lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (key_cmp(a, A[mid], B[dd - mid - 1]) <= 0) lo = mid + 1;
+                else hi = mid;
+            }
+            i = lo;
+        }
     }
-    if ((threadIdx.x & 63u) == 0) split[t] = i;
+    split[t] = i;
 }
 
 // err: the order check's result; merging unsorted runs is meaningless (and
@@ -539,7 +554,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         l.roff = roff;
         l.nruns = (uint32_t)nruns;
         // tile_base is free until the final count/scan: the round's splits
-        const uint32_t gs = (uint32_t)((ntiles + 1 + THREADS / 64 - 1) / (THREADS / 64));
+        const uint32_t gs = (uint32_t)((ntiles + 1 + THREADS - 1) / THREADS);
         hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
                            (const MEnt*)cur, tile_base, ntiles, (const unsigned long long*)err);
         hipLaunchKernelGGL(merge_level_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
