@@ -17,8 +17,8 @@
 //   2. merge_check_kernel: each table strictly increasing (else UNSORTED).
 //   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
-//      positions, takes its A/B split from merge_split_kernel (64-ary
-//      searches by one wave per tile boundary, all boundaries at once), stages
+//      positions, takes its A/B split from merge_split_kernel (a binary
+//      search per tile boundary, all boundaries at once), stages
 //      both segments in LDS and places every element by a binary search in
 //      the other segment (ties: A first).  A B element whose key also occurs
 //      in A is marked dead (newest wins).  Output runs occupy the same index
