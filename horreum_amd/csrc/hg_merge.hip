@@ -19,9 +19,10 @@
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
 //      positions, takes its A/B split from merge_split_kernel (a binary
 //      search per tile boundary, all boundaries at once), stages
-//      both segments in LDS and places every element by a binary search in
-//      the other segment (ties: A first).  A B element whose key also occurs
-//      in A is marked dead (newest wins).  Output runs occupy the same index
+//      both segments in LDS, and each thread finds its 4 outputs' split by one
+//      binary search on its diagonal and merges them sequentially (ties: A
+//      first; coalesced stores).  A B element whose key also occurs in A is
+//      marked dead (newest wins).  Output runs occupy the same index
 //      ranges as their two inputs.
 //   4. merge_count / merge_scan / merge_emit kernels: the live entries, in
 //      order, become hg_pair records pointing into the arena -- the input of
@@ -182,6 +183,9 @@ __device__ uint64_t merge_path(const MergeArgs& a, const MEnt* A, uint64_t na, c
     return lo;
 }
 
+#ifndef HG_MERGE_SEQ
+#define HG_MERGE_SEQ 1  // 0: place every element by a binary search in the other segment
+#endif
 struct LevelSmem {
     MEnt seg[TILE + 2];      // A segment then B segment
     MEnt aprev;              // A element just before the tile's A segment
@@ -264,7 +268,10 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
     __shared__ LevelSmem s;
     const uint32_t tid = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
-    if (t0 >= a.n || *err != ~0ull) return;
+    if (t0 >= a.n) return;
+    // The error word is read now and tested after the segments are staged, so
+    // the tile's global round trips (split, segments) do not wait on it.
+    const unsigned long long err0 = *err;
     const uint64_t t1 = min(t0 + TILE, a.n);
     // The tile may span several output runs (pairs); handle each piece.
     uint64_t d0 = t0;
@@ -278,21 +285,17 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         const MEnt* B = in + amid;
         const uint64_t na = amid - o, nb = oend - amid;
         if (nb == 0) {  // odd run out: copied as is
+            if (err0 != ~0ull) return;
             for (uint64_t d = d0 + tid; d < d1; d += THREADS) out[d] = in[d];
             d0 = d1;
             __syncthreads();
             continue;
         }
-        if (tid == 0) {  // splits from merge_split_kernel (pair edges are 0 / na)
-            const uint64_t i0 = d0 == t0 ? split[blockIdx.x] : 0;
-            const uint64_t i1 = d1 == oend ? na : split[blockIdx.x + 1];
-            s.i0 = i0;
-            s.i1 = i1;
-            s.has_prev = i0 > 0;
-            if (i0 > 0 && i0 <= na) s.aprev = A[i0 - 1];
-        }
-        __syncthreads();
-        const uint64_t i0 = s.i0, i1 = s.i1;
+        // splits from merge_split_kernel (pair edges are 0 / na), read by every
+        // thread (uniform addresses); the A element before the tile's A segment
+        // is fetched with the segments
+        const uint64_t i0 = d0 == t0 ? split[blockIdx.x] : 0;
+        const uint64_t i1 = d1 == oend ? na : split[blockIdx.x + 1];
         if (i1 < i0 || i0 > d0 - o || i1 > d1 - o || (d1 - o) - i1 < (d0 - o) - i0) {
             // splits of sorted runs are monotone; anything else means the
             // input was not sorted: flag it (reported as UNSORTED) and stop
@@ -303,10 +306,49 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         const uint32_t nA = (uint32_t)(i1 - i0), nB = (uint32_t)(j1 - j0);
         for (uint32_t q = tid; q < nA; q += THREADS) s.seg[q] = A[i0 + q];
         for (uint32_t q = tid; q < nB; q += THREADS) s.seg[nA + q] = B[j0 + q];
+        if (tid == THREADS - 1) {
+            s.has_prev = i0 > 0;
+            if (i0 > 0 && i0 <= na) s.aprev = A[i0 - 1];
+        }
         __syncthreads();
+        if (err0 != ~0ull) return;  // an earlier round found unsorted input
         const MEnt* SA = s.seg;
         const MEnt* SB = s.seg + nA;
         MEnt* dst = out + d0;
+#if HG_MERGE_SEQ
+        // Merge path inside the tile: thread tid owns outputs [tid*EPT, +EPT),
+        // finds how many of them come from A by one binary search on its
+        // diagonal (A first on equal keys, as merge_split_kernel), then merges
+        // sequentially and stores EPT consecutive entries (coalesced).
+        {
+            const uint32_t nt = nA + nB;
+            const uint32_t d = tid * EPT;
+            if (d < nt) {
+                uint32_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (key_cmp(a, SA[mid], SB[d - 1 - mid]) <= 0) lo = mid + 1;
+                    else hi = mid;
+                }
+                uint32_t ai = lo, bj = d - lo;
+                const uint32_t e = min(d + EPT, nt);
+                for (uint32_t q = d; q < e; ++q) {
+                    MEnt x;
+                    if (bj >= nB || (ai < nA && key_cmp(a, SA[ai], SB[bj]) <= 0)) {
+                        x = SA[ai++];
+                    } else {
+                        x = SB[bj++];
+                        // newest wins: the last A element at or before it (inside
+                        // the tile, or the one just before the tile) kills an equal key
+                        const bool eq = ai > 0 ? key_cmp(a, SA[ai - 1], x) == 0
+                                               : (s.has_prev && key_cmp(a, s.aprev, x) == 0);
+                        if (eq) x.tdead |= DEAD;
+                    }
+                    dst[q] = x;
+                }
+            }
+        }
+#else
         for (uint32_t q = tid; q < nA + nB; q += THREADS) {
             MEnt x = s.seg[q];
             uint32_t pos;
@@ -324,6 +366,7 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
             }
             dst[pos] = x;
         }
+#endif
         d0 = d1;
         __syncthreads();
     }
