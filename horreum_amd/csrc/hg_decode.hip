@@ -58,15 +58,21 @@ constexpr uint32_t BATCH = 64;
 // Floor 16: with 4-piece batches a 64 MiB table has 1024 batches whose
 // speculative passes all end together, and each look-back then walks ~16
 // windows to the nearest INCL (cfg 4 measured 8.2 ms vs 4.7 ms at 16).
-constexpr uint32_t BATCH_MIN = 16;
+#ifndef HG_BATCH_MIN
+#define HG_BATCH_MIN 16
+#endif
+constexpr uint32_t BATCH_MIN = HG_BATCH_MIN;
 constexpr uint32_t MAX_REC_PIECE = PIECE / 16;    // records per piece (>= 16 B each)
 constexpr uint32_t WALK_LOG = PIECE / 16;         // serial-walk batch
 constexpr uint32_t MAX_ROUNDS = 24;
 constexpr uint32_t CAND_CAP = 16;                 // strong candidates examined per lane
 #ifndef HG_SHORT_WALK
-#define HG_SHORT_WALK 64
+#define HG_SHORT_WALK 16
 #endif
-constexpr uint32_t SHORT_WALK = HG_SHORT_WALK;  // serial pre-walk budget (24 -> 64: medium records 0.76 -> 0.69 ms)
+// serial pre-walk budget (24 -> 64: medium records 0.76 -> 0.69 ms in round 1;
+// with the lean engine 64 -> 16: medium 0.465 -> 0.39 ms, the parallel engine
+// beats one thread walking 48 records)
+constexpr uint32_t SHORT_WALK = HG_SHORT_WALK;
 constexpr uint32_t NONE_REL = 0x3FFFFFu;          // "no record starts here"
 #ifndef HG_FAR_CAND
 #define HG_FAR_CAND 8192ull  // candidate records this long are guesses only as a fallback
@@ -78,6 +84,10 @@ constexpr uint32_t NONE_REL = 0x3FFFFFu;          // "no record starts here"
 #define HG_LEADIN 1  // general batches guess their entry from a walked lead-in piece
 #endif
 constexpr uint32_t NO_GUESS = 0xFFFFFFFFu;
+#ifndef HG_LEAN
+#define HG_LEAN 1  // lean lane guesses for pieces entered at a known position (0: candidate
+                   // evaluation + backing everywhere; 2: lean entry guesses too)
+#endif
 
 enum : uint32_t { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2, ST_ERR = 3 };
 enum : uint32_t { PK_EMPTY = 0, PK_STRIDE = 1, PK_SCRATCH = 2 };
@@ -273,8 +283,8 @@ __device__ __forceinline__ void store_span(hg_span* out, uint64_t cap, uint64_t 
 // that fixed point is exact.  Returns false if it did not converge.  On
 // return cnt = this lane's records, any_dead says whether the true path hits
 // an unreadable record, and s.exitk is the piece exit.
-template <bool DIAG>
-__device__ bool relax(DecodeSmem& s, const uint8_t* data, uint64_t base, uint64_t len,
+template <bool DIAG, typename Smem>
+__device__ bool relax(Smem& s, const uint8_t* data, uint64_t base, uint64_t len,
                       uint32_t clen, uint64_t X, uint32_t& g, Walk& w, uint32_t& cnt,
                       bool& any_dead) {
     const uint32_t t = threadIdx.x;
@@ -671,6 +681,122 @@ __device__ void general_prepare(DecodeSmem& s, const uint8_t* data, uint64_t bas
     HG_PROF(2);
 }
 
+// Lean preparation (HG_LEAN, the default): each lane's guess is the first
+// candidate of its 64 bytes that reads as a record shorter than HG_FAR_CAND
+// and fits the file (a shifted read of a small header decodes as a record
+// 256x or 65536x longer), then the lane walks <= 4 records from it.  No
+// candidate evaluation beyond the guess and no "backed" marks: relax() makes
+// the result exact from the piece entry either way, and with these guesses
+// it verifies in one round on random data (profiles/r2_pmc_small.json: the
+// evaluation of every candidate was ~40 % of the engine's time).
+// Candidate positions of the 64-byte segment at seg0 (n <= 64 positions,
+// p <= plim): bit j <=> bytes [j+8-hz, j+8) and [j+16-hz, j+16) are zero.
+__device__ __forceinline__ uint64_t cand_mask(const uint8_t* data, uint32_t seg0, uint32_t n,
+                                              uint64_t plim, uint32_t hz) {
+    const uint4* q = reinterpret_cast<const uint4*>(data + seg0);
+    const uint64_t z0 = (uint64_t)zmask16(q[0]) | ((uint64_t)zmask16(q[1]) << 16) |
+                        ((uint64_t)zmask16(q[2]) << 32) | ((uint64_t)zmask16(q[3]) << 48);
+    const uint64_t z1 = zmask16(q[4]);
+    const unsigned __int128 Z = ((unsigned __int128)z1 << 64) | z0;
+    unsigned __int128 A = Z;  // bit j: bytes j .. j+hz-1 are zero
+    for (uint32_t sh = 1; sh < hz; ++sh) A &= Z >> sh;
+    uint64_t c = (uint64_t)(A >> (8 - hz)) & (uint64_t)(A >> (16 - hz));
+    if (n < 64) c &= (1ull << n) - 1ull;
+    if (plim < seg0) return 0;
+    const uint64_t lim = plim - seg0;  // j <= lim
+    if (lim < 63) c &= (2ull << lim) - 1ull;
+    return c;
+}
+
+// Each lane publishes its candidate mask (s.sx[1], free until relax()), then
+// takes the first candidate that (a) ENDS a run of consecutive candidates, (b)
+// reads as a record shorter than `far` that fits the file, and (c) whose next
+// record start is again a candidate or lies past the piece.  (a) is the key
+// rule: a genuine header with small lengths also passes the zero-byte filter
+// 1-3 bytes to its left (those reads see the length bytes shifted up, i.e.
+// 256x / 65536x longer records whose next start usually lies past the piece,
+// so (c) cannot reject them); the genuine start is the last position of that
+// run (tools/lean_sim.py: ~28 of 256 lanes guessed wrong on small records
+// without (a), ~0.1 with it).  Lanes whose run ends hold no usable guess fall
+// back to any candidate.  All threads call it.
+template <bool DIAG>
+__device__ void lean_prepare(DecodeSmem& s, const uint8_t* data, uint64_t base, uint64_t len,
+                             uint64_t rem, uint32_t clen, uint32_t hz, uint32_t& g, Walk& w,
+                             uint64_t far = HG_FAR_CAND) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t seg0 = tid * SEG;
+    const uint32_t segend = min(seg0 + SEG, clen);
+    g = NO_GUESS;
+    w.exit = 0;
+    w.cnt = 0;
+    w.dead = true;
+    w.p01 = w.p23 = 0;
+    const uint64_t cm0 =
+        (seg0 < clen && rem >= 16) ? cand_mask(data, seg0, segend - seg0, rem - 16, hz) : 0;
+    __syncthreads();  // the previous user of s.sx is done
+    s.sx[1][tid] = cm0;
+    __syncthreads();
+    HG_PROF(0);
+    const uint64_t nextbit = tid + 1 < THREADS ? (s.sx[1][tid + 1] & 1ull) : 0ull;
+    const uint64_t runend = cm0 & ~((cm0 >> 1) | (nextbit << 63));
+    uint64_t cm = runend;
+#pragma nounroll
+    for (uint32_t pass = 0; pass < 2 && g == NO_GUESS; ++pass) {
+        if (pass) cm = cm0 & ~runend;
+        while (cm) {
+            const uint32_t p = seg0 + (uint32_t)(__ffsll((long long)cm) - 1);
+            cm &= cm - 1;
+            uint32_t k0, k1, v0, v1;
+            lds_header32(data, p, k0, k1, v0, v1);
+            const uint64_t body = (uint64_t)k0 + v0;
+            if ((k1 | v1) || body >= far || body > rem - p - 16) continue;
+            const uint64_t nx = (uint64_t)p + 16 + body;
+            if (nx < clen && !((s.sx[1][nx / SEG] >> (nx % SEG)) & 1ull)) continue;  // look-ahead
+            g = p;
+            break;
+        }
+    }
+    if (g != NO_GUESS) lane_walk(data, base, len, g, segend, w);
+    HG_PROF(1);
+}
+
+// Entry guess of a piece whose entry is unknown (lean mode): the first lane
+// guess that is LINKED (its walk exits exactly on another lane's guess), else
+// the first lane guess, else -- a piece of nothing but records longer than
+// HG_FAR_CAND -- the same with every candidate.  ~0 if the piece has none.
+// Leaves g / w as lean_prepare made them for relax().  All threads call it.
+template <bool DIAG>
+__device__ uint64_t lean_entry_guess(DecodeSmem& s, const uint8_t* data, uint64_t base,
+                                     uint64_t len, uint64_t rem, uint32_t clen, uint32_t hz,
+                                     uint32_t& g, Walk& w) {
+    const uint32_t tid = threadIdx.x;
+#pragma nounroll
+    for (uint32_t attempt = 0; attempt < 2; ++attempt) {
+        lean_prepare<DIAG>(s, data, base, len, rem, clen, hz, g, w,
+                           attempt ? ~0ull : (uint64_t)HG_FAR_CAND);
+        const bool valid = g != NO_GUESS && !w.dead;
+        s.sg[tid] = valid ? g : NO_GUESS;
+        if (tid == 0) {
+            s.best = ~0ull;
+            s.best2 = ~0ull;
+        }
+        __syncthreads();
+        bool linked = false;
+        if (valid && w.exit < base + clen) {
+            const uint32_t u = (uint32_t)(w.exit - base);
+            linked = s.sg[u / SEG] == u;
+        }
+        if (linked) atomicMin(&s.best, (unsigned long long)(base + g));
+        if (valid) atomicMin(&s.best2, (unsigned long long)(base + g));
+        __syncthreads();
+        const uint64_t b1 = uni((uint64_t)s.best), b2 = uni((uint64_t)s.best2);
+        __syncthreads();
+        if (b1 != ~0ull) return b1;
+        if (b2 != ~0ull) return b2;
+    }
+    return ~0ull;
+}
+
 // Piece entry guess from the general engine.  p1 = the first strong
 // candidate whose next start is another lane's guess ("links": the first
 // record backs the second).  The true entry is in [p1, next(p1)) and links
@@ -852,7 +978,8 @@ constexpr int32_t E_NO_GUESS = 100;  // speculative entry guess found nothing
 template <bool DIAG>
 __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, uint64_t& X,
                               bool emit_now, bool try_short, hg_span* out, uint64_t cap,
-                              uint64_t gbase, PieceSum& ps, uint64_t& exit, uint32_t& mode) {
+                              uint64_t gbase, PieceSum& ps, uint64_t& exit, uint32_t& mode,
+                              bool try_stride = true) {
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     const uint64_t base = (uint64_t)p * PIECE;
     const uint64_t rem = a.len - base;
@@ -873,6 +1000,14 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         const uint32_t f = uni(s.walk_n);
         if (f != NO_GUESS) {
             X = base + f;
+        } else if (HG_LEAN == 2) {
+            X = lean_entry_guess<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w);
+            prepared = true;
+            if (X == ~0ull) {
+                X = X_UNKNOWN;
+                mode = 0;
+                return E_NO_GUESS;
+            }
         } else {
             // first with far candidates left out of the guesses, then (a piece
             // of nothing but far records) with every candidate
@@ -907,7 +1042,7 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         }
     }
     HG_PROF(6);
-    if (!prepared && stride_run(data, base, a.len, clen, X, ps)) {
+    if (!prepared && try_stride && stride_run(data, base, a.len, clen, X, ps)) {
         mode = 1;
         exit = ps.kind == PK_EMPTY ? X : X + ps.count * ps.R;
         ps.exit = exit;
@@ -930,7 +1065,12 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         exit = ps.exit = uni(s.exitk);
         return HG_OK;
     }
-    if (!prepared) general_prepare<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w);
+    if (!prepared) {
+        if (HG_LEAN)
+            lean_prepare<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w);
+        else
+            general_prepare<DIAG>(s, data, base, a.len, rem, clen, a.hz, g, w);
+    }
     bool dead = false;
     const bool conv = relax<DIAG>(s, data, base, a.len, clen, X, g, w, cnt, dead);
     if (conv && !dead) {
@@ -1199,6 +1339,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
     for (uint32_t pass = 0;; ++pass) {
         gi = gk;
         uint32_t prev_count = 0;
+        uint32_t prev_mode = 0;  // the previous piece's mode (stride attempts while it is <= 1)
         uint32_t i = 0;
         bool lead = pass == 0 && lead0;
 #pragma nounroll
@@ -1212,7 +1353,8 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             uint32_t mode = 0;
             hg_span* out = pass ? a.spans : scratch + (size_t)i * MAX_REC_PIECE;
             const int32_t e = piece_path<DIAG>(s, a, pi, x, pass == 1, prev_count <= SHORT_WALK,
-                                               out, pass ? a.cap : ~0ull, pass ? gi : 0, ps, ex, mode);
+                                               out, pass ? a.cap : ~0ull, pass ? gi : 0, ps, ex, mode,
+                                               prev_mode <= 1);
             if (lead) {  // the lead-in only supplies the guessed entry
                 lead = false;
                 x = e == HG_OK ? ex : X_UNKNOWN;
@@ -1244,6 +1386,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             if (DIAG && mode == 2) rounds_acc += s.rounds;
             nredo += pass;
             prev_count = ps.count;
+            prev_mode = mode;
             if (e != HG_OK) {
                 if (pass == 0) {  // the guessed path fails: the exact pass reports it
                     spec_ok = false;
@@ -1404,7 +1547,10 @@ constexpr uint32_t HOP_SEG_PIECES = 4;                    // 64 KiB segments
 constexpr uint32_t HOP_SEGS = SPEC_BP / HOP_SEG_PIECES;   // per pre-pass batch, at most
 constexpr uint32_t HOP_WIN = 4096;                        // guess window (bytes)
 constexpr uint32_t HOP_CHECK = 3;                         // hops a guess must survive
-constexpr uint32_t HOP_MAX_CAND = 384;                    // large-record test on piece 0
+#ifndef HG_HOP_MAX_CAND
+#define HG_HOP_MAX_CAND 96  // ~4 candidates per record: hop only records of >= ~0.7 KiB
+#endif
+constexpr uint32_t HOP_MAX_CAND = HG_HOP_MAX_CAND;        // large-record test on piece 0
 constexpr uint32_t HOP_MAX_RECS = 128;  // a segment walk gives up past this (small records)
 constexpr uint32_t HOP_MAX_REDO = 2;    // stitch re-walks per batch before giving up
 constexpr uint32_t HOP_TRIES = 8;                         // candidates tried per lane
@@ -1751,6 +1897,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
     }
     if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
+
     if (tid == 0) {
         // publish (read by decode_kernel after the kernel boundary), count the
         // records per group, then settle the two links this batch is part of

@@ -6,15 +6,16 @@
 // union of the keys, each taken from the highest-priority table holding it;
 // tombstones are kept (no filtering, :216-217).  For tables that are sorted
 // with unique keys -- every table horreum writes (memtable BTreeMap flush,
-// compaction output) -- that is exactly the reference loop's result; the
-// engine verifies the invariant and returns HG_ERR_UNSORTED otherwise.
+// compaction output) -- that is exactly the reference loop's result, and the
+// parallel merge-path rounds below build it.  Any other input (duplicate or
+// unordered keys in a table) runs the reference loop itself (step 5).
 //
 // Design (MI355X): keys are compared through 32-byte merge entries: a 16-byte
 // big-endian key prefix (one 128-bit compare decides almost every pair), the
 // key length and a (table, record) reference; only keys that agree on their
 // first 16 bytes and are both longer fetch the rest from HBM.
 //   1. merge_prep_kernel: one entry per record (runs laid out table by table).
-//   2. merge_check_kernel: each table strictly increasing (else UNSORTED).
+//   2. merge_check_kernel: each table strictly increasing (else step 5).
 //   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
 //      positions, takes its A/B split from merge_split_kernel (a binary
@@ -27,6 +28,9 @@
 //   4. merge_count / merge_scan / merge_emit kernels: the live entries, in
 //      order, become hg_pair records pointing into the arena -- the input of
 //      hg_encode_*, so compaction is decode -> merge -> encode on device.
+//   5. merge_exact_kernel: only when step 2 found a table that is not
+//      strictly increasing (every round above then skips its work): the
+//      reference loop, step by step, by one wave.
 #include "hg_device.hpp"
 
 namespace hgm {
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         const uint64_t i1 = d1 == oend ? na : split[blockIdx.x + 1];
         if (i1 < i0 || i0 > d0 - o || i1 > d1 - o || (d1 - o) - i1 < (d0 - o) - i0) {
             // splits of sorted runs are monotone; anything else means the
-            // input was not sorted: flag it (reported as UNSORTED) and stop
+            // input was not sorted: flag it (the exact loop takes over) and stop
             if (tid == 0) atomicMin(err, (unsigned long long)o);
             return;
         }
@@ -482,16 +486,112 @@ __global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const 
     }
 }
 
-// After the check: turn a found disorder into the result's error.
-__global__ void merge_error_kernel(MergeArgs a, const unsigned long long* err, const MEnt* e,
-                                   hg_merge_result* result) {
-    const unsigned long long g = *err;
-    if (g == ~0ull) return;
-    const MEnt m = e[g < a.n ? g : a.n - 1];
-    result->n_out = 0;
-    result->kind = HG_ERR_UNSORTED;
-    result->table = m.tdead & ~DEAD;
-    result->index = m.rec;
+// ---- 5. exact reference loop for tables that are not strictly increasing ----------------
+// SSTableManager::compact_inner (src/sstable/manager.rs:199-234) step by step:
+// the smallest head key wins, the FIRST table holding it in priority order is
+// emitted (min_by_key keeps the first minimum, :209-216), and every table
+// whose head key equals it advances (:218-227), until every table is
+// exhausted (:228-230).  On strictly increasing tables this is the newest-wins
+// union the merge-path rounds build; on tables with duplicate or unordered
+// keys (legal: SSTable::new accepts any pair list, src/sstable/table.rs:93-108)
+// only the loop itself defines the output, so one wave runs it: lane l owns
+// tables l, l + 64, ...; their head entries live in a per-table state array;
+// a butterfly over (key, table) picks the winner in every lane.  Runs only
+// when merge_check_kernel found a table that is not strictly increasing.
+struct ExactHead {  // 48 bytes per table
+    MEnt e;         // current head entry (valid when idx < cnt)
+    uint64_t idx, cnt;
+};
+
+__device__ __forceinline__ bool ent_before(const MergeArgs& a, const MEnt& x, const MEnt& y) {
+    const int c = key_cmp(a, x, y);
+    return c < 0 || (c == 0 && (x.tdead & ~DEAD) < (y.tdead & ~DEAD));
+}
+
+__device__ __forceinline__ MEnt shfl_ent(const MEnt& m, int src) {
+    MEnt o;
+    o.p0 = __shfl(m.p0, src, 64);
+    o.p1 = __shfl(m.p1, src, 64);
+    o.klen = __shfl(m.klen, src, 64);
+    o.tdead = __shfl(m.tdead, src, 64);
+    o.rec = __shfl(m.rec, src, 64);
+    return o;
+}
+
+__global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt* e,
+                                                         const unsigned long long* err,
+                                                         ExactHead* hs, hg_pair* out, uint64_t cap,
+                                                         hg_merge_result* result) {
+    if (*err == ~0ull) return;  // every table strictly increasing: the rounds did the merge
+    const uint32_t lane = threadIdx.x;
+    bool any = false;
+    for (uint32_t t = lane; t < a.ntables; t += 64) {
+        ExactHead h;
+        h.idx = 0;
+        h.cnt = a.run_off[t + 1] - a.run_off[t];
+        if (h.cnt) h.e = e[a.run_off[t]];
+        any |= h.cnt != 0;
+        hs[t] = h;
+    }
+    uint64_t n = 0;
+    if (__ballot(any)) {
+        for (;;) {
+            // :209-216 the first minimum head over the tables in priority order
+            bool have = false;
+            MEnt best;
+            best.p0 = best.p1 = best.rec = 0;
+            best.klen = best.tdead = 0;
+            for (uint32_t t = lane; t < a.ntables; t += 64) {
+                const ExactHead h = hs[t];
+                if (h.idx < h.cnt && (!have || ent_before(a, h.e, best))) {
+                    best = h.e;
+                    have = true;
+                }
+            }
+#pragma unroll 1
+            for (int d = 1; d < 64; d <<= 1) {
+                const MEnt o = shfl_ent(best, (int)(lane ^ (uint32_t)d));
+                const bool oh = __shfl((int)have, (int)(lane ^ (uint32_t)d), 64) != 0;
+                if (oh && (!have || ent_before(a, o, best))) {
+                    best = o;
+                    have = true;
+                }
+            }
+            // :216-217 push the winner
+            if (lane == 0 && n < cap) {
+                const uint32_t t = best.tdead & ~DEAD;
+                const hg_span sp = a.spans[t][best.rec];
+                hg_pair p;
+                p.key_off = a.table_off[t] + sp.off + 16;
+                p.val_off = p.key_off + sp.klen;
+                p.klen = sp.klen;
+                p.vlen = sp.vlen;
+                out[n] = p;
+            }
+            ++n;
+            // :218-227 advance every table whose head key equals the winner's
+            bool left = false;
+            for (uint32_t t = lane; t < a.ntables; t += 64) {
+                ExactHead h = hs[t];
+                if (h.idx < h.cnt && key_cmp(a, h.e, best) == 0) {
+                    ++h.idx;
+                    if (h.idx < h.cnt) h.e = e[a.run_off[t] + h.idx];
+                    hs[t] = h;
+                }
+                left |= h.idx < h.cnt;
+            }
+            // :228-230 stop when every candidate is None
+            if (!__ballot(left)) break;
+        }
+    }
+    if (lane == 0) {
+        hg_merge_result r;
+        r.n_out = n;
+        r.kind = HG_OK;
+        r.table = 0;
+        r.index = 0;
+        *result = r;
+    }
 }
 
 }  // namespace hgm
@@ -506,6 +606,7 @@ extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
     b += ((ntiles * 4 + 255) & ~255ull) + ((ntiles * 8 + 255) & ~255ull);
     b += ((4 * (uint64_t)ntables + 64) * 8 + 255) & ~255ull;  // device copy of the staging
     b += 256;                                                  // error word
+    b += ((uint64_t)ntables * sizeof(ExactHead) + 255) & ~255ull;  // exact-loop heads
     return b;
 }
 
@@ -565,6 +666,8 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     uint64_t* d_stage = reinterpret_cast<uint64_t*>(p);
     p += (stage_words * 8 + 255) & ~255ull;
     unsigned long long* err = reinterpret_cast<unsigned long long*>(p);
+    p += 256;
+    ExactHead* heads = reinterpret_cast<ExactHead*>(p);
     if (hipMemcpyAsync(d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
         return HG_ERR_HIP;
     if (hipMemsetAsync(err, 0xFF, 8, stream) != hipSuccess) return HG_ERR_HIP;
@@ -615,7 +718,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     hipLaunchKernelGGL(merge_emit_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
                        (const MEnt*)cur, (const uint64_t*)tile_base, d_out, cap,
                        (const unsigned long long*)err);
-    hipLaunchKernelGGL(merge_error_kernel, dim3(1), dim3(1), 0, stream, a,
-                       (const unsigned long long*)err, (const MEnt*)e0, d_result);
+    hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)e0,
+                       (const unsigned long long*)err, heads, d_out, cap, d_result);
     return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }

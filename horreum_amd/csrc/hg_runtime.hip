@@ -148,7 +148,7 @@ const char* hg_status_string(int s) {
         case HG_ERR_TOO_LARGE: return "input too large (>= 2^40 bytes)";
         case HG_ERR_INTERNAL: return "internal error (device spin timeout)";
         case HG_ERR_EMPTY_MERGE: return "merge of zero records";
-        case HG_ERR_UNSORTED: return "merge input table not strictly increasing by key";
+        case HG_ERR_UNSORTED: return "retired status (merge input not strictly increasing, ABI <= 3)";
         default: return "unknown status";
     }
 }

@@ -89,21 +89,24 @@ class SSTableManager:
         return total if ratio > self.compaction_trigger_ratio else None
 
     def compact(self):
-        """manager.rs:137-159 with the byte work on the GPU."""
+        """manager.rs:137-159 with the byte work on the GPU.  The table list
+        and the files stay untouched until the compacted bytes exist: a read
+        error, a device error (HIP, out of memory) or a format error leaves
+        every table readable (the reference moves the list out first, :146,
+        but its CPU codec has no device failures to survive)."""
         size = self.should_compact()
         if size is None:
             return False
         eng = self.engine or default_engine()
-        tables, self.tables = self.tables, []
-        datas = [t.file.read_bytes() for t in reversed(tables)]  # newest first (:148)
+        datas = [t.file.read_bytes() for t in reversed(self.tables)]  # newest first (:148)
         out = eng.compact_host(datas, block_stride=self.block_stride)
         if out.status != 0:
-            self.tables = tables
             raise CompactionError(out)
+        data = out.data.tobytes()
+        tables, self.tables = self.tables, []  # :146
         for t in tables:
             t.delete()
-        f = PersistedFile(self._new_table_path())
-        data = out.data.tobytes()
+        f = PersistedFile(self._new_table_path())  # table_0 (:77-81 on the emptied list)
         f.write_bytes(data)
         self.tables.append(SSTable(f, Index.from_encoded(data, out.blocks), size))
         return True

@@ -59,9 +59,9 @@ enum hg_status {
     HG_ERR_TOO_LARGE = -3,  /* input length >= 2^40 bytes (engine limit) */
     HG_ERR_INTERNAL = -4,   /* e.g. a bounded device spin timed out */
     HG_ERR_EMPTY_MERGE = -5, /* merge of zero records; the reference panics (src/sstable/manager.rs:213) */
-    /* A merge input table is not strictly increasing by key.  Every table
-     * horreum writes is (BTreeMap flush, compaction output); the device
-     * merge requires it and reports the first offending record. */
+    /* Retired (ABI <= 3 returned it for a merge input that was not strictly
+     * increasing).  Since ABI 4 the merge follows the reference loop on any
+     * input, so no entry point returns it. */
     HG_ERR_UNSORTED = -6
 };
 
@@ -114,8 +114,8 @@ typedef struct hg_encode_result {
 } hg_encode_result;
 
 /* Result of a merge / compaction.  kind: HG_OK, HG_ERR_CAPACITY,
- * HG_ERR_EMPTY_MERGE, HG_ERR_UNSORTED (table, index = offending record), or
- * a decode error of an input table (table, index = failing byte offset). */
+ * HG_ERR_EMPTY_MERGE, or a decode error of an input table (table, index =
+ * failing byte offset). */
 typedef struct hg_merge_result {
     uint64_t n_out;  /* merged records (tombstones included) */
     int32_t kind;
@@ -230,9 +230,13 @@ int hg_encode_host(hg_ctx* ctx, const uint8_t* h_arena, uint64_t arena_len,
  * one hg_pair per distinct key, ascending, pointing into the arena
  * (key_off/val_off relative to d_arena), tombstones kept -- ready for
  * hg_encode_* to write the compacted table.  table_off, d_spans (an array of
- * device pointers) and counts are host arrays.  Every table must be strictly
- * increasing (else HG_ERR_UNSORTED); all tables empty is HG_ERR_EMPTY_MERGE
- * (the reference panics). */
+ * device pointers) and counts are host arrays.  Tables that are strictly
+ * increasing by key (every table horreum writes) merge by parallel merge
+ * path; any other input -- duplicate keys or keys out of order inside a
+ * table, which SSTable::new accepts (src/sstable/table.rs:93-108) -- gets the
+ * reference loop's exact output (first minimum head wins, every equal head
+ * advances) from a serial device pass.  All tables empty is
+ * HG_ERR_EMPTY_MERGE (the reference panics, manager.rs:213). */
 int hg_merge_dev(hg_ctx* ctx, uint32_t ntables, const uint8_t* d_arena,
                  uint64_t arena_len, const uint64_t* table_off,
                  const hg_span* const* d_spans, const uint64_t* counts,

@@ -102,3 +102,49 @@ def test_lexicographic_open_order(engine, tmp_path):
     assert [os.path.basename(t.file.path) for t in m2.tables][:4] == \
         ["table_0", "table_1", "table_10", "table_11"]
     assert m2.get(b"key") == InternalPair(b"key", b"v9")
+
+
+def test_compaction_failure_keeps_tables(engine, tmp_path, monkeypatch):
+    """a device failure inside compaction leaves every table and
+    file in place (get() still answers, table_0 is not overwritten)."""
+    from horreum_amd.abi import HorreumGpuError, Status
+    m = SSTableManager(tmp_path, 2, 10, engine)
+    m.create([InternalPair(b"k%02d" % i, b"old%d" % i) for i in range(20)], 100)
+    before = open(tmp_path / "table_0", "rb").read()
+
+    def boom(*a, **k):
+        raise HorreumGpuError(Status.HIP, "injected")
+
+    monkeypatch.setattr(engine, "compact_host", boom)
+    with pytest.raises(HorreumGpuError):
+        m.flush([InternalPair(b"k05", b"new")], 100)
+    assert len(m.tables) == 2
+    assert open(tmp_path / "table_0", "rb").read() == before
+    assert m.get(b"k05") == InternalPair(b"k05", b"new")
+    assert m.get(b"k06") == InternalPair(b"k06", b"old6")
+    monkeypatch.undo()
+    assert m.compact() is True and len(m.tables) == 1
+    assert m.get(b"k05") == InternalPair(b"k05", b"new")
+
+
+def test_compaction_of_duplicate_key_table(engine, golden, tmp_path):
+    """create() accepts any pair list (the reference's create_table test
+    writes 'abc' twice, src/sstable/table.rs:93-108); compaction then follows
+    the reference loop exactly instead of failing."""
+    c = golden["table_create"]
+    dup = [_p(kv) for kv in c["pairs"]]
+    m = SSTableManager(tmp_path, 1, 10, engine)
+    m.create(dup, 39)
+    m.flush([InternalPair(b"abc", b"zz"), InternalPair(b"b", None)], 5)
+    assert len(m.tables) == 1
+    tabs = [[(p.key, p.value) for p in [InternalPair(b"abc", b"zz"), InternalPair(b"b", None)]],
+            [(p.key, p.value) for p in dup]]
+    datas = []
+    for t in tabs:
+        arena, rec = oracle.pack_pairs(t)
+        datas.append(oracle.encode(arena, rec)[0])
+    dec = [(d, oracle.decode(d)[0]) for d in datas]
+    refs, _ = oracle.compact(dec)
+    merged = [InternalPair(*oracle.pairs_from_spans(dec[t][0], dec[t][1][r:r + 1])[0])
+              for t, r in refs]
+    assert m.tables[0].get_all(engine) == merged

@@ -155,22 +155,95 @@ def test_merge_large(engine):
     assert res.status == 0 and np.array_equal(got, want)
 
 
-def test_merge_unsorted_and_empty(engine):
-    tables = sorted_tables(3, 500, 0.6, 13)
-    bad = list(tables[1])
-    bad[5], bad[6] = bad[6], bad[5]  # out of order
-    datas = encode_tables([tables[0], bad, tables[2]])
-    res, _, _, _ = device_merge(engine, datas)
-    assert res.status == res.kind == -6 and res.table == 1 and res.index == 6
-    dup = list(tables[2])
-    dup.insert(3, dup[3])  # duplicate key: not strictly increasing
-    res, _, _, _ = device_merge(engine, encode_tables([tables[0], dup]))
-    assert res.kind == -6 and res.table == 1 and res.index == 4
+def test_merge_empty(engine):
     # every table empty / no tables: the reference panics (manager.rs:213)
     res, _, _, _ = device_merge(engine, [np.zeros(0, np.uint8)] * 3)
     assert res.kind == -5
     res, _, _, _ = device_merge(engine, [])
     assert res.kind == -5
+
+
+def _exact_case(engine, tables):
+    """Any pair lists -> device merge == oracle.compact (the reference loop,
+    src/sstable/manager.rs:199-234) record for record."""
+    datas = encode_tables(tables)
+    res, got, _, offs = device_merge(engine, datas)
+    want, rc = oracle_merge_pairs(datas, offs)
+    assert rc == 0 and res.status == 0 and res.kind == 0
+    assert res.n == want.size
+    assert np.array_equal(got, want)
+
+
+def test_merge_reference_duplicate_key_table(engine, golden):
+    """The table of src/sstable/table.rs:93-108 (key 'abc' twice, a tombstone
+    after its value): legal for SSTable::new, merged by the reference loop."""
+    c = golden["table_create"]
+    dup = [(bytes.fromhex(k), None if v is None else bytes.fromhex(v)) for k, v in c["pairs"]]
+    other = [(b"ab", b"1"), (b"abc", b"2"), (b"abd", None), (b"zz", b"3")]
+    _exact_case(engine, [dup])
+    _exact_case(engine, [dup, other])
+    _exact_case(engine, [other, dup])
+    _exact_case(engine, [dup, dup, other])
+
+
+@pytest.mark.parametrize("k,n_universe,frac,seed,mode", [
+    (3, 500, 0.6, 13, "swap"),      # one adjacent swap (the round-1 UNSORTED case)
+    (2, 500, 0.6, 14, "dup"),       # one duplicated record
+    (3, 4000, 0.5, 15, "shuffle"),  # one table fully shuffled (many merge tiles)
+    (4, 3000, 0.5, 16, "dups"),     # many duplicate keys, still non-decreasing
+    (1, 3000, 1.0, 17, "shuffle"),  # a single unsorted table
+    (9, 2000, 0.3, 18, "reverse"),  # one table in descending order
+])
+def test_merge_not_strictly_increasing(engine, k, n_universe, frac, seed, mode):
+    rng = np.random.default_rng(seed)
+    tables = sorted_tables(k, n_universe, frac, seed, long_prefix=seed % 2 == 1)
+    t = min(1, k - 1)
+    bad = list(tables[t])
+    if mode == "swap":
+        bad[5], bad[6] = bad[6], bad[5]
+    elif mode == "dup":
+        bad.insert(3, bad[3])
+    elif mode == "shuffle":
+        rng.shuffle(bad)
+    elif mode == "dups":
+        bad = sorted(bad + [bad[i] for i in rng.integers(0, len(bad), len(bad) // 3)],
+                     key=lambda kv: kv[0])
+    elif mode == "reverse":
+        bad = bad[::-1]
+    tables[t] = bad
+    _exact_case(engine, tables)
+
+
+def test_merge_unsorted_multi_tile(engine):
+    """Tables of 3000 and 500 records (several 1024-entry merge tiles) with
+    the disorder in the second table: exact loop output."""
+    tables = sorted_tables(2, 6000, 0.6, 19)
+    tables[0] = tables[0][:3000]
+    bad = tables[1][:500]
+    bad[100], bad[400] = bad[400], bad[100]
+    tables[1] = bad
+    _exact_case(engine, tables)
+
+
+@pytest.mark.parametrize("stride", [0, 3])
+def test_compact_host_unsorted(engine, stride):
+    """decode -> exact merge -> encode of tables with duplicate / unordered
+    keys == serialize_flatten of the oracle's compact_inner output."""
+    tables = sorted_tables(4, 2000, 0.5, 20)
+    tables[2] = tables[2][::-1]
+    tables[3] = tables[3] + tables[3][:50]
+    datas = encode_tables(tables)
+    out = engine.compact_host([d.tobytes() for d in datas], block_stride=stride)
+    assert out.status == 0 and out.kind == 0
+    tabs = [(d, oracle.decode(d)[0]) for d in datas]
+    refs, _ = oracle.compact(tabs)
+    merged = [oracle.pairs_from_spans(tabs[t][0], tabs[t][1][r:r + 1])[0] for t, r in refs]
+    arena, rec = oracle.pack_pairs(merged)
+    want, _, blocks, _ = oracle.encode(arena, rec, block_stride=stride)
+    assert out.n == len(merged)
+    assert np.array_equal(out.data, want)
+    if stride:
+        assert np.array_equal(out.blocks, blocks)
 
 
 def test_merge_capacity(engine):

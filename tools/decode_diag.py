@@ -93,50 +93,17 @@ def run(eng, sst, L, label):
 
 
 def main():
+    """Diagnostics for the decode_variants.py workloads whose label contains
+    one of the command-line words (all of them without arguments)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from decode_variants import workloads
+    only = sys.argv[1:]
     eng = Engine(0)
-    n = 8_134_407
-    sst = synth.fixed_sst(n, 16, 100, seed=2, device=eng.device)
-    run(eng, sst, sst.numel(), "cfg2 16B/100B")
-    del sst
-    # mixed sizes: values 8..4096 (cfg4-like), from the oracle-free device builder
-    rng = np.random.default_rng(4)
-    m = 200_000
-    kl = np.full(m, 16, np.int64)
-    vl = rng.integers(8, 4097, m)
-    vl[rng.random(m) < 0.05] = 0
-    sizes = 16 + kl + vl
-    offs = np.concatenate([[0], np.cumsum(sizes)])
-    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
-    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
-    for i in range(16):
-        buf[offs[:-1] + i] = hdr[:, i]
-    t = torch.from_numpy(buf).to(eng.device)
-    run(eng, t, t.numel(), "mixed 16B/8..4096B")
-    # medium records (8..64 B keys / 64..512 B values)
-    m = 1_500_000
-    kl = rng.integers(8, 65, m)
-    vl = rng.integers(64, 513, m)
-    sizes = 16 + kl + vl
-    offs = np.concatenate([[0], np.cumsum(sizes)])
-    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
-    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
-    for i in range(16):
-        buf[offs[:-1] + i] = hdr[:, i]
-    t = torch.from_numpy(buf).to(eng.device)
-    run(eng, t, t.numel(), "medium 8..64B/64..512B")
-    del t
-    # small mixed records
-    m = 2_000_000
-    kl = rng.integers(0, 24, m)
-    vl = rng.integers(0, 64, m)
-    sizes = 16 + kl + vl
-    offs = np.concatenate([[0], np.cumsum(sizes)])
-    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
-    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
-    for i in range(16):
-        buf[offs[:-1] + i] = hdr[:, i]
-    t = torch.from_numpy(buf).to(eng.device)
-    run(eng, t, t.numel(), "small mixed 0..24B/0..64B")
+    for label, sst in workloads(eng.device):
+        if only and not any(w in label for w in only):
+            continue
+        run(eng, sst, sst.numel(), label)
+        del sst
 
 
 if __name__ == "__main__":

@@ -40,11 +40,11 @@ def workloads(dev):
 
 
 def main():
-    only = sys.argv[1] if len(sys.argv) > 1 else None
+    only = sys.argv[1:]  # label words (any match); none: every workload
     eng = Engine(0)
     eng.set_stream(torch.cuda.current_stream(eng.device))
     for label, sst in workloads(eng.device):
-        if only and only not in label:
+        if only and not any(w in label for w in only):
             continue
         L = sst.numel()
         cap = L // 16
