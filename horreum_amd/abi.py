@@ -112,6 +112,21 @@ _PROTOS = {
     "hg_host_is_pinned": (ctypes.c_int, [_vp]),
     "hg_compact_host": (ctypes.c_int, [_vp, _u32, _vp, _vp, _u8p, _u64, ctypes.POINTER(_u64),
                                        _u32, _vp, ctypes.POINTER(HgMergeResult)]),
+    # range decode(ctx, sst, len, begin, stop, entry, spans, cap, [n*, exit*, err* | result])
+    "hg_decode_range_dev_async": (ctypes.c_int, [_vp, _u8p, _u64, _u64, _u64, _u64, _vp, _u64,
+                                                 _vp]),
+    "hg_decode_range_dev": (ctypes.c_int, [_vp, _u8p, _u64, _u64, _u64, _u64, _vp, _u64,
+                                           ctypes.POINTER(_u64), ctypes.POINTER(_u64),
+                                           ctypes.POINTER(HgErr)]),
+    "hg_decode_guess_entry_dev": (ctypes.c_int, [_vp, _u8p, _u64, _u64, ctypes.POINTER(_u64)]),
+    "hg_encoded_size": (ctypes.c_int, [_vp, _vp, _u64, ctypes.POINTER(_u64)]),
+    # multi(ctxs**, nctx, ...)
+    "hg_multi_decode_host": (ctypes.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "hg_multi_decode_file_host": (ctypes.c_int, [_vp, _u32, _u8p, _u64, _vp, _u64,
+                                                 ctypes.POINTER(_u64), ctypes.POINTER(HgErr)]),
+    "hg_multi_compact_host": (ctypes.c_int, [_vp, _u32, _u32, _vp, _vp, _u8p, _u64,
+                                             ctypes.POINTER(_u64), _u32, _vp,
+                                             ctypes.POINTER(HgMergeResult)]),
 }
 
 _lib = None

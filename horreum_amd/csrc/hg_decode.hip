@@ -93,8 +93,13 @@ enum : uint32_t { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2, ST_ERR = 3 };
 enum : uint32_t { PK_EMPTY = 0, PK_STRIDE = 1, PK_SCRATCH = 2 };
 
 struct DecodeArgs {
-    const uint8_t* sst;
-    uint64_t len;
+    const uint8_t* sst;          // first byte of the decoded range
+    uint64_t len;                // bytes of the table from sst (records must fit in them)
+    uint64_t rlen;               // bytes present at sst (>= min(len, stop + 16); == len for a whole table)
+    uint64_t stop;               // records START in [entry, stop) (== len for a whole table)
+    uint64_t entry;              // exact start of the first record (0 for a whole table)
+    uint64_t obase;              // added to every span offset written to `spans`
+    uint32_t range;              // a range decode: the result's err_offset on success = exit
     hg_span* spans;
     uint64_t cap;
     hg_decode_result* result;
@@ -117,6 +122,13 @@ struct DecodeArgs {
     uint32_t sbp;                // pieces per pre-pass batch (SPEC_BP_MIN..SPEC_BP)
     uint32_t q;                  // pre-pass batches per general batch (bp / sbp)
 };
+
+// Bytes of the piece at `base` where records may start: up to `stop` (the
+// piece's bytes up to `len` are still staged and readable).
+__device__ __forceinline__ uint32_t piece_clen(const DecodeArgs& a, uint64_t base) {
+    const uint64_t r = a.stop - base;
+    return r < PIECE ? (uint32_t)r : PIECE;
+}
 
 // ---- stride pre-pass records --------------------------------------------------------
 constexpr uint32_t SPEC_BP = 64;      // most pieces per pre-pass batch (LDS halo array)
@@ -271,6 +283,15 @@ __device__ __forceinline__ void store_span(hg_span* out, uint64_t cap, uint64_t 
     write_span(out, gi, base + p, kl, vl);
 }
 
+// A span from scratch (offset relative to the range) to its final slot.
+__device__ __forceinline__ void copy_span(hg_span* dst, const hg_span* src, uint64_t obase) {
+    uint4 v = *reinterpret_cast<const uint4*>(src);
+    const uint64_t off = (((uint64_t)v.y << 32) | v.x) + obase;
+    v.x = (uint32_t)off;
+    v.y = (uint32_t)(off >> 32);
+    *reinterpret_cast<uint4*>(dst) = v;
+}
+
 // ---- relaxation ---------------------------------------------------------------
 // Exact per-lane state for piece entry X (absolute).  All threads call it.
 // Each lane caches one walk (from guess g).  A lane is a pass-through when
@@ -386,8 +407,8 @@ restart:
         uint32_t f;
         int fi;
         for (;;) {
-            if (j < 0) {  // virtual batch -1: exact exit 0, 0 records
-                w0 = pack_status(ST_INCL, 0, 0);
+            if (j < 0) {  // virtual batch -1: exact exit = the entry, 0 records
+                w0 = pack_status(ST_INCL, 0, a.entry);
                 w1 = pack_status(ST_INCL, NONE_REL, 0);
             } else {
                 w0 = ld_agent(&a.status[2 * j]);
@@ -461,7 +482,8 @@ restart:
 // the whole block then writes the batch to out[gbase + i] (i < cap - gbase).
 // Returns the count; s.err_kind / s.err_pos / s.exitk describe the end.
 __device__ uint64_t serial_walk_emit(DecodeSmem& s, uint64_t len, uint64_t base, uint32_t clen,
-                                     uint64_t x, hg_span* out, uint64_t cap, uint64_t gbase) {
+                                     uint64_t x, hg_span* out, uint64_t cap, uint64_t gbase,
+                                     uint64_t ob) {
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     uint64_t emitted = 0;
     __syncthreads();
@@ -512,7 +534,7 @@ __device__ uint64_t serial_walk_emit(DecodeSmem& s, uint64_t len, uint64_t base,
         __syncthreads();
         const uint32_t n = s.walk_n;
         for (uint32_t t = threadIdx.x; t < n; t += THREADS)
-            store_span(out, cap, gbase + emitted + t, data, base, s.pc[t]);
+            store_span(out, cap, gbase + emitted + t, data, base + ob, s.pc[t]);
         emitted += n;
         const bool done = s.walk_done;
         if (done) break;
@@ -880,14 +902,14 @@ __device__ uint64_t general_entry_guess(DecodeSmem& s, const uint8_t* data, uint
 // 16 bytes at off (absolute), zero past len; register-only byte assembly at
 // the file tail.
 __device__ __forceinline__ uint4 load16(const DecodeArgs& a, uint64_t off) {
-    if (off + 16 <= a.len) return *reinterpret_cast<const uint4*>(a.sst + off);
+    if (off + 16 <= a.rlen) return *reinterpret_cast<const uint4*>(a.sst + off);
     uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
             const uint64_t o = off + q * 4 + b;
-            if (o < a.len) w[q] |= (uint32_t)a.sst[o] << (8 * b);
+            if (o < a.rlen) w[q] |= (uint32_t)a.sst[o] << (8 * b);
         }
     return make_uint4(w[0], w[1], w[2], w[3]);
 }
@@ -899,7 +921,7 @@ __device__ __forceinline__ uint4 load16(const DecodeArgs& a, uint64_t off) {
 #endif
 __device__ __forceinline__ void load_piece(const DecodeArgs& a, uint32_t p, uint4 (&v)[GPT]) {
     const uint64_t base = (uint64_t)p * PIECE;
-    if (base + PIECE <= a.len) {  // uniform: plain 16-byte loads, no per-lane branch
+    if (base + PIECE <= a.rlen) {  // uniform: plain 16-byte loads, no per-lane branch
         const uint4* src = reinterpret_cast<const uint4*>(a.sst + base) + threadIdx.x;
 #pragma unroll
         for (uint32_t i = 0; i < GPT; ++i) {
@@ -982,8 +1004,9 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
                               bool try_stride = true) {
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     const uint64_t base = (uint64_t)p * PIECE;
-    const uint64_t rem = a.len - base;
-    const uint32_t clen = rem < PIECE ? (uint32_t)rem : PIECE;
+    const uint64_t rem = a.len - base;                       // readable (record validity)
+    const uint32_t clen = piece_clen(a, base);               // where records may start
+    const uint64_t ob = emit_now ? a.obase : 0;              // span offsets into `spans`
     uint32_t g = NO_GUESS, cnt = 0;
     Walk w;
     w.exit = 0;
@@ -1048,7 +1071,7 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         ps.exit = exit;
         if (emit_now && ps.kind == PK_STRIDE)
             for (uint32_t t = threadIdx.x; t < ps.count; t += THREADS)
-                if (gbase + t < cap) write_span(out, gbase + t, X + t * ps.R, ps.kl, ps.vl);
+                if (gbase + t < cap) write_span(out, gbase + t, ob + X + t * ps.R, ps.kl, ps.vl);
         return HG_OK;
     }
     HG_PROF(7);
@@ -1060,7 +1083,7 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         mode = 4;
         const uint32_t n = uni(s.walk_n);
         for (uint32_t t = threadIdx.x; t < n; t += THREADS)
-            store_span(out, cap, gbase + t, data, base, s.pc[t]);
+            store_span(out, cap, gbase + t, data, base + ob, s.pc[t]);
         ps.count = n;
         exit = ps.exit = uni(s.exitk);
         return HG_OK;
@@ -1078,7 +1101,7 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         uint32_t tot;
         const uint32_t pre = block_excl_scan<NW>(cnt, s.scan_tmp, tot);
         for (uint32_t i = 0; i < cnt; ++i)
-            store_span(out, cap, gbase + pre + i, data, base, walk_pos(w, i));
+            store_span(out, cap, gbase + pre + i, data, base + ob, walk_pos(w, i));
         ps.count = uni(tot);
         exit = ps.exit = uni(s.exitk);
         __syncthreads();
@@ -1086,7 +1109,7 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
         return HG_OK;
     }
     mode = 3;
-    ps.count = uni((uint32_t)serial_walk_emit(s, a.len, base, clen, X, out, cap, gbase));
+    ps.count = uni((uint32_t)serial_walk_emit(s, a.len, base, clen, X, out, cap, gbase, ob));
     exit = ps.exit = uni(s.exitk);
     return uni(s.err_kind);
 }
@@ -1148,13 +1171,12 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
         const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
         const uint32_t kl = uni(pc[i].kl), vl = uni(pc[i].vl), cnt = uni(pc[i].count);
         if (uni(pc[i].pad) == SP_HOP) {  // hop segment: spans were walked into scratch
-            const uint4* src =
-                reinterpret_cast<const uint4*>(a.scratch + (size_t)(q0 + i) * MAX_REC_PIECE);
+            const hg_span* src = a.scratch + (size_t)(q0 + i) * MAX_REC_PIECE;
             for (uint32_t t = tid; t < cnt; t += THREADS)
-                if (g + t < a.cap) *reinterpret_cast<uint4*>(a.spans + g + t) = src[t];
+                if (g + t < a.cap) copy_span(a.spans + g + t, src + t, a.obase);
         } else {
             for (uint32_t t = tid; t < cnt; t += THREADS)
-                if (g + t < a.cap) write_span(a.spans, g + t, x + t * R, kl, vl);
+                if (g + t < a.cap) write_span(a.spans, g + t, a.obase + x + t * R, kl, vl);
         }
     }
     const uint64_t end = uni(pbase[SPEC_BP]);
@@ -1193,7 +1215,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             r.n_records = g;
             r.kind = HG_OK;
             r.reserved = 0;
-            r.err_offset = 0;
+            r.err_offset = a.range ? a.obase + a.sbatch[e].exit : 0;
             *a.result = r;
         }
     }
@@ -1278,7 +1300,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
                         r.n_records = gk0 + ptot;
                         r.kind = HG_OK;
                         r.reserved = 0;
-                        r.err_offset = 0;
+                        r.err_offset = a.range ? a.obase + pex : 0;
                         *a.result = r;
                     }
                 }
@@ -1292,7 +1314,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
     if (tid < np) s.halo[tid] = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
     if (tid == 0) {  // is the predecessor batch's exit already published?
         s.pred_ok = b == 0;
-        s.pred_exit = 0;
+        s.pred_exit = a.entry;
         if (b > 0) {
             unsigned long long v0 = ld_agent(&a.status[2 * (b - 1)]);
             unsigned long long v1 = ld_agent(&a.status[2 * (b - 1) + 1]);
@@ -1477,13 +1499,12 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             ps.kind = uni(ps.kind);
             if (ps.kind == PK_STRIDE) {
                 for (uint32_t t = tid; t < ps.count; t += THREADS)
-                    if (go + t < a.cap) write_span(a.spans, go + t, ps.x + t * ps.R, ps.kl, ps.vl);
+                    if (go + t < a.cap)
+                        write_span(a.spans, go + t, a.obase + ps.x + t * ps.R, ps.kl, ps.vl);
             } else if (ps.kind == PK_SCRATCH) {
                 const hg_span* src = scratch + (size_t)i * MAX_REC_PIECE;
                 for (uint32_t t = tid; t < ps.count; t += THREADS)
-                    if (go + t < a.cap)
-                        *reinterpret_cast<uint4*>(a.spans + go + t) =
-                            *reinterpret_cast<const uint4*>(src + t);
+                    if (go + t < a.cap) copy_span(a.spans + go + t, src + t, a.obase);
             }
             go += ps.count;
         }
@@ -1510,9 +1531,28 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         r.n_records = gk + total;
         r.kind = kind;
         r.reserved = 0;
-        r.err_offset = kind != HG_OK ? errpos : 0;
+        r.err_offset = kind != HG_OK ? a.obase + errpos : (a.range ? a.obase + x : 0);
         *a.result = r;
     }
+}
+
+// Speculative entry of a range that starts inside a table (a single huge
+// table split over devices): the first record start at or after
+// `stop`, found by walking the piece [begin, stop) (one piece, begin = stop -
+// 16 KiB, or 0) from a guessed entry -- the general engine's lead-in.  The
+// caller verifies the guess against the exact exit of the previous range and
+// redoes the range from that exit when they differ.  ~0 if nothing was found.
+__global__ __launch_bounds__(THREADS, 4) void decode_guess_kernel(DecodeArgs a, uint64_t* out) {
+    __shared__ DecodeSmem s;
+    uint4 v[GPT];
+    load_piece(a, 0, v);
+    if (threadIdx.x == 0) s.lead_halo = load16(a, PIECE);
+    stage_piece(s, v, 0, true);
+    PieceSum ps;
+    uint64_t ex = 0, X = a.obase == 0 ? 0 : X_UNKNOWN;  // a table's first byte is a record start
+    uint32_t mode = 0;
+    const int32_t e = piece_path<false>(s, a, 0, X, false, true, a.scratch, ~0ull, 0, ps, ex, mode);
+    if (threadIdx.x == 0) *out = e == HG_OK ? a.obase + ex : ~0ull;
 }
 
 template <bool DIAG>
@@ -1588,7 +1628,7 @@ __device__ uint64_t hop_check(const DecodeArgs& a, uint64_t p, uint64_t kl, uint
     uint64_t q = p + 16 + kl + vl;
     for (uint32_t h = 0; h < HOP_CHECK; ++h) {
         if (q == a.len) return q - p;
-        if (q + 16 > a.len) return 0;
+        if (q + 16 > a.len || q + 16 > a.rlen) return 0;
         hbm_header(a, q, kl, vl);
         if (!rec_ok(q, a.len, kl, vl)) return 0;
         q += 16 + kl + vl;
@@ -1611,7 +1651,7 @@ __device__ void hop_walk(const DecodeArgs& a, uint64_t x, uint64_t end, hg_span*
             break;
         }
         uint64_t kl, vl;
-        if (cur + 16 > a.len) {
+        if (cur + 16 > a.len || cur + 16 > a.rlen) {
             dead = 1;
             break;
         }
@@ -1675,7 +1715,7 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
                           SpecPiece* sp, uint64_t& X0, uint64_t& X, uint64_t& total) {
     const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
     const uint32_t nseg = (np + HOP_SEG_PIECES - 1) / HOP_SEG_PIECES;
-    const uint64_t bend = min((uint64_t)(p0 + np) * PIECE, a.len);
+    const uint64_t bend = min((uint64_t)(p0 + np) * PIECE, a.stop);
     // Large records?  Piece 0 is still staged: count its header candidates
     // (a record start and its shifts pass the zero-byte filter, ~4 per record
     // for short keys/values).  At most HOP_MAX_CAND (~512 B per record) -> hop.
@@ -1685,7 +1725,7 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
         const bool any_valid = rem >= 16;
         const uint64_t plim64 = any_valid ? rem - 16 : 0;
         const uint32_t plim = plim64 < 0xFFFFFFFFull ? (uint32_t)plim64 : 0xFFFFFFFFu;
-        const uint32_t clen = rem < PIECE ? (uint32_t)rem : PIECE;
+        const uint32_t clen = piece_clen(a, base);
         const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
         uint32_t nc = 0;
 #pragma unroll
@@ -1723,6 +1763,10 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
                 s.hd[k] = d;
             }
         }
+    }
+    if (p0 == 0 && tid == 0) {  // the first batch's entry is known exactly
+        s.hg[0] = a.entry;
+        s.hd[0] = 0;
     }
     __syncthreads();
     if (s.hg[0] == NO_HOP) {  // no entry for the batch: the general engine takes it
@@ -1845,7 +1889,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         const uint32_t p = p0 + i;
         const uint64_t base = (uint64_t)p * PIECE;
         const uint64_t rem = a.len - base;
-        const uint32_t clen = rem < PIECE ? (uint32_t)rem : PIECE;
+        const uint32_t clen = piece_clen(a, base);
         __syncthreads();  // (A)
         if (i == 0 && tid < np) s.halo[tid] = h;
 #pragma unroll
@@ -1857,7 +1901,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
                 tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
         if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
         __syncthreads();  // (B)
-        if (i == 0) {
+        if (i == 0 && b == 0) {
+            X = X0 = a.entry;  // the first batch's entry is known exactly
+        } else if (i == 0) {
             if (tid < 64) {
                 const uint32_t f = stride_guess(data, rem, clen, a.hz);
                 if (tid == 0) s.guess = f;
@@ -1909,7 +1955,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         o.pad = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
         sb[b] = o;
         atomicAdd(&a.gsum[b / SPEC_GROUP], (unsigned long long)total);
-        if (!ok || (b == 0 && X0 != 0)) mark_bad(a.ctl, a.nspec, b);
+        if (!ok || (b == 0 && X0 != a.entry)) mark_bad(a.ctl, a.nspec, b);
         if (b > 0) link_arrive(a, b, 0 - X0);
         if (b + 1 < a.nspec) link_arrive(a, b + 1, X);
     }
@@ -2077,11 +2123,22 @@ uint32_t device_cus() {
 namespace {
 // DecodeArgs of one table with the given batch geometry (bp pieces per
 // general batch, sbp per pre-pass batch); zero_bytes = control region to zero.
+// Range form (hgk_decode_range_launch): bytes [begin, len) readable, records
+// starting in [entry, stop) decoded, entry an exact record start; the
+// workspace is laid out for stop - begin bytes.
 hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t cap,
                           hg_decode_result* d_result, void* d_ws, uint32_t* d_diag, uint32_t bp,
-                          uint32_t sbp, uint64_t& zero_bytes) {
+                          uint32_t sbp, uint64_t& zero_bytes, uint64_t begin = 0,
+                          uint64_t stop = ~0ull, uint64_t entry = 0, bool range = false,
+                          uint64_t rlen = ~0ull) {
     using namespace hgk;
-    const DecodeLayout l = decode_layout(len);
+    if (stop > len) stop = len;
+    if (rlen > len) rlen = len;
+    d_sst += begin;
+    len -= begin;
+    stop -= begin;
+    rlen -= begin;
+    const DecodeLayout l = decode_layout(stop);
     // Zero high bytes every genuine length field must have: any record fits
     // in len bytes, so klen, vlen < 2^(8*nb) with nb = bytes needed for len.
     uint32_t nb = 0;
@@ -2089,6 +2146,11 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     DecodeArgs a;
     a.sst = d_sst;
     a.len = len;
+    a.rlen = rlen;
+    a.stop = stop;
+    a.entry = entry - begin;
+    a.obase = begin;
+    a.range = range ? 1u : 0u;
     a.spans = d_spans;
     a.cap = cap;
     a.result = d_result;
@@ -2121,18 +2183,34 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
 // d_ws must hold hgk_decode_workspace_bytes(len) bytes.  The launcher zeroes
 // the statuses and the ticket (the scratch area needs no initialisation).
 // len == 0 is handled by the caller (no launch).
-extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
-                                      uint64_t cap, hg_decode_result* d_result, void* d_ws,
-                                      uint32_t* d_diag, hipStream_t stream) {
+namespace {
+__global__ void decode_const_result(hg_decode_result* r, uint64_t off) {
+    hg_decode_result v;
+    v.n_records = 0;
+    v.kind = HG_OK;
+    v.reserved = 0;
+    v.err_offset = off;
+    *r = v;
+}
+
+int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t cap,
+                  hg_decode_result* d_result, void* d_ws, uint32_t* d_diag, hipStream_t stream,
+                  uint64_t begin, uint64_t stop, uint64_t entry, bool range, uint64_t rlen) {
     using namespace hgk;
-    const uint64_t npieces = (len + PIECE - 1) / PIECE;
+    if (stop > len) stop = len;
+    if (entry >= stop) {  // no record starts in the range: 0 records, exit = entry
+        hipLaunchKernelGGL(decode_const_result, dim3(1), dim3(1), 0, stream, d_result,
+                           range ? entry : 0ull);
+        return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    }
+    const uint64_t npieces = (stop - begin + PIECE - 1) / PIECE;
     const uint32_t res_gen = d_diag ? resident_workgroups(decode_kernel<true>, 1)
                                     : resident_workgroups(decode_kernel<false>, 2);
     const uint32_t bp = general_pieces(npieces, res_gen);
     const uint32_t sbp = spec_pieces(bp, npieces, device_cus());
     uint64_t zero_bytes = 0;
     const DecodeArgs a = make_args(d_sst, len, d_spans, cap, d_result, d_ws, d_diag, bp, sbp,
-                                   zero_bytes);
+                                   zero_bytes, begin, stop, entry, range, rlen);
     if (hipMemsetAsync(d_ws, 0, zero_bytes, stream) != hipSuccess) return HG_ERR_HIP;
     // 1. pre-pass (stride runs, hop walks): verifies, links neighbours, sums records per group
     // 2. decode_kernel: spans of the resolved prefix, then the general engine
@@ -2148,6 +2226,46 @@ extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_spa
         hipLaunchKernelGGL(decode_kernel<true>, dim3(grid), dim3(THREADS), 0, stream, a);
     else
         hipLaunchKernelGGL(decode_kernel<false>, dim3(grid), dim3(THREADS), 0, stream, a);
+    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+}  // namespace
+
+extern "C" int hgk_decode_launch_diag(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
+                                      uint64_t cap, hg_decode_result* d_result, void* d_ws,
+                                      uint32_t* d_diag, hipStream_t stream) {
+    return launch_decode(d_sst, len, d_spans, cap, d_result, d_ws, d_diag, stream, 0, len, 0,
+                         false, len);
+}
+
+// Range decode of a table of `len` bytes whose bytes [begin, rlen) are
+// present at d_sst + begin (rlen >= min(len, stop + 16)): the records starting
+// in [entry, stop) (entry an exact record start, begin <= entry) are decoded
+// with absolute offsets; the result's err_offset on success is the exit (the
+// first record start at or after stop).  d_ws holds
+// hgk_decode_workspace_bytes(stop - begin) bytes.
+extern "C" int hgk_decode_range_launch(const uint8_t* d_sst, uint64_t len, uint64_t rlen,
+                                       uint64_t begin, uint64_t stop, uint64_t entry,
+                                       hg_span* d_spans, uint64_t cap,
+                                       hg_decode_result* d_result, void* d_ws,
+                                       hipStream_t stream) {
+    return launch_decode(d_sst, len, d_spans, cap, d_result, d_ws, nullptr, stream, begin, stop,
+                         entry, true, rlen);
+}
+
+// Guess of the first record start at or after `stop` (see decode_guess_kernel)
+// into *d_out (device).  Bytes [stop - 16 KiB (or 0), min(len, stop + 16)) must
+// be present at d_sst (absolute addressing, as hgk_decode_range_launch).
+// d_ws: hgk_decode_workspace_bytes(16384) bytes.
+extern "C" int hgk_decode_guess_launch(const uint8_t* d_sst, uint64_t len, uint64_t rlen,
+                                       uint64_t stop, uint64_t* d_out, void* d_ws,
+                                       hipStream_t stream) {
+    using namespace hgk;
+    if (stop > len) stop = len;
+    const uint64_t begin = stop > PIECE ? stop - PIECE : 0;
+    uint64_t zb = 0;
+    const DecodeArgs a = make_args(d_sst, len, nullptr, 0, nullptr, d_ws, nullptr, BATCH_MIN,
+                                   SPEC_BP_MIN, zb, begin, stop, begin, true, rlen);
+    hipLaunchKernelGGL(decode_guess_kernel, dim3(1), dim3(THREADS), 0, stream, a, d_out);
     return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 

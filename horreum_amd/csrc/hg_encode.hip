@@ -585,3 +585,45 @@ extern "C" int hgk_encode_blocks_launch(const uint64_t* d_rec_off, uint64_t n,
                        (const hg_encode_result*)nullptr, total, d_blocks, nb);
     return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
+
+// Encoded size only (hg_encoded_size on device pairs): the tile sums and
+// their scan, no copy -- d_result->out_len = sum(16 + klen + vlen).
+extern "C" int hgk_encode_size_launch(const hg_pair* d_pairs, uint64_t n,
+                                      hg_encode_result* d_result, unsigned long long* d_status,
+                                      hipStream_t stream) {
+    using namespace hgk;
+    const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
+    const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
+    uint64_t* tsum = reinterpret_cast<uint64_t*>(d_status);
+    uint64_t* gsum = tsum + nt;
+    if (nt == 0)
+        return hipMemsetAsync(d_result, 0, sizeof(hg_encode_result), stream) == hipSuccess
+                   ? HG_OK
+                   : HG_ERR_HIP;
+    if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_ERR_HIP;
+    hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
+                       d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum));
+    hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng,
+                       ~0ull, d_result);
+    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}
+
+namespace hgk {
+// out[j] = v[first + j * stride] for first + j * stride < n: the record
+// offsets a key-range slice of a compaction contributes to the block index.
+__global__ void gather_stride_kernel(const uint64_t* v, uint64_t n, uint64_t first,
+                                     uint64_t stride, uint64_t* out) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t i = first + j * stride;
+    if (i < n) out[j] = v[i];
+}
+}  // namespace hgk
+
+extern "C" int hgk_gather_stride_launch(const uint64_t* d_v, uint64_t n, uint64_t first,
+                                        uint64_t stride, uint64_t* d_out, hipStream_t stream) {
+    if (first >= n || stride == 0) return HG_OK;
+    const uint64_t m = (n - first + stride - 1) / stride;
+    hipLaunchKernelGGL(hgk::gather_stride_kernel, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0,
+                       stream, d_v, n, first, stride, d_out);
+    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+}

@@ -1,0 +1,105 @@
+// hg_internal.hpp — host-runtime internals shared by hg_runtime.hip and
+// hg_multi.hip (not part of the C ABI): the context, its device / pinned
+// buffers and the staging helpers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/horreum_gpu.h"
+
+extern "C" int hgk_decode_launch(const uint8_t*, uint64_t, hg_span*, uint64_t, hg_decode_result*,
+                                 void*, hipStream_t);
+extern "C" int hgk_decode_range_launch(const uint8_t*, uint64_t, uint64_t, uint64_t, uint64_t,
+                                       uint64_t, hg_span*, uint64_t, hg_decode_result*, void*,
+                                       hipStream_t);
+extern "C" int hgk_decode_guess_launch(const uint8_t*, uint64_t, uint64_t, uint64_t, uint64_t*,
+                                       void*, hipStream_t);
+extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t);
+extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t);
+extern "C" int hgk_decode_launch_multi(uint32_t, const uint8_t* const*, const uint64_t*,
+                                       hg_span* const*, const uint64_t*, hg_decode_result*, void*,
+                                       const uint64_t*, void*, void*, hipStream_t);
+extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
+                                 uint64_t*, uint32_t, hg_block*, hg_encode_result*,
+                                 unsigned long long*, hipStream_t);
+extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t);
+extern "C" int hgk_encode_launch_at(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
+                                    uint64_t*, uint64_t, uint32_t, hg_block*, hg_encode_result*,
+                                    unsigned long long*, hipStream_t);
+extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
+                                        hipStream_t);
+extern "C" int hgk_encode_size_launch(const hg_pair*, uint64_t, hg_encode_result*, unsigned long long*,
+                                      hipStream_t);
+extern "C" int hgk_gather_stride_launch(const uint64_t*, uint64_t, uint64_t, uint64_t, uint64_t*,
+                                        hipStream_t);
+extern "C" uint64_t hgk_keyindex_bytes(uint64_t);
+extern "C" int hgk_keyindex_launch(const uint8_t*, uint64_t, const hg_span*, uint64_t, void*,
+                                   hipStream_t);
+extern "C" int hgk_lookup_launch(const uint8_t*, const hg_span*, const void*, uint64_t,
+                                 const uint8_t*, const hg_key*, uint64_t, hg_lookup_result*,
+                                 hipStream_t);
+extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
+extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
+extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
+                                const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
+                                hg_merge_result*, void*, void*, hipStream_t);
+
+namespace hgi {
+
+constexpr uint64_t kMaxLen = 1ull << 40;  // 40-bit positions in decode statuses
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace hgi
+
+struct hg_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    hgi::DevBuf ws;        // decode statuses / encode tile statuses
+    hgi::DevBuf recoff;    // encode record offsets when blocks are wanted w/o rec_off
+    hgi::DevBuf results;   // hg_decode_result + hg_encode_result
+    hgi::PinBuf hres;      // pinned mirror of `results`
+    // host-path staging (device side)
+    hgi::DevBuf d_in, d_out, d_aux;
+    hgi::PinBuf h_stage[2];
+    // merge: workspace, result, pinned argument staging and its reuse event
+    hgi::DevBuf mws, mres, mspans, mpairs;
+    hgi::DevBuf lk_index, lk_keys, lk_res;  // host lookup path
+    hgi::PinBuf mstage;
+    hipEvent_t mstage_ev = nullptr;
+    bool mstage_busy = false;
+    // batched decode: auxiliary streams (fork/join on `stream`), one workspace each
+    static constexpr int kAux = 8;
+    int naux = 0;
+    hipStream_t aux[kAux] = {};
+    hgi::DevBuf aux_ws[kAux];
+    hipEvent_t fork_ev = nullptr, join_ev[kAux] = {};
+    // batched decode in one launch: all tables' workspaces, argument staging
+    hgi::DevBuf bws, bstage_d;
+    hgi::PinBuf bstage;
+    hipEvent_t bstage_ev = nullptr;
+    bool bstage_busy = false;
+    // multi-context driver (hg_multi.hip): decode results, gathered offsets
+    hgi::DevBuf x_res, x_aux;
+};
+
+namespace hgi {
+int set_dev(hg_ctx* c);
+int ensure(hg_ctx* c, DevBuf& b, size_t bytes);
+int ensure_pin(PinBuf& b, size_t bytes);
+int ensure_aux(hg_ctx* c, int want);
+bool host_pinned(const void* p);
+int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes);
+int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes);
+void par_memcpy(void* dst, const void* src, size_t n);
+}  // namespace hgi

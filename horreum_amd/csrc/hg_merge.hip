@@ -588,7 +588,7 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt
         hg_merge_result r;
         r.n_out = n;
         r.kind = HG_OK;
-        r.table = 0;
+        r.table = 1;  // on success: 1 = the serial reference loop produced the output
         r.index = 0;
         *result = r;
     }

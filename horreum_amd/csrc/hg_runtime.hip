@@ -13,83 +13,12 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/horreum_gpu.h"
 
-extern "C" int hgk_decode_launch(const uint8_t*, uint64_t, hg_span*, uint64_t, hg_decode_result*,
-                                 void*, hipStream_t);
-extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t);
-extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t);
-extern "C" int hgk_decode_launch_multi(uint32_t, const uint8_t* const*, const uint64_t*,
-                                       hg_span* const*, const uint64_t*, hg_decode_result*, void*,
-                                       const uint64_t*, void*, void*, hipStream_t);
-extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
-                                 uint64_t*, uint32_t, hg_block*, hg_encode_result*,
-                                 unsigned long long*, hipStream_t);
-extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t);
-extern "C" int hgk_encode_launch_at(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
-                                    uint64_t*, uint64_t, uint32_t, hg_block*, hg_encode_result*,
-                                    unsigned long long*, hipStream_t);
-extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
-                                        hipStream_t);
-extern "C" uint64_t hgk_keyindex_bytes(uint64_t);
-extern "C" int hgk_keyindex_launch(const uint8_t*, uint64_t, const hg_span*, uint64_t, void*,
-                                   hipStream_t);
-extern "C" int hgk_lookup_launch(const uint8_t*, const hg_span*, const void*, uint64_t,
-                                 const uint8_t*, const hg_key*, uint64_t, hg_lookup_result*,
-                                 hipStream_t);
-extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
-extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
-extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
-                                const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
-                                hg_merge_result*, void*, void*, hipStream_t);
+#include "hg_internal.hpp"
 
-namespace {
+using namespace hgi;
 
-constexpr uint64_t kMaxLen = 1ull << 40;  // 40-bit positions in decode statuses
-
-struct DevBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-};
-
-struct PinBuf {
-    void* p = nullptr;
-    size_t bytes = 0;
-};
-
-}  // namespace
-
-struct hg_ctx {
-    int device = 0;
-    hipStream_t own = nullptr;
-    hipStream_t stream = nullptr;
-    DevBuf ws;        // decode statuses / encode tile statuses
-    DevBuf recoff;    // encode record offsets when blocks are wanted w/o rec_off
-    DevBuf results;   // hg_decode_result + hg_encode_result
-    PinBuf hres;      // pinned mirror of `results`
-    // host-path staging (device side)
-    DevBuf d_in, d_out, d_aux;
-    PinBuf h_stage[2];
-    // merge: workspace, result, pinned argument staging and its reuse event
-    DevBuf mws, mres, mspans, mpairs;
-    DevBuf lk_index, lk_keys, lk_res;  // host lookup path
-    PinBuf mstage;
-    hipEvent_t mstage_ev = nullptr;
-    bool mstage_busy = false;
-    // batched decode: auxiliary streams (fork/join on `stream`), one workspace each
-    static constexpr int kAux = 8;
-    int naux = 0;
-    hipStream_t aux[kAux] = {};
-    DevBuf aux_ws[kAux];
-    hipEvent_t fork_ev = nullptr, join_ev[kAux] = {};
-    // batched decode in one launch: all tables' workspaces, argument staging
-    DevBuf bws, bstage_d;
-    PinBuf bstage;
-    hipEvent_t bstage_ev = nullptr;
-    bool bstage_busy = false;
-};
-
-namespace {
+namespace hgi {
 
 int set_dev(hg_ctx* c) { return hipSetDevice(c->device) == hipSuccess ? HG_OK : HG_ERR_HIP; }
 
@@ -116,6 +45,10 @@ int ensure_pin(PinBuf& b, size_t bytes) {
     b.bytes = bytes;
     return HG_OK;
 }
+
+}  // namespace hgi
+
+namespace {
 
 hg_decode_result* dres(hg_ctx* c) { return reinterpret_cast<hg_decode_result*>(c->results.p); }
 hg_encode_result* eres(hg_ctx* c) {
@@ -181,7 +114,7 @@ int hg_ctx_destroy(hg_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->mws,
                       &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
-                      &c->bws, &c->bstage_d})
+                      &c->bws, &c->bstage_d, &c->x_res, &c->x_aux})
         if (b->p) hipFree(b->p);
     for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage, &c->bstage})
         if (b->p) hipHostFree(b->p);
@@ -277,7 +210,7 @@ int hg_decode_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* d_span
 // auxiliary streams forked from and joined back into the context stream
 // (HG_DECODE_STREAMS, 1..8, default 4).  Asynchronous; results land in
 // d_results[i].
-static int ensure_aux(hg_ctx* c, int want) {
+static int rt_ensure_aux(hg_ctx* c, int want) {
     if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
         return HG_ERR_HIP;
     while (c->naux < want) {
@@ -333,7 +266,7 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
     if (const char* e = getenv("HG_DECODE_STREAMS")) fan = atoi(e);
     fan = std::max(1, std::min<int>(fan, hg_ctx::kAux));
     fan = std::min<int>(fan, std::max<uint32_t>(ntables, 1));
-    int r = ensure_aux(c, fan);
+    int r = rt_ensure_aux(c, fan);
     if (r != HG_OK) return r;
     // size every auxiliary workspace first (growing synchronises that stream)
     for (int s = 0; s < fan; ++s) {
@@ -383,7 +316,7 @@ static constexpr unsigned kCopyThreads = 8;     // default (HG_HOST_COPY_THREADS
 static constexpr unsigned kMaxCopyThreads = 32;
 
 // True if `p` lies in page-locked host memory the DMA engines can address.
-static bool host_pinned(const void* p) {
+static bool rt_host_pinned(const void* p) {
     hipPointerAttribute_t a;
     const hipError_t e = hipPointerGetAttributes(&a, p);
     if (e != hipSuccess) {
@@ -401,7 +334,7 @@ static unsigned copy_threads() {
 }
 
 // memcpy split over host threads in 2 MiB-aligned slices (pageable <-> pinned).
-static void par_memcpy(void* dst, const void* src, size_t n) {
+static void rt_par_memcpy(void* dst, const void* src, size_t n) {
     const unsigned nt = copy_threads();
     const size_t grain = 2ull << 20;
     if (nt <= 1 || n < 2 * grain) {
@@ -433,8 +366,8 @@ static int copy_direct(hg_ctx* c, void* dst, const void* src, size_t bytes, hipM
     return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_ERR_HIP;
 }
 
-static int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
-    if (host_pinned(src)) return copy_direct(c, dst, src, bytes, hipMemcpyHostToDevice);
+static int rt_h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (rt_host_pinned(src)) return copy_direct(c, dst, src, bytes, hipMemcpyHostToDevice);
     if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
         return HG_ERR_HIP;
     hipEvent_t ev[2];
@@ -446,7 +379,7 @@ static int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
         const size_t n = std::min(kStage, bytes - off);
         const int b = (int)(i & 1);
         if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
-        par_memcpy(c->h_stage[b].p, static_cast<const char*>(src) + off, n);
+        rt_par_memcpy(c->h_stage[b].p, static_cast<const char*>(src) + off, n);
         if (hipMemcpyAsync(static_cast<char*>(dst) + off, c->h_stage[b].p, n,
                            hipMemcpyHostToDevice, c->stream) != hipSuccess ||
             hipEventRecord(ev[b], c->stream) != hipSuccess) {
@@ -461,8 +394,8 @@ static int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
     return rc;
 }
 
-static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
-    if (host_pinned(dst)) return copy_direct(c, dst, src, bytes, hipMemcpyDeviceToHost);
+static int rt_d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    if (rt_host_pinned(dst)) return copy_direct(c, dst, src, bytes, hipMemcpyDeviceToHost);
     if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
         return HG_ERR_HIP;
     hipEvent_t ev[2];
@@ -477,7 +410,7 @@ static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
         const int b = (int)(i & 1);
         if (used[b]) {  // drain the previous use of this buffer
             if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
-            par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
+            rt_par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
         }
         if (hipMemcpyAsync(c->h_stage[b].p, static_cast<const char*>(src) + off, n,
                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -493,7 +426,7 @@ static int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
         const int b = (int)((i + k) & 1);
         if (!used[b]) continue;
         if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
-        par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
+        rt_par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
         used[b] = false;
     }
     hipStreamSynchronize(c->stream);
@@ -522,7 +455,7 @@ int hg_host_unregister(const void* h_ptr) {
     return HG_OK;
 }
 
-int hg_host_is_pinned(const void* h_ptr) { return h_ptr && host_pinned(h_ptr) ? 1 : 0; }
+int hg_host_is_pinned(const void* h_ptr) { return h_ptr && rt_host_pinned(h_ptr) ? 1 : 0; }
 
 int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spans, uint64_t cap,
                    uint64_t* n_out, hg_err* err) {
@@ -534,19 +467,103 @@ int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spa
     int r;
     if ((r = ensure(c, c->d_in, len ? len : 1)) != HG_OK) return r;
     if ((r = ensure(c, c->d_out, (dcap ? dcap : 1) * sizeof(hg_span))) != HG_OK) return r;
-    if (len && (r = h2d_pipelined(c, c->d_in.p, h_sst, len)) != HG_OK) return r;
+    if (len && (r = rt_h2d_pipelined(c, c->d_in.p, h_sst, len)) != HG_OK) return r;
     uint64_t n = 0;
     hg_err e{};
     r = hg_decode_dev(c, static_cast<const uint8_t*>(c->d_in.p), len,
                       static_cast<hg_span*>(c->d_out.p), dcap, &n, &e);
     if (r != HG_OK && r != HG_ERR_CAPACITY && e.kind == HG_OK) return r;  // runtime failure
     const uint64_t ncopy = std::min(n, dcap);
-    if (ncopy && d2h_pipelined(c, h_spans, c->d_out.p, ncopy * sizeof(hg_span)) != HG_OK)
+    if (ncopy && rt_d2h_pipelined(c, h_spans, c->d_out.p, ncopy * sizeof(hg_span)) != HG_OK)
         return HG_ERR_HIP;
     if (n_out) *n_out = n;
     if (err) *err = e;
     if (e.kind != HG_OK) return e.kind;
     return n > cap ? HG_ERR_CAPACITY : HG_OK;
+}
+
+// ---- range decode (a table split over devices, or decoded in chunks) ----------
+int hg_decode_range_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uint64_t begin,
+                              uint64_t stop, uint64_t entry, hg_span* d_spans, uint64_t cap,
+                              hg_decode_result* d_result) {
+    if (!c || !d_result || (len && !d_sst) || (cap && !d_spans)) return HG_ERR_INVALID_ARG;
+    if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
+    if (stop > len) stop = len;
+    if (begin > entry || begin > len || entry > len) return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    const uint64_t span = stop > begin ? stop - begin : 0;
+    int r = ensure(c, c->ws, hgk_decode_workspace_bytes(span ? span : 1));
+    if (r != HG_OK) return r;
+    return hgk_decode_range_launch(d_sst, len, std::min(len, stop + 16), begin, stop, entry,
+                                   d_spans, cap, d_result, c->ws.p, c->stream);
+}
+
+int hg_decode_range_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uint64_t begin,
+                        uint64_t stop, uint64_t entry, hg_span* d_spans, uint64_t cap,
+                        uint64_t* n_out, uint64_t* exit, hg_err* err) {
+    int r = hg_decode_range_dev_async(c, d_sst, len, begin, stop, entry, d_spans, cap,
+                                      c ? dres(c) : nullptr);
+    if (r != HG_OK) return r;
+    if (hipMemcpyAsync(c->hres.p, dres(c), sizeof(hg_decode_result), hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return HG_ERR_HIP;
+    const hg_decode_result res = *reinterpret_cast<hg_decode_result*>(c->hres.p);
+    if (exit) *exit = res.kind == HG_OK ? res.err_offset : 0;
+    hg_decode_result rr = res;
+    if (res.kind == HG_OK) rr.err_offset = 0;
+    return finish_decode(rr, cap, n_out, err);
+}
+
+int hg_decode_guess_entry_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uint64_t stop,
+                              uint64_t* entry) {
+    if (!c || !entry || (len && !d_sst)) return HG_ERR_INVALID_ARG;
+    if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (stop >= len) {  // the exit of a range reaching the table's end is its length
+        *entry = len;
+        return HG_OK;
+    }
+    int r = ensure(c, c->ws, hgk_decode_workspace_bytes(16384));
+    if (r == HG_OK) r = ensure(c, c->x_res, 64);
+    if (r != HG_OK) return r;
+    uint64_t* d_out = static_cast<uint64_t*>(c->x_res.p);
+    r = hgk_decode_guess_launch(d_sst, len, std::min(len, stop + 16), stop, d_out, c->ws.p,
+                                c->stream);
+    if (r != HG_OK) return r;
+    if (hipMemcpyAsync(c->hres.p, d_out, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return HG_ERR_HIP;
+    *entry = *static_cast<uint64_t*>(c->hres.p);
+    return HG_OK;
+}
+
+// ---- encoded size --------------------------------------------------------------
+int hg_encoded_size(hg_ctx* c, const hg_pair* pairs, uint64_t n, uint64_t* bytes) {
+    if (!c || !bytes || (n && !pairs)) return HG_ERR_INVALID_ARG;
+    *bytes = 0;
+    if (n == 0) return HG_OK;
+    hipPointerAttribute_t at;
+    const hipError_t e = hipPointerGetAttributes(&at, pairs);
+    if (e != hipSuccess) (void)hipGetLastError();
+    if (e != hipSuccess || at.type != hipMemoryTypeDevice) {  // host pairs: sum here
+        uint64_t t = 0;
+        for (uint64_t i = 0; i < n; ++i) t += 16ull + pairs[i].klen + pairs[i].vlen;
+        *bytes = t;
+        return HG_OK;
+    }
+    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    int r = ensure(c, c->ws, hgk_encode_workspace_bytes(n));
+    if (r != HG_OK) return r;
+    r = hgk_encode_size_launch(pairs, n, eres(c), reinterpret_cast<unsigned long long*>(c->ws.p),
+                               c->stream);
+    if (r != HG_OK) return r;
+    if (hipMemcpyAsync(c->hres.p, eres(c), sizeof(hg_encode_result), hipMemcpyDeviceToHost,
+                       c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return HG_ERR_HIP;
+    *bytes = reinterpret_cast<hg_encode_result*>(c->hres.p)->out_len;
+    return HG_OK;
 }
 
 // ---- encode ------------------------------------------------------------------
@@ -609,7 +626,7 @@ static int encode_host_overlapped(hg_ctx* c, const uint8_t* h_arena, uint64_t ar
     auto now = [] { return std::chrono::duration<double, std::milli>(
                         std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_start = now();
-    int r = ensure_aux(c, 1);
+    int r = rt_ensure_aux(c, 1);
     if (r != HG_OK) return r;
     hipStream_t up = c->stream, down = c->aux[0];
     const size_t pairs_at = (arena_len + 63) & ~(size_t)63;
@@ -675,8 +692,8 @@ static int encode_host_overlapped(hg_ctx* c, const uint8_t* h_arena, uint64_t ar
         fprintf(stderr, "[hg] encode_host_overlapped: issue %.2f ms, wait %.2f ms, %zu chunks\n",
                 t_issued - t_start, now() - t_issued, evs.size());
     for (hipEvent_t e : evs) (void)hipEventDestroy(e);
-    if (r == HG_OK && h_rec_off) r = d2h_pipelined(c, h_rec_off, drec, n * sizeof(uint64_t));
-    if (r == HG_OK && h_blocks && nb) r = d2h_pipelined(c, h_blocks, dblk, nb * sizeof(hg_block));
+    if (r == HG_OK && h_rec_off) r = rt_d2h_pipelined(c, h_rec_off, drec, n * sizeof(uint64_t));
+    if (r == HG_OK && h_blocks && nb) r = rt_d2h_pipelined(c, h_blocks, dblk, nb * sizeof(hg_block));
     return r;
 }
 
@@ -692,7 +709,7 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
     if (out_len) *out_len = total;
     if (total > cap) return HG_ERR_CAPACITY;
     if (n && total && arena_len && getenv("HG_ENCODE_HOST_SERIAL") == nullptr &&
-        host_pinned(h_arena) && host_pinned(h_pairs) && host_pinned(h_out))
+        rt_host_pinned(h_arena) && rt_host_pinned(h_pairs) && rt_host_pinned(h_out))
         return encode_host_overlapped(c, h_arena, arena_len, h_pairs, n, h_out, total, h_rec_off,
                                       block_stride, h_blocks);
     const uint64_t nb = h_blocks ? hg_block_count(n, block_stride) : 0;
@@ -705,8 +722,8 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
     if ((r = ensure(c, c->d_out, total ? total : 1)) != HG_OK) return r;
     if ((r = ensure(c, c->d_aux, blocks_at + nb * sizeof(hg_block) + 64)) != HG_OK) return r;
     char* din = static_cast<char*>(c->d_in.p);
-    if (arena_len && (r = h2d_pipelined(c, din, h_arena, arena_len)) != HG_OK) return r;
-    if (n && (r = h2d_pipelined(c, din + pairs_at, h_pairs, n * sizeof(hg_pair))) != HG_OK)
+    if (arena_len && (r = rt_h2d_pipelined(c, din, h_arena, arena_len)) != HG_OK) return r;
+    if (n && (r = rt_h2d_pipelined(c, din + pairs_at, h_pairs, n * sizeof(hg_pair))) != HG_OK)
         return r;
     uint64_t* d_rec = static_cast<uint64_t*>(c->d_aux.p);
     hg_block* d_blk = h_blocks ? reinterpret_cast<hg_block*>(static_cast<char*>(c->d_aux.p) + blocks_at)
@@ -716,10 +733,10 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
                       reinterpret_cast<const hg_pair*>(din + pairs_at), n,
                       static_cast<uint8_t*>(c->d_out.p), total, d_rec, block_stride, d_blk, &got);
     if (r != HG_OK) return r;
-    if (total && (r = d2h_pipelined(c, h_out, c->d_out.p, total)) != HG_OK) return r;
-    if (h_rec_off && n && (r = d2h_pipelined(c, h_rec_off, d_rec, n * sizeof(uint64_t))) != HG_OK)
+    if (total && (r = rt_d2h_pipelined(c, h_out, c->d_out.p, total)) != HG_OK) return r;
+    if (h_rec_off && n && (r = rt_d2h_pipelined(c, h_rec_off, d_rec, n * sizeof(uint64_t))) != HG_OK)
         return r;
-    if (h_blocks && nb && (r = d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block))) != HG_OK)
+    if (h_blocks && nb && (r = rt_d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block))) != HG_OK)
         return r;
     return HG_OK;
 }
@@ -815,7 +832,7 @@ int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
     for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
         sp[t] = spans + sofs[t];
         counts[t] = 0;
-        if (lens[t]) r = h2d_pipelined(c, arena + toff[t], h_tables[t], lens[t]);
+        if (lens[t]) r = rt_h2d_pipelined(c, arena + toff[t], h_tables[t], lens[t]);
     }
     if (r == HG_OK && ntables) {
         const uint8_t** dt = new (std::nothrow) const uint8_t*[ntables];
@@ -881,9 +898,9 @@ int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
             if (enc > cap) {
                 r = HG_ERR_CAPACITY;
             } else {
-                if (enc) r = d2h_pipelined(c, h_out, c->d_out.p, enc);
+                if (enc) r = rt_d2h_pipelined(c, h_out, c->d_out.p, enc);
                 if (r == HG_OK && h_blocks && nb)
-                    r = d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block));
+                    r = rt_d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block));
             }
         }
     }
@@ -928,7 +945,7 @@ int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, const uint8_
     int r;
     if ((r = ensure(c, c->d_in, len ? len : 1)) != HG_OK) return r;
     if ((r = ensure(c, c->d_out, (cap ? cap : 1) * sizeof(hg_span))) != HG_OK) return r;
-    if (len && (r = h2d_pipelined(c, c->d_in.p, h_table, len)) != HG_OK) return r;
+    if (len && (r = rt_h2d_pipelined(c, c->d_in.p, h_table, len)) != HG_OK) return r;
     uint64_t n = 0;
     hg_err e{};
     if (len) {
@@ -941,8 +958,8 @@ int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, const uint8_
     if ((r = ensure(c, c->lk_keys, qat + (nq ? nq : 1) * sizeof(hg_key))) != HG_OK) return r;
     if ((r = ensure(c, c->lk_res, (nq ? nq : 1) * sizeof(hg_lookup_result))) != HG_OK) return r;
     char* kd = static_cast<char*>(c->lk_keys.p);
-    if (keys_len && (r = h2d_pipelined(c, kd, h_keys, keys_len)) != HG_OK) return r;
-    if (nq && (r = h2d_pipelined(c, kd + qat, h_queries, nq * sizeof(hg_key))) != HG_OK) return r;
+    if (keys_len && (r = rt_h2d_pipelined(c, kd, h_keys, keys_len)) != HG_OK) return r;
+    if (nq && (r = rt_h2d_pipelined(c, kd + qat, h_queries, nq * sizeof(hg_key))) != HG_OK) return r;
     r = hg_keyindex_build_dev_async(c, static_cast<const uint8_t*>(c->d_in.p), len,
                                     static_cast<const hg_span*>(c->d_out.p), n, c->lk_index.p);
     if (r == HG_OK)
@@ -952,9 +969,22 @@ int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, const uint8_
                                 reinterpret_cast<const hg_key*>(kd + qat), nq,
                                 static_cast<hg_lookup_result*>(c->lk_res.p));
     if (r != HG_OK) return r;
-    if (nq && (r = d2h_pipelined(c, h_results, c->lk_res.p, nq * sizeof(hg_lookup_result))) != HG_OK)
+    if (nq && (r = rt_d2h_pipelined(c, h_results, c->lk_res.p, nq * sizeof(hg_lookup_result))) != HG_OK)
         return r;
     return HG_OK;
 }
 
 }  // extern "C"
+
+// Internal entry points for hg_multi.hip (hg_internal.hpp).
+namespace hgi {
+int ensure_aux(hg_ctx* c, int want) { return rt_ensure_aux(c, want); }
+bool host_pinned(const void* p) { return rt_host_pinned(p); }
+int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    return rt_h2d_pipelined(c, dst, src, bytes);
+}
+int d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
+    return rt_d2h_pipelined(c, dst, src, bytes);
+}
+void par_memcpy(void* dst, const void* src, size_t n) { rt_par_memcpy(dst, src, n); }
+}  // namespace hgi

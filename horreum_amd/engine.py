@@ -141,6 +141,43 @@ class Engine:
             raise HorreumGpuError(rc, "hg_decode_host")
         return DecodeOut(spans[: min(n.value, cap)], n.value, err.kind, err.offset)
 
+    def decode_range_dev(self, sst, length, begin, stop, entry, spans=None, cap=None):
+        """Range decode (hg_decode_range_dev): the records of the device
+        table `sst` (length bytes) that start in [entry, stop), entry an exact
+        record start.  Returns (DecodeOut, exit)."""
+        if cap is None:
+            cap = max(int(stop) - int(begin), 0) // 16 + 2 if spans is None \
+                else spans.numel() // SPAN_DTYPE.itemsize
+        if spans is None:
+            spans = self.empty(max(int(cap), 1) * SPAN_DTYPE.itemsize)
+        n, ex, err = ctypes.c_uint64(), ctypes.c_uint64(), HgErr()
+        rc = self.lib.hg_decode_range_dev(self.ctx, _ptr(sst), int(length), int(begin), int(stop),
+                                          int(entry), _ptr(spans), int(cap), ctypes.byref(n),
+                                          ctypes.byref(ex), ctypes.byref(err))
+        if rc < 0:
+            raise HorreumGpuError(rc, "hg_decode_range_dev")
+        return DecodeOut(spans, n.value, err.kind, err.offset), ex.value
+
+    def guess_entry_dev(self, sst, length, stop):
+        """Speculative first record start at or after `stop` (a guess)."""
+        e = ctypes.c_uint64()
+        check(self.lib.hg_decode_guess_entry_dev(self.ctx, _ptr(sst), int(length), int(stop),
+                                                 ctypes.byref(e)), "hg_decode_guess_entry_dev")
+        return e.value
+
+    def encoded_size(self, pairs, n=None):
+        """sum(16 + klen + vlen) of hg_pair records: a numpy PAIR_DTYPE array
+        (summed on the host) or a uint8 device tensor (reduced on the device)."""
+        out = ctypes.c_uint64()
+        if isinstance(pairs, np.ndarray):
+            pairs = np.ascontiguousarray(pairs, dtype=PAIR_DTYPE)
+            ptr, n = pairs.ctypes.data_as(ctypes.c_void_p), pairs.size
+        else:
+            ptr = _ptr(pairs)
+            n = pairs.numel() // PAIR_DTYPE.itemsize if n is None else int(n)
+        check(self.lib.hg_encoded_size(self.ctx, ptr, n, ctypes.byref(out)), "hg_encoded_size")
+        return out.value
+
     # ---- host memory ---------------------------------------------------------------
     def host_register(self, array):
         """Page-lock a host numpy buffer for direct DMA (hipHostRegister)."""

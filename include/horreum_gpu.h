@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 3
+#define HG_ABI_VERSION 4
 
 /* Status codes: return values, and the `kind` field of hg_err / results. */
 enum hg_status {
@@ -115,7 +115,9 @@ typedef struct hg_encode_result {
 
 /* Result of a merge / compaction.  kind: HG_OK, HG_ERR_CAPACITY,
  * HG_ERR_EMPTY_MERGE, or a decode error of an input table (table, index =
- * failing byte offset). */
+ * failing byte offset).  On HG_OK from hg_merge_dev*, table = 1 when the
+ * input was not strictly increasing and the serial reference loop produced
+ * the output, else 0. */
 typedef struct hg_merge_result {
     uint64_t n_out;  /* merged records (tombstones included) */
     int32_t kind;
@@ -194,6 +196,36 @@ int hg_decode_host(hg_ctx* ctx, const uint8_t* h_sst, uint64_t len,
                    hg_span* h_spans, uint64_t cap,
                    uint64_t* n_out, hg_err* err);
 
+/* ---- range decode ------------------------------------------------------
+ * A table decoded in byte ranges: a single huge table split over devices
+ * (the entry handoff is one u64 per split, no collective), or
+ * decoded in chunks as its bytes arrive.  d_sst is the table's first byte;
+ * bytes [begin, min(len, stop + 16)) must be valid device memory.  Decodes
+ * the records that START in [entry, stop) -- `entry` must be the exact start
+ * of a record (0 for the first range, else the exit of the previous range;
+ * begin <= entry) -- with absolute offsets in the spans.  Records may end
+ * past `stop` (up to len).  On HG_OK *exit is the first record start at or
+ * after `stop` (the next range's entry; len at the table's end); the async
+ * form stores it in d_result->err_offset.  Format errors are reported as by
+ * hg_decode_dev (absolute offset), exactly where the reference's cursor walk
+ * (src/format.rs:54-58) would fail inside the range. */
+int hg_decode_range_dev_async(hg_ctx* ctx, const uint8_t* d_sst, uint64_t len,
+                              uint64_t begin, uint64_t stop, uint64_t entry,
+                              hg_span* d_spans, uint64_t cap,
+                              hg_decode_result* d_result);
+int hg_decode_range_dev(hg_ctx* ctx, const uint8_t* d_sst, uint64_t len,
+                        uint64_t begin, uint64_t stop, uint64_t entry,
+                        hg_span* d_spans, uint64_t cap, uint64_t* n_out,
+                        uint64_t* exit, hg_err* err);
+/* A GUESS of the first record start at or after `stop`: the 16 KiB before it
+ * are walked from a guessed entry (the decode engine's lead-in); the walk's
+ * exit is the guess.  Verify it against the exact exit of the previous range
+ * and decode again from that exit when they differ.  *entry = UINT64_MAX
+ * when nothing was found, len when stop >= len.  Bytes [stop - 16384 (or 0),
+ * min(len, stop + 16)) must be valid device memory. */
+int hg_decode_guess_entry_dev(hg_ctx* ctx, const uint8_t* d_sst, uint64_t len,
+                              uint64_t stop, uint64_t* entry);
+
 /* ---- encode ----------------------------------------------------------
  * Replaces InternalPair::serialize (src/format.rs:23-37) and
  * serialize_flatten (src/format.rs:40-42) as used by PersistedFile::new
@@ -219,6 +251,10 @@ int hg_encode_host(hg_ctx* ctx, const uint8_t* h_arena, uint64_t arena_len,
                    const hg_pair* h_pairs, uint64_t n, uint8_t* h_out,
                    uint64_t cap, uint64_t* h_rec_off, uint32_t block_stride,
                    hg_block* h_blocks, uint64_t* out_len);
+/* Bytes serialize_flatten would produce for pairs[0..n) (src/format.rs:40-42):
+ * sum(16 + klen + vlen).  `pairs` may be host or device memory (device: one
+ * reduction on the context stream, synchronised). */
+int hg_encoded_size(hg_ctx* ctx, const hg_pair* pairs, uint64_t n, uint64_t* bytes);
 
 /* ---- merge (compaction) ------------------------------------------------
  * Replaces SSTableManager::compact_inner (src/sstable/manager.rs:199-234),
@@ -290,6 +326,43 @@ int hg_lookup_host(hg_ctx* ctx, const uint8_t* h_table, uint64_t len,
 int hg_host_register(const void* h_ptr, uint64_t len);
 int hg_host_unregister(const void* h_ptr);
 int hg_host_is_pinned(const void* h_ptr);
+
+/* ---- several contexts: one host thread per context, no collectives -------
+ * ctxs[0..nctx) may be on different devices or on the same one; each is used
+ * by exactly one thread for the duration of the call.
+ *
+ * Many tables (SSTableManager::new opening a directory, manager.rs:47-55;
+ * BASELINE config 4): table i goes to context i % nctx; each context uploads
+ * its tables and decodes them in one batched launch chain.  spans of table i
+ * to h_spans[i] (capacity caps[i]), n_out[i] records, errs[i] its format
+ * error (kind HG_OK if none; errs may be NULL).  Returns HG_OK unless a
+ * runtime error occurred. */
+int hg_multi_decode_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
+                         const uint8_t* const* h_tables, const uint64_t* lens,
+                         hg_span* const* h_spans, const uint64_t* caps,
+                         uint64_t* n_out, hg_err* errs);
+/* One table cut into nctx byte ranges (16 KiB-aligned cuts): every context
+ * guesses its range's entry (hg_decode_guess_entry_dev), decodes the range
+ * from it, then the host hands the exact entry over in order (the previous
+ * range's exit) and a range entered off its guess is decoded again.  The
+ * result equals hg_decode_host's (spans, n_out, error kind and offset). */
+int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx,
+                              const uint8_t* h_sst, uint64_t len,
+                              hg_span* h_spans, uint64_t cap,
+                              uint64_t* n_out, hg_err* err);
+/* SSTableManager::compact (manager.rs:137-159) split by key range: every
+ * table is decoded on context i % nctx and its keys sampled; nctx-1
+ * splitter keys are taken from the samples; every context decodes, merges
+ * and encodes the slice of every table inside its key range; the output is
+ * the concatenation in key order with its block index -- byte-identical to
+ * hg_compact_host.  Input that is not strictly increasing (found by a
+ * slice's merge or at a cut) and tables that do not decode are compacted by
+ * hg_compact_host on ctxs[0], which follows the reference loop exactly. */
+int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
+                          const uint8_t* const* h_tables, const uint64_t* lens,
+                          uint8_t* h_out, uint64_t cap, uint64_t* out_len,
+                          uint32_t block_stride, hg_block* h_blocks,
+                          hg_merge_result* result);
 
 /* Number of blocks Index::new produces for n pairs: ceil(n / stride). */
 uint64_t hg_block_count(uint64_t n, uint32_t block_stride);

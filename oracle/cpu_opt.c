@@ -1,0 +1,196 @@
+/*
+ * cpu_opt.c — TEST INFRASTRUCTURE ONLY (bench.py's cpu_baseline leg).
+ *
+ * The "optimised multi-threaded CPU codec" row of BASELINE.md / SURVEY §8(d):
+ * the same byte work as the reference's codec (src/format.rs:23-77) written
+ * the way a tuned CPU implementation would, on all the host cores it is
+ * given -- no per-record allocation, spans instead of owned copies, and the
+ * serial cursor walk of deserialize_from_bytes (src/format.rs:54-58) split
+ * into byte ranges whose entries are guessed and then handed over in order
+ * (a wrong guess is redone from the exact entry), as the GPU engine does.
+ * Results are checked against hgo_decode / hgo_encode by the tests.
+ */
+#define _POSIX_C_SOURCE 199309L
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "horreum_oracle.h"
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static inline uint64_t ld64(const uint8_t* p) {
+    uint64_t v;
+    memcpy(&v, p, 8); /* little-endian host (x86-64 / aarch64) */
+    return v;
+}
+
+/* Record at pos readable as the reference would read it (src/format.rs:63-69). */
+static inline int rec_ok(const uint8_t* b, uint64_t len, uint64_t pos, uint64_t* next) {
+    if (len - pos < 16) return 0;
+    const uint64_t k = ld64(b + pos), v = ld64(b + pos + 8);
+    if (k > UINT64_MAX - v || k + v > len - pos - 16) return 0;
+    if ((k >> 32) | (v >> 32)) return 0;
+    *next = pos + 16 + k + v;
+    return 1;
+}
+
+/* Serial walk of the records starting in [x, stop): spans to out (<= cap),
+ * count, exit.  Returns 0, or the error kind at *err_pos. */
+static int walk_range(const uint8_t* b, uint64_t len, uint64_t x, uint64_t stop, hg_span* out,
+                      uint64_t cap, uint64_t* cnt, uint64_t* exit, uint64_t* err_pos) {
+    uint64_t n = 0, pos = x;
+    int kind = HG_OK;
+    while (pos < stop) {
+        if (len - pos < 16) { kind = HG_ERR_TRUNCATED_HEADER; break; }
+        const uint64_t k = ld64(b + pos), v = ld64(b + pos + 8);
+        if (k > UINT64_MAX - v) { kind = HG_ERR_LEN_OVERFLOW; break; }
+        if (k + v > len - pos - 16) { kind = HG_ERR_TRUNCATED_BODY; break; }
+        if ((k >> 32) | (v >> 32)) { kind = HG_ERR_SPAN_RANGE; break; }
+        if (n < cap) {
+            out[n].off = pos;
+            out[n].klen = (uint32_t)k;
+            out[n].vlen = (uint32_t)v;
+        }
+        ++n;
+        pos += 16 + k + v;
+    }
+    *cnt = n;
+    *exit = pos;
+    *err_pos = pos;
+    return kind;
+}
+
+/* Guess of the first record start at or after b0: the first position whose
+ * record and the next three chain as readable records (or reach len). */
+static uint64_t guess_entry(const uint8_t* b, uint64_t len, uint64_t b0) {
+    for (uint64_t p = b0; p + 16 <= len; ++p) {
+        uint64_t q = p, nx;
+        int ok = 1;
+        for (int h = 0; h < 4 && q < len; ++h) {
+            if (!rec_ok(b, len, q, &nx)) { ok = 0; break; }
+            q = nx;
+        }
+        if (ok) return p;
+    }
+    return len;
+}
+
+typedef struct {
+    const uint8_t* b;
+    uint64_t len, lo, hi, guess, cnt, exit, err_pos;
+    hg_span* out;
+    uint64_t cap;
+    int kind;
+} range_job;
+
+static void* range_worker(void* arg) {
+    range_job* j = (range_job*)arg;
+    j->guess = j->lo ? guess_entry(j->b, j->len, j->lo) : 0;
+    j->kind = walk_range(j->b, j->len, j->guess, j->hi, j->out, j->cap, &j->cnt, &j->exit,
+                         &j->err_pos);
+    return NULL;
+}
+
+uint64_t hgo_mt_decode(const uint8_t* bytes, uint64_t len, hg_span* spans, uint64_t cap,
+                       hg_span* scratch, uint32_t nthreads, double* seconds) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    range_job jobs[256];
+    pthread_t th[256];
+    const double t0 = now_s();
+    for (uint32_t t = 0; t < nthreads; ++t) {
+        range_job* j = &jobs[t];
+        j->b = bytes;
+        j->len = len;
+        j->lo = len / nthreads * t;
+        j->hi = t + 1 == nthreads ? len : len / nthreads * (t + 1);
+        /* a range of W bytes holds <= W/16 + 1 starts; scratch holds
+         * len/16 + 2*nthreads + 2 spans, regions never overlap */
+        j->out = scratch + j->lo / 16 + 2 * (uint64_t)t;
+        j->cap = (j->hi - j->lo) / 16 + 2;
+        if (t) pthread_create(&th[t], NULL, range_worker, j);
+    }
+    range_worker(&jobs[0]);
+    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    /* entry handoff in order; spans into place */
+    uint64_t total = 0, bad = 0;
+    for (uint32_t t = 0; t < nthreads; ++t) {
+        range_job* j = &jobs[t];
+        if (t && j->guess != jobs[t - 1].exit) { /* redo from the exact entry */
+            j->guess = jobs[t - 1].exit;
+            j->kind = walk_range(bytes, len, j->guess, j->hi, j->out, j->cap, &j->cnt, &j->exit,
+                                 &j->err_pos);
+        }
+        const uint64_t m = total + j->cnt <= cap ? j->cnt : (total < cap ? cap - total : 0);
+        if (m) memmove(spans + total, j->out, m * sizeof(hg_span));
+        total += j->cnt;
+        if (j->kind != HG_OK) { bad = 1; break; }
+    }
+    if (seconds) *seconds = now_s() - t0;
+    return bad ? UINT64_MAX : total;
+}
+
+typedef struct {
+    const uint8_t* arena;
+    const hg_pair* pairs;
+    uint64_t lo, hi, base, bytes;
+    uint8_t* out;
+} enc_job;
+
+static void* enc_size_worker(void* arg) {
+    enc_job* j = (enc_job*)arg;
+    uint64_t s = 0;
+    for (uint64_t i = j->lo; i < j->hi; ++i) s += 16 + (uint64_t)j->pairs[i].klen + j->pairs[i].vlen;
+    j->bytes = s;
+    return NULL;
+}
+
+static void* enc_copy_worker(void* arg) {
+    enc_job* j = (enc_job*)arg;
+    uint8_t* o = j->out + j->base;
+    for (uint64_t i = j->lo; i < j->hi; ++i) {
+        const hg_pair* p = &j->pairs[i];
+        const uint64_t k = p->klen, v = p->vlen;
+        memcpy(o, &k, 8);
+        memcpy(o + 8, &v, 8);
+        memcpy(o + 16, j->arena + p->key_off, k);
+        if (v) memcpy(o + 16 + k, j->arena + p->val_off, v);
+        o += 16 + k + v;
+    }
+    return NULL;
+}
+
+uint64_t hgo_mt_encode(const uint8_t* arena, const hg_pair* pairs, uint64_t n, uint8_t* out,
+                       uint32_t nthreads, double* seconds) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    enc_job jobs[256];
+    pthread_t th[256];
+    const double t0 = now_s();
+    for (uint32_t t = 0; t < nthreads; ++t) {
+        jobs[t].arena = arena;
+        jobs[t].pairs = pairs;
+        jobs[t].out = out;
+        jobs[t].lo = n / nthreads * t;
+        jobs[t].hi = t + 1 == nthreads ? n : n / nthreads * (t + 1);
+        if (t) pthread_create(&th[t], NULL, enc_size_worker, &jobs[t]);
+    }
+    enc_size_worker(&jobs[0]);
+    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    uint64_t base = 0;
+    for (uint32_t t = 0; t < nthreads; ++t) {
+        jobs[t].base = base;
+        base += jobs[t].bytes;
+    }
+    for (uint32_t t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, enc_copy_worker, &jobs[t]);
+    enc_copy_worker(&jobs[0]);
+    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    if (seconds) *seconds = now_s() - t0;
+    return base;
+}

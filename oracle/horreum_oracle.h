@@ -65,6 +65,16 @@ uint64_t hgo_bench_decode_owned(const uint8_t* bytes, uint64_t len,
 uint64_t hgo_bench_encode_owned(const uint8_t* arena, const hg_pair* pairs,
                                 uint64_t n, double* seconds);
 
+/* Optimised multi-threaded CPU codec (cpu_opt.c; bench.py's cpu_baseline):
+ * decode into spans over `nthreads` byte ranges with guessed entries handed
+ * over in order (scratch: len/16 + 2*nthreads + 2 spans); records decoded,
+ * UINT64_MAX on a format error.  Encode: sizes, prefix, copy on `nthreads`
+ * threads; returns bytes written.  *seconds = wall time of the call. */
+uint64_t hgo_mt_decode(const uint8_t* bytes, uint64_t len, hg_span* spans, uint64_t cap,
+                       hg_span* scratch, uint32_t nthreads, double* seconds);
+uint64_t hgo_mt_encode(const uint8_t* arena, const hg_pair* pairs, uint64_t n, uint8_t* out,
+                       uint32_t nthreads, double* seconds);
+
 #ifdef __cplusplus
 }
 #endif

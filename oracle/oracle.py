@@ -12,7 +12,7 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboracle.so")
+LIB = os.environ.get("HGO_LIBRARY") or os.path.join(HERE, "liboracle.so")
 
 SPAN_DTYPE = np.dtype([("off", "<u8"), ("klen", "<u4"), ("vlen", "<u4")])
 PAIR_DTYPE = np.dtype([("key_off", "<u8"), ("val_off", "<u8"), ("klen", "<u4"), ("vlen", "<u4")])
@@ -51,6 +51,10 @@ def lib():
         L.hgo_bench_decode_owned.restype = u64
         L.hgo_bench_encode_owned.argtypes = [vp, vp, u64, ctypes.POINTER(ctypes.c_double)]
         L.hgo_bench_encode_owned.restype = u64
+        L.hgo_mt_decode.argtypes = [vp, u64, vp, u64, vp, u32, ctypes.POINTER(ctypes.c_double)]
+        L.hgo_mt_decode.restype = u64
+        L.hgo_mt_encode.argtypes = [vp, vp, u64, vp, u32, ctypes.POINTER(ctypes.c_double)]
+        L.hgo_mt_encode.restype = u64
         _lib = L
     return _lib
 
@@ -170,3 +174,26 @@ def bench_encode_owned(arena, pairs):
     t = ctypes.c_double()
     n = lib().hgo_bench_encode_owned(_p(arena), _p(pairs), pairs.size, ctypes.byref(t))
     return n, t.value
+
+
+def mt_decode(data, nthreads, spans=None, scratch=None):
+    """Optimised multi-threaded CPU decode (cpu_opt.c) -> (spans, n, seconds)."""
+    buf = _u8(data)
+    if spans is None:
+        spans = np.zeros(max(buf.size // 16, 1), dtype=SPAN_DTYPE)
+    if scratch is None:
+        scratch = np.empty(buf.size // 16 + 2 * nthreads + 2, dtype=SPAN_DTYPE)
+    t = ctypes.c_double()
+    n = lib().hgo_mt_decode(_p(buf), buf.size, _p(spans), spans.size, _p(scratch), nthreads,
+                            ctypes.byref(t))
+    return spans, n, t.value
+
+
+def mt_encode(arena, pairs, nthreads, out=None):
+    """Optimised multi-threaded CPU encode (cpu_opt.c) -> (bytes, seconds)."""
+    total = int((16 + pairs["klen"].astype(np.uint64) + pairs["vlen"].astype(np.uint64)).sum())
+    if out is None:
+        out = np.empty(max(total, 1), dtype=np.uint8)
+    t = ctypes.c_double()
+    n = lib().hgo_mt_encode(_p(arena), _p(pairs), pairs.size, _p(out), nthreads, ctypes.byref(t))
+    return out[:n], t.value

@@ -1,0 +1,220 @@
+"""GPU parity of the multi-context paths (include/horreum_gpu.h
+"several contexts"): range decode with an explicit entry, the speculative
+range entry, a single table split over contexts with the host entry handoff,
+many tables spread over contexts, and compaction split by key range -- all
+against the oracle (src/format.rs:50-77, src/sstable/manager.rs:199-234) and
+against the single-context engine, byte for byte.  The contexts are two or
+three on device 0, each driven by its own host thread inside the library;
+one test also drives two Engine contexts from two Python threads."""
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from tests import corpus
+from tests.test_merge_gpu import encode_tables, sorted_tables
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def multi2():
+    from horreum_amd.multi import MultiEngine
+    m = MultiEngine([0, 0])
+    yield m
+    m.close()
+
+
+@pytest.fixture(scope="module")
+def multi3():
+    from horreum_amd.multi import MultiEngine
+    m = MultiEngine([0, 0, 0])
+    yield m
+    m.close()
+
+
+# ---- range decode -----------------------------------------------------------------
+@pytest.mark.parametrize("name", ["fixed_16_100", "mixed_small", "tiny", "zero_values",
+                                  "mixed_4k", "large_values"])
+def test_range_decode_chain(engine, name):
+    """Cut a table at arbitrary byte offsets; decoding range after range from
+    the previous range's exit reproduces the whole-table spans exactly."""
+    _, _, data, _ = corpus.make(name)
+    want, wn, wk, _, _ = oracle.decode(data)
+    assert wk == 0
+    d = engine.to_device(data)
+    L = data.size
+    rng = np.random.default_rng(L)
+    cuts = sorted(set([0, L] + rng.integers(1, L, size=5).tolist() + [16384, 16400]))
+    cuts = [c for c in cuts if c <= L]
+    entry, got = 0, []
+    for b, e in zip(cuts[:-1], cuts[1:]):
+        out, ex = engine.decode_range_dev(d, L, b, e, entry)
+        assert out.kind == 0, (b, e, out.kind, out.offset)
+        got.append(engine.spans_to_numpy(out.spans, out.n))
+        assert ex >= e or ex == L
+        entry = ex
+    got = np.concatenate(got) if got else np.zeros(0, oracle.SPAN_DTYPE)
+    assert got.size == wn
+    assert np.array_equal(got, want)
+
+
+def test_range_decode_error_inside(engine):
+    """A truncated table: the range holding the failing record reports the
+    reference's error kind and absolute offset."""
+    _, _, data, rec_off = corpus.make("mixed_small")
+    bad = data[: int(rec_off[20000]) + 9]  # cut inside a header
+    want, wn, wk, wo, _ = oracle.decode(bad)
+    d = engine.to_device(bad)
+    L = bad.size
+    mid = (L // 2) & ~15
+    out0, ex = engine.decode_range_dev(d, L, 0, mid, 0)
+    assert out0.kind == 0
+    out1, _ = engine.decode_range_dev(d, L, mid, L, ex)
+    assert (out0.n + out1.n, out1.kind, out1.offset) == (wn, wk, wo)
+
+
+@pytest.mark.parametrize("name", ["fixed_16_100", "mixed_small", "mixed_4k"])
+def test_guess_entry(engine, name):
+    """The speculative entry of a cut is (on these corpora) the exact first
+    record start at or after it."""
+    _, _, data, rec_off = corpus.make(name)
+    d = engine.to_device(data)
+    starts = np.asarray(rec_off, dtype=np.uint64)
+    for cut in (16384, 50000, data.size // 2, data.size - 100):
+        g = engine.guess_entry_dev(d, data.size, cut)
+        i = np.searchsorted(starts, cut)
+        exact = int(starts[i]) if i < starts.size else data.size
+        assert g == exact, (cut, g, exact)
+    assert engine.guess_entry_dev(d, data.size, data.size) == data.size
+
+
+# ---- encoded size -----------------------------------------------------------------
+def test_encoded_size(engine):
+    arena, pairs, data, _ = corpus.make("mixed_4k")
+    assert engine.encoded_size(pairs) == data.size
+    dp = engine.to_device(pairs.view(np.uint8))
+    assert engine.encoded_size(dp, pairs.size) == data.size
+    assert engine.encoded_size(pairs[:0]) == 0
+
+
+# ---- one table over several contexts ---------------------------------------------------
+@pytest.mark.parametrize("name", ["fixed_16_100", "mixed_small", "tiny", "empty_keys_tombs",
+                                  "zero_values", "mixed_4k", "large_values"])
+def test_decode_file_split(multi3, name):
+    _, _, data, _ = corpus.make(name)
+    want, wn, wk, wo, _ = oracle.decode(data)
+    out = multi3.decode_file(data)
+    assert (out.n, out.kind, out.offset) == (wn, wk, wo)
+    assert np.array_equal(out.spans, want)
+
+
+def test_decode_file_split_errors(multi2):
+    _, _, data, rec_off = corpus.make("mixed_small")
+    for cut in (int(rec_off[25000]) + 3, int(rec_off[3000]) + 20, data.size - 1):
+        bad = data[:cut]
+        want, wn, wk, wo, _ = oracle.decode(bad)
+        out = multi2.decode_file(bad)
+        assert (out.n, out.kind, out.offset) == (wn, wk, wo), cut
+        assert np.array_equal(out.spans[:wn], want[:wn])
+
+
+def test_decode_file_split_large(multi2):
+    """cfg 2 shape, 64 MiB, split over two contexts."""
+    arena, pairs = corpus.fixed(500_000, 16, 100, seed=21)
+    data = oracle.encode(arena, pairs)[0]
+    want, wn, wk, _, _ = oracle.decode(data)
+    out = multi2.decode_file(data)
+    assert (out.n, out.kind) == (wn, wk) and np.array_equal(out.spans, want)
+
+
+# ---- many tables over several contexts -------------------------------------------------
+def test_decode_tables_round_robin(multi3):
+    """cfg 4 shape in miniature: 7 tables of mixed 8 B..4 KiB values with
+    tombstones (and one empty, one truncated) over three contexts."""
+    tables = []
+    for t in range(7):
+        arena, pairs = corpus.mixed(400 + 50 * t, 16, 4096, seed=40 + t, kmin=16, vmin=8)
+        tables.append(oracle.encode(arena, pairs)[0])
+    tables[3] = np.zeros(0, np.uint8)
+    tables[5] = tables[5][:-7]
+    outs = multi3.decode_tables(tables)
+    for d, o in zip(tables, outs):
+        want, wn, wk, wo, _ = oracle.decode(d)
+        assert (o.n, o.kind, o.offset) == (wn, wk, wo)
+        assert np.array_equal(o.spans[:wn], want[:wn])
+
+
+# ---- compaction split by key range ------------------------------------------------------
+@pytest.mark.parametrize("k,n_universe,frac,seed,stride", [
+    (8, 20000, 0.3, 31, 0),
+    (8, 8000, 0.8, 32, 10),   # heavy overlap
+    (3, 6000, 0.5, 33, 7),
+    (5, 9000, 0.4, 34, 1),
+])
+def test_compact_split_by_key_range(engine, multi3, k, n_universe, frac, seed, stride):
+    tables = sorted_tables(k, n_universe, frac, seed, long_prefix=seed % 2 == 0)
+    datas = [d.tobytes() for d in encode_tables(tables)]
+    single = engine.compact_host(datas, block_stride=stride)
+    split = multi3.compact(datas, block_stride=stride)
+    assert split.status == 0 and single.status == 0
+    assert split.n == single.n
+    assert np.array_equal(split.data, single.data)
+    if stride:
+        assert np.array_equal(split.blocks, single.blocks)
+    # and the oracle: serialize_flatten(compact_inner(tables newest first))
+    tabs = [(np.frombuffer(d, np.uint8), oracle.decode(np.frombuffer(d, np.uint8))[0])
+            for d in datas]
+    refs, _ = oracle.compact(tabs)
+    merged = [oracle.pairs_from_spans(tabs[t][0], tabs[t][1][r:r + 1])[0] for t, r in refs]
+    arena, rec = oracle.pack_pairs(merged)
+    want, _, wblocks, _ = oracle.encode(arena, rec, block_stride=stride)
+    assert np.array_equal(split.data, want)
+    if stride:
+        assert np.array_equal(split.blocks, wblocks)
+
+
+def test_compact_split_unsorted_falls_back(engine, multi2):
+    """Tables with duplicate / unordered keys are not range-separable: the
+    split compaction hands them to one context's exact reference loop."""
+    tables = sorted_tables(4, 3000, 0.5, 35)
+    tables[1] = tables[1][::-1]
+    tables[2] = tables[2] + tables[2][:30]
+    datas = [d.tobytes() for d in encode_tables(tables)]
+    single = engine.compact_host(datas, block_stride=3)
+    split = multi2.compact(datas, block_stride=3)
+    assert split.status == single.status == 0
+    assert np.array_equal(split.data, single.data)
+    assert np.array_equal(split.blocks, single.blocks)
+
+
+# ---- contexts driven from separate Python threads ---------------------------------------
+def test_two_contexts_two_threads():
+    """include/horreum_gpu.h: distinct contexts may be used from distinct
+    threads.  Two Engines on device 0, each decoding and encoding its own
+    corpus repeatedly in its own thread, both bit-exact."""
+    from horreum_amd.engine import Engine
+    jobs = [corpus.make("mixed_small"), corpus.make("mixed_4k")]
+    errors = []
+
+    def work(i):
+        try:
+            eng = Engine(0, use_torch_stream=False)
+            arena, pairs, data, _ = jobs[i]
+            want = oracle.decode(data)[0]
+            for _ in range(5):
+                out = eng.decode_host(data)
+                assert out.kind == 0 and np.array_equal(out.spans, want)
+                enc = eng.encode_host(arena, pairs)
+                assert np.array_equal(enc.data, data)
+            eng.close()
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((i, repr(e)))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors

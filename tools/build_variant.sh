@@ -9,7 +9,7 @@ rm -rf "$out"; mkdir -p "$out"
 cd "$root/horreum_amd/csrc"
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-value -Wno-unused-result $defs"
 pids=()
-for f in hg_decode hg_encode hg_merge hg_lookup hg_runtime; do
+for f in hg_decode hg_encode hg_merge hg_lookup hg_runtime hg_multi; do
   /opt/rocm/bin/hipcc $F -c $f.hip -o "$out/$f.o" & pids+=($!)
 done
 for p in "${pids[@]}"; do wait $p || { echo "compile failed" >&2; exit 1; }; done
