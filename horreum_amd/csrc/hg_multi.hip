@@ -483,8 +483,13 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
         return (int)HG_OK;
     });
     if (r != HG_OK) return r;
-    for (uint32_t t = 0; t < ntables; ++t)
+    for (uint32_t t = 0; t < ntables; ++t) {
+        // lower bounds over unordered keys need not be monotone either
+        for (uint32_t g = 0; g < nrange && cut_ok[t]; ++g)
+            if (cut_rec[t][g] > cut_rec[t][g + 1] || cut_off[t][g] > cut_off[t][g + 1])
+                cut_ok[t] = 0;
         if (!cut_ok[t]) return single();
+    }
     // 4. every range on its context: its slice of every table -> decode ->
     //    merge -> encode (+ record offsets for the block index)
     struct Out {

@@ -457,11 +457,94 @@ int hg_host_unregister(const void* h_ptr) {
 
 int hg_host_is_pinned(const void* h_ptr) { return h_ptr && rt_host_pinned(h_ptr) ? 1 : 0; }
 
+// Page-locked table and span buffers: the table goes up in chunks on one
+// stream (each chunk carries 4 KiB of the next one, the bytes a range decode
+// may read past its stop), chunk i is range-decoded on the context stream as
+// soon as it has landed -- entered at the exit of chunk i-1, its spans written
+// straight after chunk i-1's -- and its spans go down on a third stream while
+// later chunks are still going up (PCIe is full duplex).  One host sync per
+// chunk reads its exit and count.  HG_DEC_CHUNK_MB sets the chunk (default 128).
+static int decode_host_overlapped(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spans,
+                                  uint64_t cap, uint64_t* n_out, hg_err* err) {
+    const char* env = getenv("HG_DEC_CHUNK_MB");
+    const uint64_t C = (uint64_t)(env ? std::max(1, atoi(env)) : 128) << 20;
+    const uint64_t K = (len + C - 1) / C;
+    int r = rt_ensure_aux(c, 2);
+    if (r == HG_OK) r = ensure(c, c->d_in, len);
+    if (r == HG_OK) r = ensure(c, c->d_out, (len / 16 + 2 * K + 2) * sizeof(hg_span));
+    if (r == HG_OK) r = ensure(c, c->ws, hgk_decode_workspace_bytes(C));
+    if (r != HG_OK) return r;
+    hipStream_t up = c->aux[0], down = c->aux[1], cs = c->stream;
+    std::vector<hipEvent_t> ev(2 * K, nullptr);
+    for (auto& e : ev)
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = HG_ERR_HIP;
+    uint8_t* din = static_cast<uint8_t*>(c->d_in.p);
+    hg_span* dsp = static_cast<hg_span*>(c->d_out.p);
+    for (uint64_t i = 0; r == HG_OK && i < K; ++i) {
+        const uint64_t b = i * C, hi = std::min(len, (i + 1) * C + 4096);
+        if (hipMemcpyAsync(din + b, h_sst + b, hi - b, hipMemcpyHostToDevice, up) != hipSuccess ||
+            hipEventRecord(ev[i], up) != hipSuccess)
+            r = HG_ERR_HIP;
+    }
+    uint64_t entry = 0, G = 0, errpos = 0;
+    int32_t kind = HG_OK;
+    for (uint64_t i = 0; r == HG_OK && i < K; ++i) {
+        const uint64_t b = i * C, stop = std::min(len, (i + 1) * C);
+        const uint64_t rlen = std::min(len, (i + 1) * C + 4096);
+        if (hipStreamWaitEvent(cs, ev[i], 0) != hipSuccess) { r = HG_ERR_HIP; break; }
+        r = hgk_decode_range_launch(din, len, rlen, b, stop, entry, dsp + G, (stop - b) / 16 + 2,
+                                    dres(c), c->ws.p, cs);
+        if (r != HG_OK) break;
+        if (hipMemcpyAsync(c->hres.p, dres(c), sizeof(hg_decode_result), hipMemcpyDeviceToHost,
+                           cs) != hipSuccess ||
+            hipStreamSynchronize(cs) != hipSuccess) {
+            r = HG_ERR_HIP;
+            break;
+        }
+        const hg_decode_result res = *static_cast<hg_decode_result*>(c->hres.p);
+        const uint64_t ncopy = G < cap ? std::min(res.n_records, cap - G) : 0;
+        if (ncopy && (hipEventRecord(ev[K + i], cs) != hipSuccess ||
+                      hipStreamWaitEvent(down, ev[K + i], 0) != hipSuccess ||
+                      hipMemcpyAsync(h_spans + G, dsp + G, ncopy * sizeof(hg_span),
+                                     hipMemcpyDeviceToHost, down) != hipSuccess)) {
+            r = HG_ERR_HIP;
+            break;
+        }
+        G += res.n_records;
+        if (res.kind != HG_OK) {  // the reference stops at the first unreadable record
+            kind = res.kind;
+            errpos = res.err_offset;
+            break;
+        }
+        entry = res.err_offset;  // the exit: the next chunk's entry
+    }
+    if (hipStreamSynchronize(down) != hipSuccess || hipStreamSynchronize(up) != hipSuccess)
+        r = r == HG_OK ? HG_ERR_HIP : r;
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (r != HG_OK) return r;
+    if (n_out) *n_out = G;
+    if (err) {
+        err->kind = kind;
+        err->reserved = 0;
+        err->offset = kind != HG_OK ? errpos : 0;
+    }
+    if (kind != HG_OK) return kind;
+    return G > cap ? HG_ERR_CAPACITY : HG_OK;
+}
+
 int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spans, uint64_t cap,
                    uint64_t* n_out, hg_err* err) {
     if (!c || (len && !h_sst) || (cap && !h_spans)) return HG_ERR_INVALID_ARG;
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
     if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    {
+        const char* env = getenv("HG_DEC_CHUNK_MB");
+        const uint64_t C = (uint64_t)(env ? std::max(1, atoi(env)) : 128) << 20;
+        if (len >= 2 * C && getenv("HG_DECODE_HOST_SERIAL") == nullptr && rt_host_pinned(h_sst) &&
+            (!cap || rt_host_pinned(h_spans)))
+            return decode_host_overlapped(c, h_sst, len, h_spans, cap, n_out, err);
+    }
     // A file of L bytes holds at most L/16 records.
     const uint64_t dcap = std::min<uint64_t>(cap, len / 16);
     int r;

@@ -17,6 +17,7 @@ DecodeOut = namedtuple("DecodeOut", "spans n kind offset")
 EncodeOut = namedtuple("EncodeOut", "data rec_off blocks out_len")
 MergeOut = namedtuple("MergeOut", "status n kind table index")
 CompactOut = namedtuple("CompactOut", "status data blocks n kind table index")
+ResidentTable = namedtuple("ResidentTable", "table spans index n kind offset")
 
 
 def _torch():
@@ -178,6 +179,34 @@ class Engine:
         check(self.lib.hg_encoded_size(self.ctx, ptr, n, ctypes.byref(out)), "hg_encoded_size")
         return out.value
 
+    def decode_many_host(self, tables):
+        """Many host tables (bytes-like) decoded by ONE batched launch chain on
+        this context (hg_multi_decode_host with one context; the cold open of
+        a table directory, src/sstable/manager.rs:47-55) -> [DecodeOut]."""
+        bufs = [np.ascontiguousarray(np.frombuffer(memoryview(t).cast("B"), dtype=np.uint8))
+                for t in tables]
+        k = len(bufs)
+        if k == 0:
+            return []
+        spans = [np.zeros(max(b.size // 16, 1), dtype=SPAN_DTYPE) for b in bufs]
+        tp = (ctypes.c_void_p * k)(*[b.ctypes.data if b.size else 0 for b in bufs])
+        ln = (ctypes.c_uint64 * k)(*[b.size for b in bufs])
+        sp = (ctypes.c_void_p * k)(*[x.ctypes.data for x in spans])
+        cp = (ctypes.c_uint64 * k)(*[b.size // 16 for b in bufs])
+        n_out = (ctypes.c_uint64 * k)()
+        errs = (HgErr * k)()
+        ctxs = (ctypes.c_void_p * 1)(self.ctx.value)
+        check(self.lib.hg_multi_decode_host(ctypes.cast(ctxs, ctypes.c_void_p), 1, k,
+                                            ctypes.cast(tp, ctypes.c_void_p),
+                                            ctypes.cast(ln, ctypes.c_void_p),
+                                            ctypes.cast(sp, ctypes.c_void_p),
+                                            ctypes.cast(cp, ctypes.c_void_p),
+                                            ctypes.cast(n_out, ctypes.c_void_p),
+                                            ctypes.cast(errs, ctypes.c_void_p)),
+              "hg_multi_decode_host")
+        return [DecodeOut(spans[i][:min(n_out[i], bufs[i].size // 16)], n_out[i], errs[i].kind,
+                          errs[i].offset) for i in range(k)]
+
     # ---- host memory ---------------------------------------------------------------
     def host_register(self, array):
         """Page-lock a host numpy buffer for direct DMA (hipHostRegister)."""
@@ -270,6 +299,32 @@ class Engine:
                                       desc.ctypes.data_as(ctypes.c_void_p), desc.size,
                                       out.ctypes.data_as(ctypes.c_void_p)), "hg_lookup_host")
         return out[: desc.size]
+
+    def resident_table(self, data):
+        """Upload host table bytes once and keep what lookups need in HBM:
+        the bytes, their spans and the key index (SSTable::get's state,
+        src/sstable/table.rs:54-70).  Raises DecodeError-like HorreumGpuError
+        via the caller if the table does not decode."""
+        buf = np.ascontiguousarray(np.frombuffer(memoryview(data).cast("B"), dtype=np.uint8))
+        dev = self.to_device(buf)
+        out = self.decode_dev(dev, buf.size)
+        idx = self.keyindex_build(dev, out.spans, out.n) if out.kind == 0 else None
+        return ResidentTable(dev, out.spans, idx, out.n, out.kind, out.offset)
+
+    def lookup_resident(self, rt, keys):
+        """Batched point lookups against a ResidentTable: only the query keys
+        go up and the results come back (LOOKUP_DTYPE)."""
+        torch = _torch()
+        arena, desc = self.pack_keys(keys)
+        nq = desc.size
+        res = torch.empty(max(nq, 1) * LOOKUP_DTYPE.itemsize, dtype=torch.uint8,
+                          device=self.device)
+        if nq:
+            kd = self.to_device(arena)
+            qd = self.to_device(desc.view(np.uint8))
+            self.lookup_dev_async(rt.table, rt.spans, rt.index, rt.n, kd, qd, nq, res)
+        out = res[: nq * LOOKUP_DTYPE.itemsize].cpu().numpy().view(LOOKUP_DTYPE)
+        return out
 
     def keyindex_build(self, table, spans, n):
         """Device key index (32 B per record) of a decoded device table."""

@@ -20,6 +20,7 @@ Reference quirks kept on purpose:
 import os
 
 from .engine import default_engine
+from .format import DecodeError
 from .index import Index
 from .table import PersistedFile, SSTable
 
@@ -39,8 +40,25 @@ class SSTableManager:
         self.engine = engine
         paths = sorted(os.path.join(self.table_directory, f)
                        for f in os.listdir(self.table_directory))
-        self.tables = [SSTable.open(p, block_stride, engine) for p in paths]
+        self.tables = self._open_all(paths)
         self.compaction_trigger_ratio = compaction_trigger_ratio / 100.0
+
+    def _open_all(self, paths):
+        """manager.rs:47-55 as ONE batched decode of every table (the files
+        mmap'd and page-locked, one launch chain for all of them); a table
+        that does not decode raises DecodeError like SSTable.open."""
+        if not paths:
+            return []
+        eng = self.engine or default_engine()
+        files = [PersistedFile.open(p) for p in paths]
+        datas = [f.read_bytes(eng) for f in files]
+        outs = eng.decode_many_host(datas)
+        tables = []
+        for f, d, o in zip(files, datas, outs):
+            if o.kind != 0:
+                raise DecodeError(o.kind, o.offset, o.n)
+            tables.append(SSTable.from_decoded(f, d, o.spans, self.block_stride))
+        return tables
 
     def _new_table_path(self):
         return os.path.join(self.table_directory, f"table_{len(self.tables)}")
@@ -98,7 +116,7 @@ class SSTableManager:
         if size is None:
             return False
         eng = self.engine or default_engine()
-        datas = [t.file.read_bytes() for t in reversed(self.tables)]  # newest first (:148)
+        datas = [t.file.read_bytes(eng) for t in reversed(self.tables)]  # newest first (:148)
         out = eng.compact_host(datas, block_stride=self.block_stride)
         if out.status != 0:
             raise CompactionError(out)

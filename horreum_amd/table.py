@@ -5,6 +5,13 @@ The byte work -- encoding on write, decoding on open / get / get_all, the
 block index -- runs in libhorreum_gpu.so; this module does file I/O and the
 reference's host logic (binary searches, size accounting) only.
 
+Host memory: a table file is mmap'd once and the mapping is
+page-locked with hg_host_register, so every later transfer of its bytes
+(open, get_all, compaction) is a direct DMA from the page cache's pages --
+no read() copy and no staging copy.  A directory opens with one batched
+decode of all its tables (SSTableManager).  Batched lookups keep the table,
+its spans and its key index resident in HBM after the first batch.
+
 Quirks kept from the reference:
 - `PersistedFile.new` opens with create+write+read and NO truncate
   (storage.rs:24-30): writing a shorter table over a longer file leaves the
@@ -13,9 +20,12 @@ Quirks kept from the reference:
   (table.rs:36-45); for a decoded table that is L - 16·n.
 """
 import bisect
+import mmap
 import os
 
-from .format import decode_spans, pairs_from_spans, serialize_flatten
+import numpy as np
+
+from .format import DecodeError, decode_spans, pairs_from_spans, serialize_flatten
 from .index import Index
 
 
@@ -24,6 +34,7 @@ class PersistedFile:
 
     def __init__(self, path):
         self.path = os.fspath(path)
+        self._map = None      # (mmap, numpy view, registered engine or None)
 
     @classmethod
     def new(cls, path, pairs, engine=None):
@@ -33,6 +44,7 @@ class PersistedFile:
         return f
 
     def write_bytes(self, data):
+        self.unmap()
         fd = os.open(self.path, os.O_CREAT | os.O_RDWR, 0o644)  # no O_TRUNC (storage.rs:24-30)
         try:
             mv = memoryview(data)
@@ -49,9 +61,57 @@ class PersistedFile:
             raise FileNotFoundError(path)
         return cls(path)
 
-    def read_bytes(self):
+    def mapped(self, engine=None):
+        """The whole file as a uint8 array over a private mmap of it,
+        page-locked with hg_host_register when the engine can (so transfers
+        are direct DMA); the mapping lives until delete() / unmap()."""
+        if self._map is not None:
+            return self._map[1]
+        size = os.path.getsize(self.path)
+        if size == 0:
+            self._map = (None, np.zeros(0, dtype=np.uint8), None)
+            return self._map[1]
         with open(self.path, "rb") as fh:
-            return fh.read()
+            mm = mmap.mmap(fh.fileno(), size, access=mmap.ACCESS_COPY)
+        arr = np.frombuffer(mm, dtype=np.uint8)
+        reg = None
+        try:
+            from .engine import default_engine
+            eng = engine or default_engine()
+            eng.host_register(arr)
+            reg = eng
+        except Exception:  # noqa: BLE001 -- pageable fallback (staged copies)
+            reg = None
+        self._map = (mm, arr, reg)
+        return arr
+
+    def unmap(self):
+        if self._map is None:
+            return
+        mm, arr, reg = self._map
+        self._map = None
+        if reg is not None:
+            try:
+                reg.host_unregister(arr)
+            except Exception:  # noqa: BLE001
+                pass
+        del arr
+        if mm is not None:
+            try:
+                mm.close()
+            except BufferError:  # views still exported: the mapping goes with them
+                pass
+
+    def __del__(self):
+        # a registration must end before its pages are unmapped: a stale one
+        # would make a later mapping at the same address look page-locked
+        try:
+            self.unmap()
+        except Exception:  # noqa: BLE001 -- interpreter shutdown
+            pass
+
+    def read_bytes(self, engine=None):
+        return self.mapped(engine)
 
     def read_at(self, position, length):
         """storage.rs:52-57: exactly `length` bytes at `position`
@@ -65,10 +125,11 @@ class PersistedFile:
 
     def read_all(self, engine=None):
         """storage.rs:60-67 (decode errors raise DecodeError; the reference panics)."""
-        data = self.read_bytes()
+        data = self.read_bytes(engine)
         return pairs_from_spans(data, decode_spans(data, engine))
 
     def delete(self):
+        self.unmap()
         os.remove(self.path)
 
 
@@ -79,6 +140,7 @@ class SSTable:
         self.file = file
         self.index = index
         self.size = size
+        self._resident = None  # (engine, ResidentTable): lookups stay in HBM
 
     @classmethod
     def create(cls, path, pairs, size, block_stride, engine=None):
@@ -101,8 +163,14 @@ class SSTable:
         """table.rs:33-49: decode the whole file once; size and index come
         from the spans (no re-encode)."""
         f = PersistedFile.open(path)
-        data = f.read_bytes()
-        spans = decode_spans(data, engine)
+        data = f.read_bytes(engine)
+        return cls.from_decoded(f, data, decode_spans(data, engine), block_stride)
+
+    @classmethod
+    def from_decoded(cls, f, data, spans, block_stride):
+        """An opened table from its bytes and spans (table.rs:36-49)."""
+        if block_stride <= 0:
+            raise ValueError("block_stride must be positive (reference: chunks(0) panics)")
         size = len(data) - 16 * int(spans.size)
         return cls(f, Index.from_spans(data, spans, block_stride), size)
 
@@ -119,16 +187,29 @@ class SSTable:
         i = bisect.bisect_left(keys, key)
         return pairs[i] if i < len(keys) and keys[i] == key else None
 
+    def resident(self, engine=None):
+        """The table in HBM for batched lookups: uploaded, decoded and
+        indexed by the first call, reused by every later one."""
+        from .engine import default_engine
+        eng = engine or default_engine()
+        if self._resident is None or self._resident[0] is not eng:
+            rt = eng.resident_table(self.file.read_bytes(eng))
+            if rt.kind != 0:
+                raise DecodeError(rt.kind, rt.offset, rt.n)
+            self._resident = (eng, rt)
+        return self._resident[1]
+
     def get_many(self, keys, engine=None):
-        """SSTable::get for a batch of keys in one device launch (the table is
-        read once, decoded, indexed and searched on the GPU).  Returns one
-        InternalPair (tombstones included) or None per key."""
+        """SSTable::get for a batch of keys in one device launch against the
+        resident table (only the keys go up).  Returns one InternalPair
+        (tombstones included) or None per key."""
         from .engine import default_engine
         from .format import InternalPair
         eng = engine or default_engine()
-        data = self.file.read_bytes()
-        res = eng.lookup_host(data, keys)
-        mv = memoryview(data)
+        rt = self.resident(eng)
+        res = eng.lookup_resident(rt, keys)
+        data = self.file.read_bytes(eng)
+        mv = memoryview(data).cast("B")
         out = []
         for k, r in zip(keys, res):
             if not r["found"]:
@@ -146,4 +227,5 @@ class SSTable:
         return self.size
 
     def delete(self):
+        self._resident = None
         self.file.delete()

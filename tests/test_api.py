@@ -135,7 +135,7 @@ def test_storage_read(engine, golden, tmp_path):
     """src/sstable/storage.rs:78-107."""
     c = golden["storage_read"]
     f = PersistedFile.new(tmp_path / "s", _pairs(c), engine)
-    assert f.read_bytes() == bytes.fromhex(c["bytes"])
+    assert bytes(f.read_bytes(engine)) == bytes.fromhex(c["bytes"])
     assert f.read_at(0, 24) == bytes.fromhex(c["bytes"])[:24]
     assert f.read_all(engine) == _pairs(c)
     pairs = _pairs(golden["storage_read_all"])
@@ -228,7 +228,7 @@ def test_no_truncate_overwrite_fails_decode(engine, golden, tmp_path):
     path = tmp_path / "q"
     PersistedFile.new(path, long_pairs, engine)
     f = PersistedFile.new(path, short_pairs, engine)
-    data = f.read_bytes()
+    data = bytes(f.read_bytes(engine))
     assert data.startswith(InternalPair.serialize_flatten(short_pairs, engine))
     want = oracle.decode(np.frombuffer(data, np.uint8))
     try:
@@ -237,3 +237,34 @@ def test_no_truncate_overwrite_fails_decode(engine, golden, tmp_path):
         assert [(p.key, p.value) for p in got] == oracle.pairs_from_spans(data, want[0])
     except DecodeError as e:
         assert (e.kind, e.offset, e.n_ok) == (want[2], want[3], want[1])
+
+
+@pytest.mark.gpu
+def test_mapped_file_is_page_locked(engine, golden, tmp_path):
+    """a table file is mmap'd and registered once; its bytes
+    then go to the device by direct DMA (hg_host_is_pinned)."""
+    c = golden["storage_read"]
+    f = PersistedFile.new(tmp_path / "m", _pairs(c), engine)
+    arr = f.mapped(engine)
+    assert bytes(arr) == bytes.fromhex(c["bytes"])
+    assert engine.host_is_pinned(arr)
+    assert f.read_all(engine) == _pairs(c)
+    f.delete()
+    assert not (tmp_path / "m").exists()
+
+
+@pytest.mark.gpu
+def test_resident_lookups(engine, golden, tmp_path):
+    """SSTable.get_many keeps the table resident in HBM: a second batch
+    reuses it (no re-upload, no re-decode) and agrees with get()."""
+    from horreum_amd.table import SSTable
+    c = golden["table_search"]
+    pairs = _pairs(c)
+    t = SSTable.create(tmp_path / "r", pairs, 0, 3, engine)
+    keys = [p.key for p in pairs] + [b"abc", b"zzz", b""]
+    first = t.get_many(keys, engine)
+    rt = t.resident(engine)
+    second = t.get_many(list(reversed(keys)), engine)
+    assert t.resident(engine) is rt
+    assert first == [t.get(k, engine) for k in keys]
+    assert second == list(reversed(first))
