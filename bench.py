@@ -93,16 +93,25 @@ DECODE_KERNELS = ("decode_spec_kernel", "decode_kernel")
 
 
 def load_traffic(kernels):
-    """HBM bytes per decode call (sum over its kernels) from the committed PMC
-    summary, or None if it does not cover every kernel."""
+    """(HBM bytes per decode call summed over its kernels, source commit of
+    the PMC summary) from the committed profiles/pmc_summary.json; (None,
+    None) if it does not cover every kernel."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path, encoding="utf-8") as f:
             pmc = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, None
     vals = [pmc.get(k, {}).get("hbm_bytes_per_launch") for k in kernels]
-    return None if any(v is None for v in vals) else float(sum(vals))
+    src = dict(pmc.get("_source", {}))
+    try:  # does the summary describe the decode kernels being run now?
+        import hashlib
+        cur = hashlib.sha256(open(os.path.join(ROOT, "horreum_amd", "csrc", "hg_decode.hip"),
+                                  "rb").read()).hexdigest()
+        src["current_source"] = src.get("hg_decode_sha256") == cur
+    except OSError:
+        src["current_source"] = None
+    return (None if any(v is None for v in vals) else float(sum(vals))), src
 
 
 def time_async(torch, fn, steps, warmup, world, device):
@@ -147,7 +156,57 @@ def cpu_baseline(sst_dev, n_records, sample_mb, seconds):
             "kind": "port",
             "sample": f"{passes} passes over the first {nrec} records ({host.size} B) of the "
                       f"same table, hgo_bench_decode_owned, {total_s:.2f} s",
+            "all_cores": cpu_all_cores(host),
             "extra": cpu_extras(host)}
+
+
+def host_cores():
+    """(threads to use, the machine's nproc, this process's CPU affinity): the
+    GPU box gives one GPU's job a share of a larger machine (OMP_NUM_THREADS
+    holds that share), so nproc alone overstates it."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = nproc
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or aff
+    return max(1, min(share, aff)), nproc, aff
+
+
+def cpu_all_cores(host_sample, seconds=2.0):
+    """The optimised multi-threaded CPU codec (oracle/cpu_opt.c: byte ranges
+    with guessed entries handed over in order, spans not owned copies;
+    sizes / prefix / copy for encode) on every host core this job may use:
+    cfg 2 decode of the same sample, cfg 3 encode of a 1 M-pair sample."""
+    from horreum_amd import synth
+    from oracle import oracle
+    threads, nproc, aff = host_cores()
+    want_n = host_sample.size // (16 + CFG2["k"] + CFG2["v"])
+    spans = np.zeros(host_sample.size // 16 + 1, dtype=oracle.SPAN_DTYPE)
+    scratch = np.empty(host_sample.size // 16 + 2 * threads + 2, dtype=oracle.SPAN_DTYPE)
+    tot, k = 0.0, 0
+    while k == 0 or tot < seconds:
+        _, n, t = oracle.mt_decode(host_sample, threads, spans, scratch)
+        assert n == want_n, (n, want_n)
+        tot += t
+        k += 1
+    dec = k * host_sample.size / tot / GIB
+    arena, pairs = synth.fixed_arena(1_000_000, 32, 256, seed=3, device="cpu")
+    a, p = arena.numpy(), pairs.numpy().view(oracle.PAIR_DTYPE)
+    out = np.empty(304_000_000, dtype=np.uint8)
+    tot, k = 0.0, 0
+    while k == 0 or tot < seconds:
+        got, t = oracle.mt_encode(a, p, threads, out)
+        assert got.size == 304_000_000
+        tot += t
+        k += 1
+    enc = k * 304_000_000 / tot / GIB
+    ok = bool(np.array_equal(spans[:1000], oracle.decode(host_sample[:132000])[0]))
+    return {"cores": threads, "nproc": nproc, "affinity": aff, "kind": "port (tuned)",
+            "decode_cfg2_GiB_s": round(dec, 3), "encode_cfg3_1M_GiB_s": round(enc, 3),
+            "sample": f"decode: the same {host_sample.size} B cfg 2 sample; encode: 1 M pairs of "
+                      f"32 B / 256 B; hgo_mt_decode / hgo_mt_encode, >= {seconds} s each",
+            "parity_spot": ok}
 
 
 def cpu_extras(host_sample, seconds=1.0):
@@ -246,7 +305,7 @@ def main(argv=None):
     mean_launch_ms = sum(launch_ms) / len(launch_ms)
     alg_bytes = L + 16 * n
     achieved = alg_bytes / (mean_launch_ms * 1e-3) / 1e9
-    traffic = load_traffic(DECODE_KERNELS)
+    traffic, traffic_src = load_traffic(DECODE_KERNELS)
 
     extra = {}
     if not args.no_encode:
@@ -258,6 +317,9 @@ def main(argv=None):
         extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank,
                                                          host=not args.no_host and world == 1)
 
+    if not args.no_extra:
+        extra["decode_general"] = general_legs(torch, eng, device, world)
+        extra["lookups"] = lookup_leg(torch, eng, sst, n, k, v)
     if not args.no_host and world == 1:
         extra["host_inclusive"] = host_leg(torch, eng, sst, n, world)
 
@@ -277,6 +339,8 @@ def main(argv=None):
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (device Philox, seed 2 + 1000*rank)",
+            "value_is": "decode of BASELINE configs[1] (cfg2), GiB/s of SSTable bytes; encode "
+                        "(cfg3) and the other configs are under extra",
             "config": {"workload": "cfg2 single-SSTable decode (BASELINE configs[1])",
                        "records_per_gpu": n, "sst_bytes_per_gpu": L, "key_bytes": k,
                        "value_bytes": v, "decode_piece_bytes": 16384,
@@ -285,6 +349,7 @@ def main(argv=None):
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "decode call: status memset + decode_spec_kernel (dominant) + "
                                    "decode_kernel (prefix spans + general engine)",
                          "alg_bytes_per_launch": alg_bytes,
@@ -298,6 +363,100 @@ def main(argv=None):
         import torch.distributed as dist
         dist.destroy_process_group()
     return 0 if ok else 1
+
+
+GENERAL_SHAPES = [  # (label, records, key range, value range, tombstones, seed)
+    ("small mixed 0..24B/0..64B", 4_000_000, (0, 24), (0, 64), 0.05, 4),
+    ("medium 8..64B/64..512B", 1_500_000, (8, 65), (64, 513), 0.05, 4),
+]
+
+
+def general_legs(torch, eng, device, world, reps=8):
+    """The general decode engine (no stride run, no hop) on variable-size
+    records: small (0-24 B keys / 0-64 B values) and medium (8-64 B / 64-512 B)
+    tables, device resident; roofline against the same algorithmic bytes as
+    the headline (L + 16 n), HIP-event time of the decode call; spans checked
+    against the oracle."""
+    from horreum_amd import synth
+    from oracle import oracle
+    out = {}
+    pmc = {}
+    try:
+        for s in ("small", "medium"):
+            with open(os.path.join(ROOT, "profiles", f"r2_pmc_{s}.json"), encoding="utf-8") as f:
+                pmc[s] = json.load(f)
+    except (OSError, ValueError):
+        pass
+    for label, m, kr, vr, tomb, seed in GENERAL_SHAPES:
+        host = synth.mixed_sst_host(m, kr, vr, tomb, seed)
+        sst = torch.from_numpy(host).to(device)
+        L = host.size
+        cap = L // 16
+        spans = eng.empty(cap * 16)
+        res = eng.empty(64)
+        eng.reserve(L, 0)
+
+        def step():
+            eng.decode_dev_async(sst, L, spans, cap, res)
+
+        wall, ms = time_async(torch, step, reps, 2, world, device)
+        mean_ms = sum(ms) / len(ms)
+        want, wn, wk, _, _ = oracle.decode(host)
+        nn = int(res[:8].cpu().numpy().view("<u8")[0])
+        ok = nn == wn and bool(np.array_equal(
+            spans[: nn * 16].cpu().numpy().view(oracle.SPAN_DTYPE), want))
+        alg = L + 16 * wn
+        key = "small" if label.startswith("small") else "medium"
+        kern = pmc.get(key, {}).get("kernels", {})
+        traffic = sum(kern.get(k, {}).get("hbm_read_bytes", 0) + kern.get(k, {}).get(
+            "hbm_write_bytes", 0) for k in ("hgk::decode_spec_kernel",
+                                            "hgk::decode_kernel<false>")) or None
+        out[key] = {"workload": label, "bytes": L, "records": wn,
+                    "ms": round(mean_ms, 4), "value_GiB_s": round(L / (mean_ms * 1e-3) / GIB, 2),
+                    "roofline": {"bound": "hbm", "achieved": round(alg / (mean_ms * 1e-3) / 1e9, 1),
+                                 "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                 "frac": round(alg / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                 "traffic": traffic,
+                                 "traffic_source": f"profiles/r2_pmc_{key}.json"},
+                    "parity_ok": ok}
+        del sst, spans
+        torch.cuda.empty_cache()
+    return out
+
+
+def lookup_leg(torch, eng, sst, n, k, v, batch=1 << 20):
+    """SSTable::get (src/sstable/table.rs:54-70) for 1 M-key batches against
+    the cfg 2 table resident in HBM (spans + key index built once): lookups
+    per second, half the keys present, half absent."""
+    from horreum_amd import synth
+    L = sst.numel()
+    out = eng.decode_dev(sst, L)
+    idx = eng.keyindex_build(sst, out.spans, out.n)
+    g = torch.Generator(device=sst.device)
+    g.manual_seed(7)
+    ids = torch.randint(0, 2 * n, (batch,), device=sst.device, generator=g)
+    keys = synth.be_counter_keys(2 * n, k, sst.device)[ids].contiguous()  # [batch, k]
+    q = torch.empty((batch, 2), dtype=torch.int64, device=sst.device)
+    q[:, 0] = torch.arange(batch, device=sst.device) * k
+    q[:, 1] = k
+    res = eng.empty(batch * 24)
+
+    def step():
+        eng.lookup_dev_async(sst, out.spans, idx, out.n, keys.view(-1), q.view(torch.uint8),
+                             batch, res)
+
+    wall, ms = time_async(torch, step, 10, 2, 1, sst.device)
+    r = res.cpu().numpy().view(np.dtype([("rec", "<u8"), ("val_off", "<u8"), ("vlen", "<u4"),
+                                         ("found", "<i4")]))
+    ids_h = ids.cpu().numpy()
+    ok = bool(np.array_equal(r["found"] != 0, ids_h < n)
+              and np.array_equal(r["rec"][ids_h < n], ids_h[ids_h < n]))
+    mean_ms = sum(ms) / len(ms)
+    del idx, keys, q, res
+    torch.cuda.empty_cache()
+    return {"lookups_per_s": round(batch / (mean_ms * 1e-3)), "batch": batch,
+            "ms_per_batch": round(mean_ms, 4), "table": "cfg2 (8.1 M records, resident)",
+            "parity_ok": ok}
 
 
 def encode_leg(torch, eng, device, args, world, rank):
@@ -318,7 +477,10 @@ def encode_leg(torch, eng, device, args, world, rank):
     r = res[:16].cpu().numpy()
     out_len = int(r[:8].view("<u8")[0])
     rr = out.view(n, 16 + k + v)
-    ok = out_len == total and torch.equal(rr[:, 16:], arena.view(n, k + v))
+    hdr = torch.zeros(16, dtype=torch.uint8, device=device)
+    hdr[0], hdr[8], hdr[9] = k, v & 0xFF, v >> 8  # [u64 LE klen][u64 LE vlen] (src/format.rs:24-28)
+    ok = (out_len == total and torch.equal(rr[:, 16:], arena.view(n, k + v))
+          and bool((rr[:, :16] == hdr).all()))
     mean_ms = sum(launch_ms) / len(launch_ms)
     alg = n * (k + v) + 24 * n + total  # read payload + descriptors, write table
     del arena, pairs, out
@@ -452,6 +614,11 @@ def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32):
     r = res.cpu().numpy()
     ok = all(int(r[24 * i:24 * i + 8].view("<u8")[0]) == n and
              int(r[24 * i + 8:24 * i + 12].view("<i4")[0]) == 0 for i, (_, n) in enumerate(tabs))
+    from oracle import oracle  # spans of the first and last table, record for record
+    for i in (0, len(tabs) - 1):
+        want = oracle.decode(bufs[i].cpu().numpy())[0]
+        got = spans[i][: want.size * 16].cpu().numpy().view(oracle.SPAN_DTYPE)
+        ok = ok and bool(np.array_equal(got, want))
     recs = sum(n for _, n in tabs)
     mean_ms = sum(ms) / len(ms)
     del tabs, spans, bufs
@@ -459,8 +626,11 @@ def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32):
     return {"value": round(aggregate(wall, steps, world, total), 3), "unit": "GiB/s",
             "tables_per_gpu": tables_per_gpu, "bytes_per_gpu": total, "records_per_gpu": recs,
             "ms_per_step": round(wall / steps * 1e3, 4),
-            "achieved_GBs": round((total + 16 * recs) / (mean_ms * 1e-3) / 1e9, 1),
-            "parity_ok": bool(ok)}
+            "alg_GBs": round((total + 16 * recs) / (mean_ms * 1e-3) / 1e9, 1),
+            "alg_GBs_note": "table bytes + spans per second; hop mode reads ~1 cache line "
+                            "per ~2 KiB record, so this is not an HBM fraction",
+            "parity_ok": bool(ok), "parity": "counts + kinds of all tables, spans of the first "
+                                              "and last table vs the oracle"}
 
 
 def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000, host=False):

@@ -1588,7 +1588,7 @@ constexpr uint32_t HOP_SEGS = SPEC_BP / HOP_SEG_PIECES;   // per pre-pass batch,
 constexpr uint32_t HOP_WIN = 4096;                        // guess window (bytes)
 constexpr uint32_t HOP_CHECK = 3;                         // hops a guess must survive
 #ifndef HG_HOP_MAX_CAND
-#define HG_HOP_MAX_CAND 96  // ~4 candidates per record: hop only records of >= ~0.7 KiB
+#define HG_HOP_MAX_CAND 32  // candidate run ends in piece 0 (~1-2 per record): hop >= ~0.5-1 KiB records
 #endif
 constexpr uint32_t HOP_MAX_CAND = HG_HOP_MAX_CAND;        // large-record test on piece 0
 constexpr uint32_t HOP_MAX_RECS = 128;  // a segment walk gives up past this (small records)
@@ -1727,10 +1727,19 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
         const uint32_t plim = plim64 < 0xFFFFFFFFull ? (uint32_t)plim64 : 0xFFFFFFFFu;
         const uint32_t clen = piece_clen(a, base);
         const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
+        // count RUN ENDS of candidates: a genuine header with small lengths
+        // also passes the filter 1-3 bytes to its left, zero key bytes add
+        // runs of their own; the last position of each run is ~one per record
         uint32_t nc = 0;
+        uint32_t c = filter_bits(data, tid * GPT, a.hz, clen, plim, any_valid);
 #pragma unroll
-        for (uint32_t j = 0; j < GPT; ++j)
-            nc += __popc(filter_bits(data, tid * GPT + j, a.hz, clen, plim, any_valid));
+        for (uint32_t j = 0; j < GPT; ++j) {
+            const uint32_t nxt = (j + 1 < GPT || tid + 1 < THREADS)
+                                     ? filter_bits(data, tid * GPT + j + 1, a.hz, clen, plim, any_valid)
+                                     : 0u;
+            nc += __popc(c & ~((c >> 1) | ((nxt & 1u) << 15)));
+            c = nxt;
+        }
         nc = wave_sum<uint32_t>(nc);
         if (tid == 0) s.hcnt[0] = 0;
         __syncthreads();

@@ -106,3 +106,19 @@ def mixed_table_vlens(max_bytes, vmin, vmax, tomb_frac, seed):
     v[rng.random(est) < tomb_frac] = 0
     c = np.cumsum(32 + v)
     return v[: int(np.searchsorted(c, max_bytes, side="right"))]
+
+
+def mixed_sst_host(m, krange, vrange, tomb_frac, seed):
+    """numpy SSTable of m records, key lengths uniform in krange = (lo, hi)
+    and value lengths in vrange (hi exclusive), tomb_frac of the values
+    tombstones, random key/value bytes (tools/decode_variants.py shapes)."""
+    rng = np.random.default_rng(seed)
+    kl = rng.integers(*krange, m)
+    vl = rng.integers(*vrange, m)
+    vl[rng.random(m) < tomb_frac] = 0
+    offs = np.concatenate([[0], np.cumsum(16 + kl + vl)])
+    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
+    for i in range(16):
+        buf[offs[:-1] + i] = hdr[:, i]
+    return buf

@@ -95,6 +95,10 @@ def main():
                      "source": f"profiles/{tag}_pmc.json"}
     with open(os.path.join(prof, f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1)
+    import hashlib
+    src = os.path.join(ROOT, "horreum_amd", "csrc", "hg_decode.hip")
+    flat["_source"] = {"tag": tag, "commit": os.environ.get("GIT_COMMIT"),
+                       "hg_decode_sha256": hashlib.sha256(open(src, "rb").read()).hexdigest()}
     with open(os.path.join(prof, "pmc_summary.json"), "w") as f:
         json.dump(flat, f, indent=1)
     print(json.dumps(summary, indent=1))
