@@ -131,6 +131,12 @@ def index_get(blocks, arena, pairs, key):
 
 def compact(tables_newest_first):
     """tables: [(data uint8, spans)] newest first -> [(table, rec)], status."""
+    ot, orr, rc = compact_arrays(tables_newest_first)
+    return list(zip(ot.tolist(), orr.tolist())), rc
+
+
+def compact_arrays(tables_newest_first):
+    """compact() as arrays: (table index uint32[n], record index uint64[n], status)."""
     T = len(tables_newest_first)
     datas = [_u8(d) for d, _ in tables_newest_first]
     spans = [np.ascontiguousarray(s, dtype=SPAN_DTYPE) for _, s in tables_newest_first]
@@ -143,7 +149,36 @@ def compact(tables_newest_first):
     n = ctypes.c_uint64()
     rc = lib().hgo_compact(T, ctypes.cast(dptr, ctypes.c_void_p), ctypes.cast(sptr, ctypes.c_void_p),
                            _p(counts), _p(ot), _p(orr), cap, ctypes.byref(n))
-    return list(zip(ot[: n.value].tolist(), orr[: n.value].tolist())), rc
+    return ot[: n.value], orr[: n.value], rc
+
+
+def compacted_table(tables_newest_first, block_stride=0):
+    """serialize_flatten(compact_inner(decode(t) for t in tables)) -- the bytes
+    SSTableManager::compact writes (src/sstable/manager.rs:137-159, 199-234;
+    src/format.rs:40-42) -> (bytes uint8, blocks | None, records)."""
+    datas = [_u8(d) for d in tables_newest_first]
+    decs = []
+    for d in datas:
+        spans, n, kind, _, _ = decode(d)
+        assert kind == 0, "input table does not decode"
+        decs.append((d, spans[:n]))
+    ot, orr, rc = compact_arrays(decs)
+    assert rc == 0
+    base = np.zeros(len(datas) + 1, dtype=np.uint64)
+    np.cumsum([d.size for d in datas], out=base[1:])
+    arena = np.concatenate(datas) if datas else np.zeros(1, np.uint8)
+    pairs = np.zeros(ot.size, dtype=PAIR_DTYPE)
+    for t, (_, spans) in enumerate(decs):
+        sel = ot == t
+        s = spans[orr[sel]]
+        ko = base[t] + s["off"] + np.uint64(16)
+        pairs["key_off"][sel] = ko
+        pairs["val_off"][sel] = ko + s["klen"].astype(np.uint64)
+        pairs["klen"][sel] = s["klen"]
+        pairs["vlen"][sel] = s["vlen"]
+    data, _, blocks, rc = encode(arena, pairs, block_stride=block_stride)
+    assert rc == 0
+    return data, blocks, int(ot.size)
 
 
 def table_get(data, spans, stride, key):

@@ -153,3 +153,24 @@ def test_oracle_table_get(golden):
         else:
             got = oracle.pairs_from_spans(data, spans[r:r + 1])[0]
             assert got == (bytes.fromhex(want[0]), None if want[1] is None else bytes.fromhex(want[1]))
+
+
+def test_compacted_table_matches_compact_then_encode():
+    """oracle.compacted_table (used by the config-size GPU tests) equals
+    compact() + serialize_flatten of the picked pairs, blocks included."""
+    rng = np.random.default_rng(3)
+    tabs = []
+    for _ in range(4):
+        keys = sorted(set(rng.integers(0, 500, 300).tolist()))
+        pairs = [(b"k%05d" % k, None if rng.random() < .1 else
+                  bytes(rng.integers(0, 256, rng.integers(1, 40), dtype=np.uint8))) for k in keys]
+        arena, rec = oracle.pack_pairs(pairs)
+        tabs.append(oracle.encode(arena, rec)[0])
+    got, blocks, n = oracle.compacted_table(tabs, block_stride=7)
+    decs = [(d, oracle.decode(d)[0]) for d in tabs]
+    refs, _ = oracle.compact(decs)
+    merged = [oracle.pairs_from_spans(decs[t][0], decs[t][1][r:r + 1])[0] for t, r in refs]
+    arena, rec = oracle.pack_pairs(merged)
+    want, _, wblocks, _ = oracle.encode(arena, rec, block_stride=7)
+    assert n == len(merged)
+    assert np.array_equal(got, want) and np.array_equal(blocks, wblocks)
