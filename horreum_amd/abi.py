@@ -21,8 +21,12 @@ class HorreumGpuError(RuntimeError):
 
     def __init__(self, status, msg=""):
         self.status = int(status)
-        super().__init__(f"{msg}: {status_string(self.status)} ({self.status})" if msg
-                         else f"{status_string(self.status)} ({self.status})")
+        text = f"{status_string(self.status)} ({self.status})"
+        if self.status == Status.HIP:
+            site = last_hip_error()
+            if site:
+                text += f" at {site}"
+        super().__init__(f"{msg}: {text}" if msg else text)
 
 
 class Status(enum.IntEnum):
@@ -77,6 +81,7 @@ _u32 = ctypes.c_uint32
 _PROTOS = {
     "hg_abi_version": (ctypes.c_int, []),
     "hg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
+    "hg_last_hip_error": (ctypes.c_char_p, []),
     "hg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
     "hg_ctx_destroy": (ctypes.c_int, [_vp]),
     "hg_ctx_set_stream": (ctypes.c_int, [_vp, _vp]),
@@ -163,6 +168,14 @@ def status_string(status):
         return load_library().hg_status_string(int(status)).decode()
     except HorreumGpuError:
         return Status(status).name if status in Status._value2member_map_ else "unknown"
+
+
+def last_hip_error():
+    """Where the most recent HG_ERR_HIP came from (hg_last_hip_error)."""
+    global _lib
+    if _lib is None:
+        return ""
+    return _lib.hg_last_hip_error().decode()
 
 
 def check(status, what=""):

@@ -2210,7 +2210,7 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
     if (entry >= stop) {  // no record starts in the range: 0 records, exit = entry
         hipLaunchKernelGGL(decode_const_result, dim3(1), dim3(1), 0, stream, d_result,
                            range ? entry : 0ull);
-        return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+        return HG_LAUNCH_STATUS();
     }
     const uint64_t npieces = (stop - begin + PIECE - 1) / PIECE;
     const uint32_t res_gen = d_diag ? resident_workgroups(decode_kernel<true>, 1)
@@ -2220,7 +2220,7 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
     uint64_t zero_bytes = 0;
     const DecodeArgs a = make_args(d_sst, len, d_spans, cap, d_result, d_ws, d_diag, bp, sbp,
                                    zero_bytes, begin, stop, entry, range, rlen);
-    if (hipMemsetAsync(d_ws, 0, zero_bytes, stream) != hipSuccess) return HG_ERR_HIP;
+    if (hipMemsetAsync(d_ws, 0, zero_bytes, stream) != hipSuccess) return HG_HIP_FAIL;
     // 1. pre-pass (stride runs, hop walks): verifies, links neighbours, sums records per group
     // 2. decode_kernel: spans of the resolved prefix, then the general engine
     //    from the first unresolved batch on (exits at once if there is none)
@@ -2235,7 +2235,7 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
         hipLaunchKernelGGL(decode_kernel<true>, dim3(grid), dim3(THREADS), 0, stream, a);
     else
         hipLaunchKernelGGL(decode_kernel<false>, dim3(grid), dim3(THREADS), 0, stream, a);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }
 }  // namespace
 
@@ -2275,7 +2275,7 @@ extern "C" int hgk_decode_guess_launch(const uint8_t* d_sst, uint64_t len, uint6
     const DecodeArgs a = make_args(d_sst, len, nullptr, 0, nullptr, d_ws, nullptr, BATCH_MIN,
                                    SPEC_BP_MIN, zb, begin, stop, begin, true, rlen);
     hipLaunchKernelGGL(decode_guess_kernel, dim3(1), dim3(THREADS), 0, stream, a, d_out);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }
 
 extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
@@ -2331,7 +2331,7 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
     }
     const uint64_t bytes = hgk_decode_multi_stage_bytes(ntab);
     if (hipMemcpyAsync(d_stage, h_stage, bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     char* ds = static_cast<char*>(d_stage);
     const DecodeArgs* dargs = reinterpret_cast<const DecodeArgs*>(ds);
     const uint64_t* dzb = reinterpret_cast<const uint64_t*>(ds + args_b);
@@ -2344,5 +2344,5 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
     if (pre_d[ntab])
         hipLaunchKernelGGL(decode_multi, dim3(pre_d[ntab]), dim3(THREADS), 0, stream, dargs, dpre_d,
                            ntab);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }

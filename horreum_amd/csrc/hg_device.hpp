@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/horreum_gpu.h"
+#include "hg_err.hpp"
 
 namespace hgk {
 

@@ -529,16 +529,16 @@ extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pai
     uint64_t* gsum = tsum + nt;
     if (nt == 0) {
         if (hipMemsetAsync(d_result, 0, sizeof(hg_encode_result), stream) != hipSuccess)
-            return HG_ERR_HIP;
+            return HG_HIP_FAIL;
         return HG_OK;
     }
-    if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_ERR_HIP;
+    if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_HIP_FAIL;
     hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
                        d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum));
-    if (hipGetLastError() != hipSuccess) return HG_ERR_HIP;
+    if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng, cap,
                        d_result);
-    if (hipGetLastError() != hipSuccess) return HG_ERR_HIP;
+    if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     EncodeArgs a;
     a.arena = d_arena;
     a.pairs = d_pairs;
@@ -551,14 +551,14 @@ extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pai
     a.tile_sum = tsum;
     a.group_base = gsum;
     hipLaunchKernelGGL(encode_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream, a);
-    if (hipGetLastError() != hipSuccess) return HG_ERR_HIP;
+    if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     if (d_blocks) {
         const uint64_t nb = (n + block_stride - 1) / block_stride;
         const uint32_t grid = (uint32_t)((nb + 255) / 256);
         hipLaunchKernelGGL(blocks_kernel, dim3(grid), dim3(256), 0, stream, d_rec_off, n,
                            block_stride, (const hg_encode_result*)d_result, (uint64_t)0, d_blocks,
                            nb);
-        if (hipGetLastError() != hipSuccess) return HG_ERR_HIP;
+        if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     }
     return HG_OK;
 }
@@ -583,7 +583,7 @@ extern "C" int hgk_encode_blocks_launch(const uint64_t* d_rec_off, uint64_t n,
     const uint32_t grid = (uint32_t)((nb + 255) / 256);
     hipLaunchKernelGGL(blocks_kernel, dim3(grid), dim3(256), 0, stream, d_rec_off, n, block_stride,
                        (const hg_encode_result*)nullptr, total, d_blocks, nb);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }
 
 // Encoded size only (hg_encoded_size on device pairs): the tile sums and
@@ -599,13 +599,13 @@ extern "C" int hgk_encode_size_launch(const hg_pair* d_pairs, uint64_t n,
     if (nt == 0)
         return hipMemsetAsync(d_result, 0, sizeof(hg_encode_result), stream) == hipSuccess
                    ? HG_OK
-                   : HG_ERR_HIP;
-    if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_ERR_HIP;
+                   : HG_HIP_FAIL;
+    if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_HIP_FAIL;
     hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
                        d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum));
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng,
                        ~0ull, d_result);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }
 
 namespace hgk {
@@ -625,5 +625,5 @@ extern "C" int hgk_gather_stride_launch(const uint64_t* d_v, uint64_t n, uint64_
     const uint64_t m = (n - first + stride - 1) / stride;
     hipLaunchKernelGGL(hgk::gather_stride_kernel, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0,
                        stream, d_v, n, first, stride, d_out);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }

@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "../../include/horreum_gpu.h"
+#include "hg_err.hpp"
 
 extern "C" int hgk_decode_launch(const uint8_t*, uint64_t, hg_span*, uint64_t, hg_decode_result*,
                                  void*, hipStream_t);

@@ -115,7 +115,7 @@ extern "C" int hgk_keyindex_launch(const uint8_t* d_table, uint64_t len, const h
     hipLaunchKernelGGL(keyindex_kernel, dim3((uint32_t)((n + THREADS - 1) / THREADS)),
                        dim3(THREADS), 0, stream, d_table, len, d_spans, n,
                        static_cast<KEnt*>(d_index));
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }
 
 extern "C" int hgk_lookup_launch(const uint8_t* d_table, const hg_span* d_spans,
@@ -127,5 +127,5 @@ extern "C" int hgk_lookup_launch(const uint8_t* d_table, const hg_span* d_spans,
     hipLaunchKernelGGL(lookup_kernel, dim3((uint32_t)((nq + THREADS - 1) / THREADS)),
                        dim3(THREADS), 0, stream, d_table, d_spans,
                        static_cast<const KEnt*>(d_index), n, d_keys, d_queries, nq, d_results);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }

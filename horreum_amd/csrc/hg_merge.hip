@@ -273,8 +273,9 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
     const uint32_t tid = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
     if (t0 >= a.n) return;
-    // The error word is read now and tested after the segments are staged, so
-    // the tile's global round trips (split, segments) do not wait on it.
+    // The error word is loaded with the splits (one round trip) and tested
+    // before anything is staged: once the order check failed the splits are
+    // all 0 and the segments they imply run past the runs' ends.
     const unsigned long long err0 = *err;
     const uint64_t t1 = min(t0 + TILE, a.n);
     // The tile may span several output runs (pairs); handle each piece.
@@ -300,6 +301,7 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         // is fetched with the segments
         const uint64_t i0 = d0 == t0 ? split[blockIdx.x] : 0;
         const uint64_t i1 = d1 == oend ? na : split[blockIdx.x + 1];
+        if (err0 != ~0ull) return;  // an earlier check or round found unsorted input
         if (i1 < i0 || i0 > d0 - o || i1 > d1 - o || (d1 - o) - i1 < (d0 - o) - i0) {
             // splits of sorted runs are monotone; anything else means the
             // input was not sorted: flag it (the exact loop takes over) and stop
@@ -315,7 +317,6 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
             if (i0 > 0 && i0 <= na) s.aprev = A[i0 - 1];
         }
         __syncthreads();
-        if (err0 != ~0ull) return;  // an earlier round found unsorted input
         const MEnt* SA = s.seg;
         const MEnt* SB = s.seg + nA;
         MEnt* dst = out + d0;
@@ -669,8 +670,8 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     p += 256;
     ExactHead* heads = reinterpret_cast<ExactHead*>(p);
     if (hipMemcpyAsync(d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
-        return HG_ERR_HIP;
-    if (hipMemsetAsync(err, 0xFF, 8, stream) != hipSuccess) return HG_ERR_HIP;
+        return HG_HIP_FAIL;
+    if (hipMemsetAsync(err, 0xFF, 8, stream) != hipSuccess) return HG_HIP_FAIL;
 
     MergeArgs a;
     a.arena = d_arena;
@@ -685,7 +686,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         hg_merge_result r{0, HG_ERR_EMPTY_MERGE, 0, 0};
         return hipMemcpyAsync(d_result, &r, sizeof r, hipMemcpyHostToDevice, stream) == hipSuccess
                    ? HG_OK
-                   : HG_ERR_HIP;
+                   : HG_HIP_FAIL;
     }
     const uint32_t g1 = (uint32_t)((n + THREADS - 1) / THREADS);
     hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, e0);
@@ -720,5 +721,5 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                        (const unsigned long long*)err);
     hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)e0,
                        (const unsigned long long*)err, heads, d_out, cap, d_result);
-    return hipGetLastError() == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return HG_LAUNCH_STATUS();
 }

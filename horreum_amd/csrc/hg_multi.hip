@@ -54,7 +54,7 @@ int sync_d2h(hg_ctx* c, void* dst, const void* src, size_t n) {
     if (!n) return HG_OK;
     if (hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     return HG_OK;
 }
 
@@ -73,7 +73,7 @@ int decode_share(hg_ctx* c, Share& sh, const uint8_t* const* h_tables, const uin
     sh.soff.resize(k);
     sh.res.assign(k, hg_decode_result{0, HG_OK, 0, 0});
     if (!k) return HG_OK;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     uint64_t ab = 0, sb = 0;
     for (uint32_t j = 0; j < k; ++j) {
         const uint64_t L = lens[sh.ids[j]];
@@ -276,7 +276,7 @@ int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx, const uint8_t*
     int r = fan_out(nr, [&](uint32_t c) {
         hg_ctx* x = ctxs[c];
         Part& p = P[c];
-        if (set_dev(x) != HG_OK) return (int)HG_ERR_HIP;
+        if (set_dev(x) != HG_OK) return (int)HG_HIP_FAIL;
         p.lo = c ? B[c] - std::min(B[c], kPiece) : 0;
         p.hi = std::min(len, B[c + 1] + 16);
         int rr = ensure(x, x->d_in, p.hi - p.lo ? p.hi - p.lo : 1);
@@ -306,7 +306,7 @@ int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx, const uint8_t*
             break;
         }
         if (P[c].guess != P[c - 1].exit) {
-            if (set_dev(ctxs[c]) != HG_OK) return HG_ERR_HIP;
+            if (set_dev(ctxs[c]) != HG_OK) return HG_HIP_FAIL;
             P[c].guess = P[c - 1].exit;
             if ((r = decode_range(c, P[c].guess)) != HG_OK) return r;
         }
@@ -326,7 +326,7 @@ int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx, const uint8_t*
     // 3. spans into place
     r = fan_out(last + 1, [&](uint32_t c) {
         hg_ctx* x = ctxs[c];
-        if (set_dev(x) != HG_OK) return (int)HG_ERR_HIP;
+        if (set_dev(x) != HG_OK) return (int)HG_HIP_FAIL;
         if (G[c] >= cap) return (int)HG_OK;
         const uint64_t nc = std::min(P[c].n, cap - G[c]);
         return nc ? d2h_pipelined(x, h_spans + G[c], x->mspans.p, nc * sizeof(hg_span))
@@ -409,7 +409,7 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
         const KeyRef& kr = all[all.size() * g / nctx];
         hg_ctx* c = ctxs[owner[kr.table]];
         const Share& s = sh[owner[kr.table]];
-        if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+        if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
         hg_span sp;
         const hg_span* dsp = static_cast<const hg_span*>(c->mspans.p) + s.soff[slot[kr.table]];
         if ((r = sync_d2h(c, &sp, dsp + kr.rec, sizeof sp)) != HG_OK) return r;
@@ -447,7 +447,7 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
         hg_ctx* c = ctxs[ci];
         const Share& s = sh[ci];
         if (s.ids.empty()) return (int)HG_OK;
-        if (set_dev(c) != HG_OK) return (int)HG_ERR_HIP;
+        if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
         const size_t kb = (kbytes.size() + 255) & ~(size_t)255;
         const size_t need = kb + 16 * (nsplit + 1) + 256 + 24 * (size_t)(nsplit + 1) * s.ids.size();
         int rr = ensure(c, c->x_aux, need);
@@ -461,7 +461,7 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
                                           hipMemcpyHostToDevice) != hipSuccess) ||
             hipMemcpy(dko, kofs.data(), 8 * (nsplit + 1), hipMemcpyHostToDevice) != hipSuccess ||
             (nsplit && hipMemcpy(dkl, kls.data(), 4 * nsplit, hipMemcpyHostToDevice) != hipSuccess))
-            return (int)HG_ERR_HIP;
+            return (int)HG_HIP_FAIL;
         for (size_t j = 0; j < s.ids.size(); ++j)
             hipLaunchKernelGGL(split_points_kernel, dim3((nsplit + 63) / 64), dim3(64), 0, c->stream,
                                static_cast<const uint8_t*>(c->d_in.p) + s.aoff[j],
@@ -571,7 +571,7 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
     r = fan_out(nwork, [&](uint32_t w) {
         for (uint32_t g = w; g < nrange; g += nwork) {
             hg_ctx* c = ctxs[w];
-            if (set_dev(c) != HG_OK) return (int)HG_ERR_HIP;
+            if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
             int rr = O[g].bytes ? d2h_pipelined(c, h_out + OB[g], c->d_out.p, O[g].bytes) : HG_OK;
             if (rr != HG_OK || !nb || !O[g].n) return rr;
             // block starts inside this slice: global record b * stride

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <mutex>
 #include <new>
 #include <thread>
 #include <vector>
@@ -20,18 +21,58 @@ using namespace hgi;
 
 namespace hgi {
 
-int set_dev(hg_ctx* c) { return hipSetDevice(c->device) == hipSuccess ? HG_OK : HG_ERR_HIP; }
+}  // namespace hgi
+
+// ---- HIP failure sites (hg_err.hpp) ----------------------------------------------
+namespace hgerr {
+static std::mutex g_mu;
+static char g_msg[256];
+
+static void record(const char* file, int line, hipError_t e) {
+    const char* base = strrchr(file, '/');
+    std::lock_guard<std::mutex> lk(g_mu);
+    snprintf(g_msg, sizeof g_msg, "%s:%d: %s (%d)", base ? base + 1 : file, line,
+             hipGetErrorName(e), (int)e);
+}
+
+void note(const char* file, int line) { record(file, line, hipPeekAtLastError()); }
+
+int launch_status(const char* file, int line) {
+    const hipError_t e = hipGetLastError();
+    if (e == hipSuccess) return HG_OK;
+    record(file, line, e);
+    return HG_ERR_HIP;
+}
+}  // namespace hgerr
+
+extern "C" const char* hg_last_hip_error(void) {
+    static thread_local char copy[256];
+    std::lock_guard<std::mutex> lk(hgerr::g_mu);
+    memcpy(copy, hgerr::g_msg, sizeof copy);
+    return copy;
+}
+
+namespace hgi {
+// Every ABI entry starts here: besides selecting the device it drops a stale
+// per-thread launch error left by earlier, unrelated runtime calls (a query
+// that reported "not ready", a failed allocation already returned as
+// HG_ERR_HIP), so the hipGetLastError() after this entry's own launches
+// reports only those launches.
+int set_dev(hg_ctx* c) {
+    (void)hipGetLastError();
+    return hipSetDevice(c->device) == hipSuccess ? HG_OK : HG_HIP_FAIL;
+}
 
 // Grow a device buffer; only ever called outside stream-ordered hot loops
 // (hg_ctx_reserve pre-sizes everything the bench touches).
 int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return HG_OK;
-    if (hipStreamSynchronize(c->stream) != hipSuccess) return HG_ERR_HIP;
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return HG_HIP_FAIL;
     if (b.p) hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
     size_t want = std::max(bytes, (size_t)256);
-    if (hipMalloc(&b.p, want) != hipSuccess) return HG_ERR_HIP;
+    if (hipMalloc(&b.p, want) != hipSuccess) return HG_HIP_FAIL;
     b.bytes = want;
     return HG_OK;
 }
@@ -41,7 +82,7 @@ int ensure_pin(PinBuf& b, size_t bytes) {
     if (b.p) hipHostFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
-    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) return HG_ERR_HIP;
+    if (hipHostMalloc(&b.p, bytes, hipHostMallocDefault) != hipSuccess) return HG_HIP_FAIL;
     b.bytes = bytes;
     return HG_OK;
 }
@@ -63,7 +104,7 @@ extern "C" {
 // blocking device->host copy, for tools/spec_diag.py.
 void* hgk_ctx_workspace(hg_ctx* c) { return c ? c->ws.p : nullptr; }
 int hgk_debug_d2h(void* dst, const void* src, uint64_t n) {
-    return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }
 
 int hg_abi_version(void) { return HG_ABI_VERSION; }
@@ -97,12 +138,12 @@ int hg_ctx_create(int device, hg_ctx** out) {
     c->device = device;
     if (set_dev(c) != HG_OK || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
         delete c;
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     }
     c->stream = c->own;
     if (ensure(c, c->results, 256) != HG_OK || ensure_pin(c->hres, 256) != HG_OK) {
         hg_ctx_destroy(c);
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     }
     *out = c;
     return HG_OK;
@@ -147,12 +188,12 @@ void* hg_ctx_stream(hg_ctx* c) { return c ? reinterpret_cast<void*>(c->stream) :
 
 int hg_ctx_synchronize(hg_ctx* c) {
     if (!c) return HG_ERR_INVALID_ARG;
-    return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_ERR_HIP;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }
 
 int hg_ctx_reserve(hg_ctx* c, uint64_t max_sst_bytes, uint64_t max_pairs) {
     if (!c) return HG_ERR_INVALID_ARG;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     size_t need = std::max(hgk_decode_workspace_bytes(max_sst_bytes),
                            hgk_encode_workspace_bytes(max_pairs));
     int r = ensure(c, c->ws, need);
@@ -169,11 +210,11 @@ int hg_decode_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* 
                         uint64_t cap, hg_decode_result* d_result) {
     if (!c || !d_result || (len && !d_sst) || (cap && !d_spans)) return HG_ERR_INVALID_ARG;
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     if (len == 0)  // empty file: zero records (src/format.rs:54 loop never runs)
         return hipMemsetAsync(d_result, 0, sizeof(hg_decode_result), c->stream) == hipSuccess
                    ? HG_OK
-                   : HG_ERR_HIP;
+                   : HG_HIP_FAIL;
     int r = ensure(c, c->ws, hgk_decode_workspace_bytes(len));
     if (r != HG_OK) return r;
     return hgk_decode_launch(d_sst, len, d_spans, cap, d_result, c->ws.p, c->stream);
@@ -198,7 +239,7 @@ int hg_decode_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* d_span
     if (hipMemcpyAsync(c->hres.p, dres(c), sizeof(hg_decode_result), hipMemcpyDeviceToHost,
                        c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     return finish_decode(*reinterpret_cast<hg_decode_result*>(c->hres.p), cap, n_out, err);
 }
 
@@ -212,12 +253,12 @@ int hg_decode_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* d_span
 // d_results[i].
 static int rt_ensure_aux(hg_ctx* c, int want) {
     if (!c->fork_ev && hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     while (c->naux < want) {
         const int i = c->naux;
         if (hipStreamCreateWithFlags(&c->aux[i], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->join_ev[i], hipEventDisableTiming) != hipSuccess)
-            return HG_ERR_HIP;
+            return HG_HIP_FAIL;
         ++c->naux;
     }
     return HG_OK;
@@ -232,7 +273,7 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
         if ((lens[i] && !d_tables[i]) || (caps[i] && !d_spans[i])) return HG_ERR_INVALID_ARG;
         if (lens[i] >= kMaxLen) return HG_ERR_TOO_LARGE;
     }
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     const char* mode = getenv("HG_DECODE_BATCH");
     if (!(mode && strcmp(mode, "streams") == 0)) {
         if (ntables == 0) return HG_OK;
@@ -248,17 +289,17 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
         if (r == HG_OK) r = ensure(c, c->bstage_d, sb);
         if (r == HG_OK && !c->bstage_ev &&
             hipEventCreateWithFlags(&c->bstage_ev, hipEventDisableTiming) != hipSuccess)
-            r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
         // the previous call's arguments may still be in flight from the pinned stage
         if (r == HG_OK && c->bstage_busy && hipEventSynchronize(c->bstage_ev) != hipSuccess)
-            r = HG_ERR_HIP;
-        if (r == HG_OK && ensure_pin(c->bstage, sb) != HG_OK) r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
+        if (r == HG_OK && ensure_pin(c->bstage, sb) != HG_OK) r = HG_HIP_FAIL;
         if (r == HG_OK)
             r = hgk_decode_launch_multi(ntables, d_tables, lens, d_spans, caps, d_results, c->bws.p,
                                         off, c->bstage.p, c->bstage_d.p, c->stream);
         free(off);
         if (r != HG_OK) return r;
-        if (hipEventRecord(c->bstage_ev, c->stream) != hipSuccess) return HG_ERR_HIP;
+        if (hipEventRecord(c->bstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
         c->bstage_busy = true;
         return HG_OK;
     }
@@ -275,22 +316,22 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
             need = std::max<uint64_t>(need, hgk_decode_workspace_bytes(lens[i]));
         DevBuf& b = c->aux_ws[s];
         if (need > b.bytes) {
-            if (hipStreamSynchronize(c->aux[s]) != hipSuccess) return HG_ERR_HIP;
+            if (hipStreamSynchronize(c->aux[s]) != hipSuccess) return HG_HIP_FAIL;
             if (b.p) hipFree(b.p);
             b.p = nullptr;
             b.bytes = 0;
-            if (hipMalloc(&b.p, need) != hipSuccess) return HG_ERR_HIP;
+            if (hipMalloc(&b.p, need) != hipSuccess) return HG_HIP_FAIL;
             b.bytes = need;
         }
     }
-    if (hipEventRecord(c->fork_ev, c->stream) != hipSuccess) return HG_ERR_HIP;
+    if (hipEventRecord(c->fork_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
     for (int s = 0; s < fan; ++s)
-        if (hipStreamWaitEvent(c->aux[s], c->fork_ev, 0) != hipSuccess) return HG_ERR_HIP;
+        if (hipStreamWaitEvent(c->aux[s], c->fork_ev, 0) != hipSuccess) return HG_HIP_FAIL;
     for (uint32_t i = 0; i < ntables; ++i) {
         const int s = (int)(i % (uint32_t)fan);
         if (lens[i] == 0) {
             if (hipMemsetAsync(d_results + i, 0, sizeof(hg_decode_result), c->aux[s]) != hipSuccess)
-                return HG_ERR_HIP;
+                return HG_HIP_FAIL;
             continue;
         }
         r = hgk_decode_launch(d_tables[i], lens[i], d_spans[i], caps[i], d_results + i,
@@ -300,7 +341,7 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
     for (int s = 0; s < fan; ++s)
         if (hipEventRecord(c->join_ev[s], c->aux[s]) != hipSuccess ||
             hipStreamWaitEvent(c->stream, c->join_ev[s], 0) != hipSuccess)
-            return HG_ERR_HIP;
+            return HG_HIP_FAIL;
     return HG_OK;
 }
 
@@ -362,14 +403,14 @@ static int copy_direct(hg_ctx* c, void* dst, const void* src, size_t bytes, hipM
     for (size_t off = 0; off < bytes; off += kStage)
         if (hipMemcpyAsync(static_cast<char*>(dst) + off, static_cast<const char*>(src) + off,
                            std::min(kStage, bytes - off), kind, c->stream) != hipSuccess)
-            return HG_ERR_HIP;
-    return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_ERR_HIP;
+            return HG_HIP_FAIL;
+    return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }
 
 static int rt_h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
     if (rt_host_pinned(src)) return copy_direct(c, dst, src, bytes, hipMemcpyHostToDevice);
     if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     hipEvent_t ev[2];
     hipEventCreateWithFlags(&ev[0], hipEventDisableTiming);
     hipEventCreateWithFlags(&ev[1], hipEventDisableTiming);
@@ -378,12 +419,12 @@ static int rt_h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes)
     for (size_t off = 0, i = 0; off < bytes; off += kStage, ++i) {
         const size_t n = std::min(kStage, bytes - off);
         const int b = (int)(i & 1);
-        if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
+        if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_HIP_FAIL; break; }
         rt_par_memcpy(c->h_stage[b].p, static_cast<const char*>(src) + off, n);
         if (hipMemcpyAsync(static_cast<char*>(dst) + off, c->h_stage[b].p, n,
                            hipMemcpyHostToDevice, c->stream) != hipSuccess ||
             hipEventRecord(ev[b], c->stream) != hipSuccess) {
-            rc = HG_ERR_HIP;
+            rc = HG_HIP_FAIL;
             break;
         }
         used[b] = true;
@@ -397,7 +438,7 @@ static int rt_h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes)
 static int rt_d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes) {
     if (rt_host_pinned(dst)) return copy_direct(c, dst, src, bytes, hipMemcpyDeviceToHost);
     if (ensure_pin(c->h_stage[0], kStage) != HG_OK || ensure_pin(c->h_stage[1], kStage) != HG_OK)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     hipEvent_t ev[2];
     hipEventCreateWithFlags(&ev[0], hipEventDisableTiming);
     hipEventCreateWithFlags(&ev[1], hipEventDisableTiming);
@@ -409,13 +450,13 @@ static int rt_d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes)
         const size_t n = std::min(kStage, bytes - off);
         const int b = (int)(i & 1);
         if (used[b]) {  // drain the previous use of this buffer
-            if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
+            if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_HIP_FAIL; break; }
             rt_par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
         }
         if (hipMemcpyAsync(c->h_stage[b].p, static_cast<const char*>(src) + off, n,
                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
             hipEventRecord(ev[b], c->stream) != hipSuccess) {
-            rc = HG_ERR_HIP;
+            rc = HG_HIP_FAIL;
             break;
         }
         used[b] = true;
@@ -425,7 +466,7 @@ static int rt_d2h_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes)
     for (int k = 0; k < 2 && rc == HG_OK; ++k) {
         const int b = (int)((i + k) & 1);
         if (!used[b]) continue;
-        if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_ERR_HIP; break; }
+        if (hipEventSynchronize(ev[b]) != hipSuccess) { rc = HG_HIP_FAIL; break; }
         rt_par_memcpy(static_cast<char*>(dst) + pend_off[b], c->h_stage[b].p, pend_n[b]);
         used[b] = false;
     }
@@ -440,7 +481,7 @@ int hg_host_register(const void* h_ptr, uint64_t len) {
     const hipError_t e = hipHostRegister(const_cast<void*>(h_ptr), len, hipHostRegisterDefault);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     }
     return HG_OK;
 }
@@ -450,7 +491,7 @@ int hg_host_unregister(const void* h_ptr) {
     const hipError_t e = hipHostUnregister(const_cast<void*>(h_ptr));
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     }
     return HG_OK;
 }
@@ -477,28 +518,28 @@ static int decode_host_overlapped(hg_ctx* c, const uint8_t* h_sst, uint64_t len,
     hipStream_t up = c->aux[0], down = c->aux[1], cs = c->stream;
     std::vector<hipEvent_t> ev(2 * K, nullptr);
     for (auto& e : ev)
-        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = HG_ERR_HIP;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) r = HG_HIP_FAIL;
     uint8_t* din = static_cast<uint8_t*>(c->d_in.p);
     hg_span* dsp = static_cast<hg_span*>(c->d_out.p);
     for (uint64_t i = 0; r == HG_OK && i < K; ++i) {
         const uint64_t b = i * C, hi = std::min(len, (i + 1) * C + 4096);
         if (hipMemcpyAsync(din + b, h_sst + b, hi - b, hipMemcpyHostToDevice, up) != hipSuccess ||
             hipEventRecord(ev[i], up) != hipSuccess)
-            r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
     }
     uint64_t entry = 0, G = 0, errpos = 0;
     int32_t kind = HG_OK;
     for (uint64_t i = 0; r == HG_OK && i < K; ++i) {
         const uint64_t b = i * C, stop = std::min(len, (i + 1) * C);
         const uint64_t rlen = std::min(len, (i + 1) * C + 4096);
-        if (hipStreamWaitEvent(cs, ev[i], 0) != hipSuccess) { r = HG_ERR_HIP; break; }
+        if (hipStreamWaitEvent(cs, ev[i], 0) != hipSuccess) { r = HG_HIP_FAIL; break; }
         r = hgk_decode_range_launch(din, len, rlen, b, stop, entry, dsp + G, (stop - b) / 16 + 2,
                                     dres(c), c->ws.p, cs);
         if (r != HG_OK) break;
         if (hipMemcpyAsync(c->hres.p, dres(c), sizeof(hg_decode_result), hipMemcpyDeviceToHost,
                            cs) != hipSuccess ||
             hipStreamSynchronize(cs) != hipSuccess) {
-            r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
             break;
         }
         const hg_decode_result res = *static_cast<hg_decode_result*>(c->hres.p);
@@ -507,7 +548,7 @@ static int decode_host_overlapped(hg_ctx* c, const uint8_t* h_sst, uint64_t len,
                       hipStreamWaitEvent(down, ev[K + i], 0) != hipSuccess ||
                       hipMemcpyAsync(h_spans + G, dsp + G, ncopy * sizeof(hg_span),
                                      hipMemcpyDeviceToHost, down) != hipSuccess)) {
-            r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
             break;
         }
         G += res.n_records;
@@ -519,7 +560,7 @@ static int decode_host_overlapped(hg_ctx* c, const uint8_t* h_sst, uint64_t len,
         entry = res.err_offset;  // the exit: the next chunk's entry
     }
     if (hipStreamSynchronize(down) != hipSuccess || hipStreamSynchronize(up) != hipSuccess)
-        r = r == HG_OK ? HG_ERR_HIP : r;
+        r = r == HG_OK ? HG_HIP_FAIL : r;
     for (auto e : ev)
         if (e) (void)hipEventDestroy(e);
     if (r != HG_OK) return r;
@@ -537,7 +578,7 @@ int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spa
                    uint64_t* n_out, hg_err* err) {
     if (!c || (len && !h_sst) || (cap && !h_spans)) return HG_ERR_INVALID_ARG;
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     {
         const char* env = getenv("HG_DEC_CHUNK_MB");
         const uint64_t C = (uint64_t)(env ? std::max(1, atoi(env)) : 128) << 20;
@@ -558,7 +599,7 @@ int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spa
     if (r != HG_OK && r != HG_ERR_CAPACITY && e.kind == HG_OK) return r;  // runtime failure
     const uint64_t ncopy = std::min(n, dcap);
     if (ncopy && rt_d2h_pipelined(c, h_spans, c->d_out.p, ncopy * sizeof(hg_span)) != HG_OK)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     if (n_out) *n_out = n;
     if (err) *err = e;
     if (e.kind != HG_OK) return e.kind;
@@ -573,7 +614,7 @@ int hg_decode_range_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uin
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
     if (stop > len) stop = len;
     if (begin > entry || begin > len || entry > len) return HG_ERR_INVALID_ARG;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     const uint64_t span = stop > begin ? stop - begin : 0;
     int r = ensure(c, c->ws, hgk_decode_workspace_bytes(span ? span : 1));
     if (r != HG_OK) return r;
@@ -590,7 +631,7 @@ int hg_decode_range_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uint64_t 
     if (hipMemcpyAsync(c->hres.p, dres(c), sizeof(hg_decode_result), hipMemcpyDeviceToHost,
                        c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     const hg_decode_result res = *reinterpret_cast<hg_decode_result*>(c->hres.p);
     if (exit) *exit = res.kind == HG_OK ? res.err_offset : 0;
     hg_decode_result rr = res;
@@ -602,7 +643,7 @@ int hg_decode_guess_entry_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uin
                               uint64_t* entry) {
     if (!c || !entry || (len && !d_sst)) return HG_ERR_INVALID_ARG;
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     if (stop >= len) {  // the exit of a range reaching the table's end is its length
         *entry = len;
         return HG_OK;
@@ -616,7 +657,7 @@ int hg_decode_guess_entry_dev(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uin
     if (r != HG_OK) return r;
     if (hipMemcpyAsync(c->hres.p, d_out, 8, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     *entry = *static_cast<uint64_t*>(c->hres.p);
     return HG_OK;
 }
@@ -635,7 +676,7 @@ int hg_encoded_size(hg_ctx* c, const hg_pair* pairs, uint64_t n, uint64_t* bytes
         *bytes = t;
         return HG_OK;
     }
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     int r = ensure(c, c->ws, hgk_encode_workspace_bytes(n));
     if (r != HG_OK) return r;
     r = hgk_encode_size_launch(pairs, n, eres(c), reinterpret_cast<unsigned long long*>(c->ws.p),
@@ -644,7 +685,7 @@ int hg_encoded_size(hg_ctx* c, const hg_pair* pairs, uint64_t n, uint64_t* bytes
     if (hipMemcpyAsync(c->hres.p, eres(c), sizeof(hg_encode_result), hipMemcpyDeviceToHost,
                        c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     *bytes = reinterpret_cast<hg_encode_result*>(c->hres.p)->out_len;
     return HG_OK;
 }
@@ -655,11 +696,11 @@ int hg_encode_dev_async(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pair
                         hg_block* d_blocks, hg_encode_result* d_result) {
     if (!c || !d_result || (n && !d_pairs) || (cap && !d_out)) return HG_ERR_INVALID_ARG;
     if (d_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;  // slice::chunks(0) panics
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     if (n == 0)
         return hipMemsetAsync(d_result, 0, sizeof(hg_encode_result), c->stream) == hipSuccess
                    ? HG_OK
-                   : HG_ERR_HIP;
+                   : HG_HIP_FAIL;
     int r = ensure(c, c->ws, hgk_encode_workspace_bytes(n));
     if (r != HG_OK) return r;
     if (d_blocks && !d_rec_off) {
@@ -679,7 +720,7 @@ int hg_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uin
     if (hipMemcpyAsync(c->hres.p, eres(c), sizeof(hg_encode_result), hipMemcpyDeviceToHost,
                        c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     const hg_encode_result res = *reinterpret_cast<hg_encode_result*>(c->hres.p);
     if (out_len) *out_len = res.out_len;
     return res.kind;
@@ -744,13 +785,13 @@ static int encode_host_overlapped(hg_ctx* c, const uint8_t* h_arena, uint64_t ar
         if (need > up_arena) {
             if (hipMemcpyAsync(din + up_arena, h_arena + up_arena, need - up_arena,
                                hipMemcpyHostToDevice, up) != hipSuccess)
-                r = HG_ERR_HIP;
+                r = HG_HIP_FAIL;
             up_arena = need;
         }
         if (r == HG_OK && hipMemcpyAsync(dpairs + p_lo, h_pairs + p_lo,
                                          (p_hi - p_lo) * sizeof(hg_pair), hipMemcpyHostToDevice,
                                          up) != hipSuccess)
-            r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
         if (r == HG_OK)
             r = hgk_encode_launch_at(darena, dpairs + p_lo, p_hi - p_lo, dout + base, bytes,
                                      want_rec ? drec + p_lo : nullptr, base, 0, nullptr, eres(c),
@@ -761,7 +802,7 @@ static int encode_host_overlapped(hg_ctx* c, const uint8_t* h_arena, uint64_t ar
                            hipStreamWaitEvent(down, ev, 0) != hipSuccess ||
                            hipMemcpyAsync(h_out + base, dout + base, bytes, hipMemcpyDeviceToHost,
                                           down) != hipSuccess))
-            r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
         if (ev) evs.push_back(ev);
         base += bytes;
         p_lo = p_hi;
@@ -770,7 +811,7 @@ static int encode_host_overlapped(hg_ctx* c, const uint8_t* h_arena, uint64_t ar
         r = hgk_encode_blocks_launch(drec, n, block_stride, total, dblk, up);
     const double t_issued = now();
     if (hipStreamSynchronize(up) != hipSuccess || hipStreamSynchronize(down) != hipSuccess)
-        r = r == HG_OK ? HG_ERR_HIP : r;
+        r = r == HG_OK ? HG_HIP_FAIL : r;
     if (tm)
         fprintf(stderr, "[hg] encode_host_overlapped: issue %.2f ms, wait %.2f ms, %zu chunks\n",
                 t_issued - t_start, now() - t_issued, evs.size());
@@ -786,7 +827,7 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
     if (!c || (n && !h_pairs) || (arena_len && !h_arena) || (cap && !h_out))
         return HG_ERR_INVALID_ARG;
     if (h_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     uint64_t total = 0;
     for (uint64_t i = 0; i < n; ++i) total += 16ull + h_pairs[i].klen + h_pairs[i].vlen;
     if (out_len) *out_len = total;
@@ -831,17 +872,17 @@ int hg_merge_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint
                        hg_merge_result* d_result) {
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     if (!c->mstage_ev && hipEventCreateWithFlags(&c->mstage_ev, hipEventDisableTiming) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     if (ntables == 0) {  // min_by_key over no candidates: the reference panics (:213)
         hg_merge_result r{0, HG_ERR_EMPTY_MERGE, 0, 0};
-        if (ensure_pin(c->mstage, 4096) != HG_OK) return HG_ERR_HIP;
-        if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_ERR_HIP;
+        if (ensure_pin(c->mstage, 4096) != HG_OK) return HG_HIP_FAIL;
+        if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_HIP_FAIL;
         memcpy(c->mstage.p, &r, sizeof r);
         if (hipMemcpyAsync(d_result, c->mstage.p, sizeof r, hipMemcpyHostToDevice, c->stream) !=
             hipSuccess)
-            return HG_ERR_HIP;
+            return HG_HIP_FAIL;
     } else {
         uint64_t n = 0;
         for (uint32_t t = 0; t < ntables; ++t) {
@@ -852,14 +893,14 @@ int hg_merge_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint
                                       hgk_merge_staging_bytes(ntables) + 4096);
         if (r != HG_OK) return r;
         // the previous call's argument copy must have left the pinned staging
-        if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_ERR_HIP;
+        if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_HIP_FAIL;
         if (ensure_pin(c->mstage, hgk_merge_staging_bytes(ntables) + 4096) != HG_OK)
-            return HG_ERR_HIP;
+            return HG_HIP_FAIL;
         r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
                              d_result, c->mws.p, c->mstage.p, c->stream);
         if (r != HG_OK) return r;
     }
-    if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_ERR_HIP;
+    if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
     c->mstage_busy = true;
     return HG_OK;
 }
@@ -868,7 +909,7 @@ int hg_merge_dev(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t a
                  const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
                  hg_pair* d_out, uint64_t cap, hg_merge_result* result) {
     if (!c) return HG_ERR_INVALID_ARG;
-    if (ensure(c, c->mres, 64) != HG_OK) return HG_ERR_HIP;
+    if (ensure(c, c->mres, 64) != HG_OK) return HG_HIP_FAIL;
     hg_merge_result* dres_m = static_cast<hg_merge_result*>(c->mres.p);
     int r = hg_merge_dev_async(c, ntables, d_arena, arena_len, table_off, d_spans, counts, d_out,
                                cap, dres_m);
@@ -876,7 +917,7 @@ int hg_merge_dev(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t a
     if (hipMemcpyAsync(c->hres.p, dres_m, sizeof(hg_merge_result), hipMemcpyDeviceToHost,
                        c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
-        return HG_ERR_HIP;
+        return HG_HIP_FAIL;
     const hg_merge_result res = *static_cast<hg_merge_result*>(c->hres.p);
     if (result) *result = res;
     if (res.kind != HG_OK) return res.kind;
@@ -888,7 +929,7 @@ int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
                     uint32_t block_stride, hg_block* h_blocks, hg_merge_result* result) {
     if (!c || (ntables && (!h_tables || !lens)) || (cap && !h_out)) return HG_ERR_INVALID_ARG;
     if (h_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     hg_merge_result res{0, HG_OK, 0, 0};
     if (out_len) *out_len = 0;
     // 1. all tables into one device arena (8-byte aligned starts), spans per table
@@ -935,7 +976,7 @@ int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
             (hipMemcpyAsync(hr, dr, ntables * sizeof(hg_decode_result), hipMemcpyDeviceToHost,
                             c->stream) != hipSuccess ||
              hipStreamSynchronize(c->stream) != hipSuccess))
-            r = HG_ERR_HIP;
+            r = HG_HIP_FAIL;
         for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
             if (hr[t].kind != HG_OK) {  // the reference's read_all unwrap (storage.rs:64-66)
                 res = hg_merge_result{0, hr[t].kind, t, hr[t].err_offset};
@@ -1001,7 +1042,7 @@ uint64_t hg_keyindex_bytes(uint64_t n) { return hgk_keyindex_bytes(n); }
 int hg_keyindex_build_dev_async(hg_ctx* c, const uint8_t* d_table, uint64_t len,
                                 const hg_span* d_spans, uint64_t n, void* d_index) {
     if (!c || (n && (!d_table || !d_spans || !d_index))) return HG_ERR_INVALID_ARG;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     return hgk_keyindex_launch(d_table, len, d_spans, n, d_index, c->stream);
 }
 
@@ -1010,7 +1051,7 @@ int hg_lookup_dev_async(hg_ctx* c, const uint8_t* d_table, const hg_span* d_span
                         const hg_key* d_queries, uint64_t nq, hg_lookup_result* d_results) {
     if (!c || (nq && (!d_queries || !d_results)) || (n && nq && (!d_table || !d_spans || !d_index)))
         return HG_ERR_INVALID_ARG;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     return hgk_lookup_launch(d_table, d_spans, d_index, n, d_keys, d_queries, nq, d_results,
                              c->stream);
 }
@@ -1021,7 +1062,7 @@ int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, const uint8_
     if (!c || (len && !h_table) || (nq && (!h_queries || !h_results)) || (keys_len && !h_keys))
         return HG_ERR_INVALID_ARG;
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
-    if (set_dev(c) != HG_OK) return HG_ERR_HIP;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     for (uint64_t i = 0; i < nq; ++i)
         if (h_queries[i].off + h_queries[i].len > keys_len) return HG_ERR_INVALID_ARG;
     const uint64_t cap = len / 16;

@@ -147,6 +147,10 @@ typedef struct hg_ctx hg_ctx;
 /* ---- library / context ---------------------------------------------- */
 int hg_abi_version(void);
 const char* hg_status_string(int status);
+/* Where the most recent HG_ERR_HIP in this process came from:
+ * "file:line: hipErrorName (code)", or "" if none yet.  Diagnostics only
+ * (a HIP failure has no counterpart in the reference, which runs on the CPU). */
+const char* hg_last_hip_error(void);
 
 /* Create a context bound to HIP device `device` with its own stream. */
 int hg_ctx_create(int device, hg_ctx** out);
