@@ -111,6 +111,7 @@ struct DecodeArgs {
     uint32_t hz;                 // zero high bytes required in klen/vlen
     uint32_t bp;                 // pieces per batch (BATCH_MIN..BATCH)
     uint32_t* diag;              // DIAG builds only: DIAG_WORDS per batch
+    uint32_t* sdiag;             // diagnostics: LW_PROF words per pre-pass batch (or null)
     // Stride pre-pass results (decode_spec_kernel): batches of SPEC_BP
     // pieces [0, first_bad) are resolved; decode_kernel writes their spans.
     struct SpecBatch* sbatch;
@@ -157,7 +158,8 @@ struct SpecPiece {                // one per piece of an ok pre-pass batch
 };
 enum : uint32_t { SP_STRIDE = 0, SP_HOP = 1 };
 // SpecBatch.pad (diagnostics, tools/spec_diag.py): how the pre-pass batch went
-enum : uint32_t { SB_STRIDE = 1, SB_STRIDE_BROKE = 2, SB_HOP_SMALL = 3, SB_HOP_DEAD = 4, SB_HOP = 5 };
+enum : uint32_t { SB_STRIDE = 1, SB_STRIDE_BROKE = 2, SB_HOP_SMALL = 3, SB_HOP_DEAD = 4, SB_HOP = 5,
+                  SB_LW = 6, SB_LW_DEAD = 7 };
 
 // Diagnostic record per batch (tools/decode_diag.py).
 constexpr uint32_t DIAG_WORDS = 24;
@@ -1608,6 +1610,20 @@ struct SpecSmem {
     uint32_t hok;
     uint64_t hx, ht;          // batch exit and records after stitching
     uint32_t hcode;           // SpecBatch.pad: how the batch went (SB_*)
+    // lane-walk mode (lw_piece): per-wave exit maxima / change flags / record
+    // counts of the last two relaxation rounds, lane guesses, the entry guess
+    uint64_t lw_wx[2][NW];    // per wave: entry used, exit, records, unresolved (two rounds)
+    uint64_t lw_wexit[2][NW];
+    uint32_t lw_wcnt[2][NW];
+    uint32_t lw_wbad[2][NW];
+    uint32_t lw_cnt[NW];
+    uint32_t lw_sg[THREADS];
+    uint8_t lw_tg[THREADS];
+    uint16_t lw_zm[NGRAN + 8];  // 16-bit zero mask per granule of the staged piece (+ halo)
+    unsigned long long lw_best, best_any;
+    uint32_t lw_nser;         // serial fallbacks of the batch (SpecBatch.pad >> 32, diagnostics)
+    uint32_t lw_prof[8];      // diagnostics (a.sdiag): cycles per lane-walk phase, see LW_STAMP
+    uint64_t lw_last;
 };
 
 __device__ __forceinline__ bool rec_ok(uint64_t q, uint64_t len, uint64_t kl, uint64_t vl) {
@@ -1842,6 +1858,569 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
     return true;
 }
 
+// ---- lane-walk mode (small and medium records) ----------------------------------
+// A pre-pass batch whose records are too small to hop (hop_batch: more than
+// HOP_MAX_CAND candidate run ends in piece 0) is resolved here, piece by piece
+// from the batch's entry, each piece staged in LDS as in the stride path (the
+// next piece's loads in flight meanwhile).  A piece with entry X:
+//   - every lane owns 64 bytes; the lane holding X starts there, every later
+//     lane guesses its first record start: the first candidate that ENDS a
+//     run of zero-mask candidates (a short header also passes the filter 1-3
+//     bytes to its left), reads as a record shorter than HG_FAR_CAND that fits
+//     the file and whose next header (if inside the piece) is readable; then it
+//     walks <= 4 records to its segment end;
+//   - relaxation: a lane's entry is the largest exit of the lanes before it
+//     (block max-scan: wave scans + one word per wave), a segment that entry
+//     jumps over is passed through, a lane entered off its guess walks again;
+//     rounds repeat until no exit changes -- that fixed point is exact from X
+//     by induction over the lanes;
+//   - spans go to the piece's scratch slot (decode_kernel copies them, as for
+//     hop segments), the count and exit to the piece record.
+// Any unreadable record on the exact path, or no convergence, leaves the batch
+// to decode_kernel's engine, which reports errors exactly.
+constexpr uint32_t LW_WROUNDS = 64;   // wave-local relaxation rounds before the serial fallback
+constexpr uint32_t LW_WSPAN = 64 * SEG;  // bytes per wave
+constexpr uint32_t LW_LEAD = 1024;     // lead-in bytes walked before a batch's first piece
+constexpr uint32_t LW_TRIES = 3;       // candidates a lane examines for its guess
+constexpr uint32_t LW_PROF = 8;
+// Diagnostics (a.sdiag != null, tools/lw_diag.py): thread 0 charges the cycles
+// since the last stamp to phase k (0 staging, 1 masks + guesses + walks,
+// 2 chain marks, 3 relaxation rounds, 4 count scan, 5 span stores, 6 lead-in
+// probe, 7 rounds run).
+#define LW_STAMP(k)                                                   \
+    do {                                                              \
+        if (a.sdiag && threadIdx.x == 0) {                            \
+            const uint64_t now_ = __builtin_amdgcn_s_memtime();       \
+            s.lw_prof[k] += (uint32_t)(now_ - s.lw_last);             \
+            s.lw_last = now_;                                         \
+        }                                                             \
+    } while (0)
+
+// Workgroup barrier for LDS only: waits this wave's LDS operations, not its
+// vector memory ones, so a global->LDS prefetch of the next piece stays in
+// flight across it (__syncthreads() would drain it with vmcnt(0)).
+__device__ __forceinline__ void lw_bar() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+__device__ __forceinline__ void lw_wait_vm() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Global -> LDS DMA of the whole piece at base (base + PIECE <= rlen): one
+// 16-byte global_load_lds per thread and granule column; each wave
+// instruction fills 1 KiB of dst contiguously (lane-linear).  No registers
+// hold the bytes, so the lane walks of the current piece keep their VGPRs.
+__device__ __forceinline__ void lw_dma_piece(const DecodeArgs& a, uint64_t base, uint8_t* dst) {
+    const uint32_t tid = threadIdx.x, wid = tid >> 6;
+#pragma unroll
+    for (uint32_t q = 0; q < GPT; ++q) {
+        const uint32_t g0 = q * THREADS + wid * 64;  // the wave's first granule
+        __builtin_amdgcn_global_load_lds(
+            static_cast<const void*>(a.sst + base + (uint64_t)(g0 + (tid & 63u)) * 16),
+            (__attribute__((address_space(3))) void*)(dst + g0 * 16), 16, 0, 0);
+    }
+}
+
+// Plain staging of [base, base + PIECE) + halo (zero past rlen) into dst.
+__device__ __forceinline__ void lw_plain_stage(const DecodeArgs& a, uint64_t base, uint8_t* dst) {
+    const uint32_t tid = threadIdx.x;
+#pragma unroll 1
+    for (uint32_t q = 0; q < GPT; ++q)  // rolled: few registers
+        *reinterpret_cast<uint4*>(dst + (q * THREADS + tid) * 16) =
+            load16(a, base + (q * THREADS + tid) * 16);
+    if (tid < 4)
+        *reinterpret_cast<uint4*>(dst + PIECE + tid * 16) =
+            tid == 0 ? load16(a, base + PIECE) : make_uint4(0, 0, 0, 0);
+}
+
+// This lane's guess in [seg0, segend) (piece-relative) or NO_GUESS; cm0 / the
+// next lane's first candidate bit as in lean_prepare.
+__device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, uint32_t seg0, uint32_t segend,
+                                             uint32_t clen, uint64_t rem, uint32_t hz,
+                                             uint64_t cm0, uint64_t nextbit) {
+    const uint64_t runend = cm0 & ~((cm0 >> 1) | (nextbit << 63));
+    uint64_t cm = runend;
+    uint32_t tries = 0;  // a lane left without a guess is entered by the relaxation
+#pragma nounroll
+    for (uint32_t pass = 0; pass < 2; ++pass) {
+        if (pass) cm = cm0 & ~runend;
+        while (cm && tries++ < LW_TRIES) {
+            const uint32_t p = seg0 + (uint32_t)(__ffsll((long long)cm) - 1);
+            cm &= cm - 1;
+            uint32_t k0, k1, v0, v1;
+            lds_header32(data, p, k0, k1, v0, v1);
+            const uint64_t body = (uint64_t)k0 + v0;
+            if ((k1 | v1) || body >= HG_FAR_CAND || body > rem - p - 16) continue;
+            const uint64_t nx = (uint64_t)p + 16 + body;
+            if (nx < clen) {  // look-ahead: the next header must be a readable record
+                if (nx + 16 > rem) continue;
+                lds_header32(data, (uint32_t)nx, k0, k1, v0, v1);
+                if ((k1 | v1) || (uint64_t)k0 + v0 > rem - nx - 16) continue;
+            }
+            return p;
+        }
+    }
+    (void)segend;
+    return NO_GUESS;
+}
+
+// Zero masks of the staged piece: one 16-bit mask per 16-byte granule (plus
+// the halo and the zero slack after it) in s.lw_zm, from registers while
+// staging (lw_stage) or from LDS.
+__device__ __forceinline__ void lw_zm_from_lds(SpecSmem& s, const uint8_t* data) {
+#pragma unroll
+    for (uint32_t q = 0; q < GPT; ++q) {
+        const uint32_t gi = q * THREADS + threadIdx.x;
+        s.lw_zm[gi] = (uint16_t)zmask16(*reinterpret_cast<const uint4*>(data + gi * 16));
+    }
+    if (threadIdx.x < 4)
+        s.lw_zm[NGRAN + threadIdx.x] =
+            (uint16_t)zmask16(*reinterpret_cast<const uint4*>(data + PIECE + threadIdx.x * 16));
+}
+
+// Candidate mask of this lane's segment and the next lane's first bit, from
+// the granule masks (one aligned 8-byte LDS read + one 2-byte read): bit j of
+// the 80 zero-mask bits z1:z0 <=> byte j is zero, candidate j <=> bytes
+// [j+8-hz, j+8) and [j+16-hz, j+16) are zero.
+__device__ __forceinline__ void lw_masks(const SpecSmem& s, uint32_t seg0, uint32_t clen,
+                                         uint64_t rem, uint32_t hz, uint64_t& cm0,
+                                         uint64_t& nextbit) {
+    cm0 = 0;
+    nextbit = 0;
+    if (seg0 >= clen || rem < 16) return;
+    const uint32_t gi = seg0 / 16;
+    const uint64_t z0 = *reinterpret_cast<const uint64_t*>(&s.lw_zm[gi]);
+    const uint32_t z1 = s.lw_zm[gi + 4];
+    uint64_t c = 0, c64 = 0;
+    if (hz == 0) {
+        c = ~0ull;
+        c64 = 1;
+    } else {  // 80-bit shifts as 64 + 16 bits (a switch over templated HZ spilled registers)
+        const uint32_t hi = z1 & 0xFFFFu;
+        uint64_t alo = z0;
+        uint32_t ahi = hi;
+        for (uint32_t k = 1; k < hz; ++k) {  // bit i of A: bytes i .. i+hz-1 are zero
+            alo &= (z0 >> k) | ((uint64_t)hi << (64 - k));
+            ahi &= hi >> k;
+        }
+        const uint32_t s1 = 8 - hz, s2 = 16 - hz;  // s1 in [0, 7], s2 in [8, 15]
+        const uint64_t a1 = s1 ? ((alo >> s1) | ((uint64_t)ahi << (64 - s1))) : alo;
+        const uint64_t a2 = (alo >> s2) | ((uint64_t)ahi << (64 - s2));
+        c = a1 & a2;
+        c64 = ((ahi >> s1) & (ahi >> s2)) & 1u;
+    }
+    const uint32_t n = min(seg0 + SEG, clen) - seg0;  // positions where records may start
+    if (n < 64) c &= (1ull << n) - 1ull;
+    const uint64_t plim = rem - 16;  // last readable header position
+    if (plim < seg0) {
+        c = 0;
+    } else if (plim - seg0 < 63) {
+        c &= (2ull << (plim - seg0)) - 1ull;
+    }
+    const uint32_t q = seg0 + SEG;
+    nextbit = (q < clen && (uint64_t)q <= plim) ? c64 : 0ull;
+    cm0 = c;
+}
+
+// Entry guess of the staged bytes at base (clen bytes where records may
+// start) when nothing is known: the first lane guess whose walk exits exactly
+// on another lane's guess, else the first lane guess; ~0 if no lane has one.
+// All threads.
+__device__ __forceinline__ uint64_t lw_entry_guess(SpecSmem& s, const DecodeArgs& a,
+                                                   const uint8_t* data, uint64_t base, uint32_t clen) {
+    const uint32_t tid = threadIdx.x;
+    const uint64_t rem = a.len - base;
+    const uint32_t seg0 = tid * SEG, segend = min(seg0 + SEG, clen);
+    uint64_t cm0, nb;
+    lw_masks(s, seg0, clen, rem, a.hz, cm0, nb);
+    uint32_t g = NO_GUESS;
+    Walk w;
+    w.dead = true;
+    w.exit = 0;
+    if (seg0 < clen) g = lw_guess(data, seg0, segend, clen, rem, a.hz, cm0, nb);
+    if (g != NO_GUESS) lane_walk(data, base, a.len, g, segend, w);
+    const bool valid = g != NO_GUESS && !w.dead;
+    s.lw_sg[tid] = valid ? g : NO_GUESS;
+    if (tid == 0) {
+        s.lw_best = ~0ull;
+        s.best_any = ~0ull;
+    }
+    lw_bar();
+    bool linked = false;
+    if (valid && w.exit < base + clen) {
+        const uint32_t u = (uint32_t)(w.exit - base);
+        linked = s.lw_sg[u / SEG] == u;
+    }
+    if (linked) atomicMin(&s.lw_best, (unsigned long long)(base + g));
+    if (valid) atomicMin(&s.best_any, (unsigned long long)(base + g));
+    lw_bar();
+    const uint64_t b1 = uni((uint64_t)s.lw_best), b2 = uni((uint64_t)s.best_any);
+    lw_bar();
+    return b1 != ~0ull ? b1 : b2;
+}
+
+// Exact serial walk of the staged bytes from X by thread 0 (the relaxation
+// did not converge: rare, e.g. a wrong guess that links and pushes a long run
+// of lanes past their entries).  Emits to out, or (out == nullptr) finds the
+// first start >= cut.  False if a record on the path cannot be read.
+__device__ __forceinline__ bool lw_serial(SpecSmem& s, const DecodeArgs& a, const uint8_t* data,
+                                          uint64_t base, uint32_t clen, uint64_t X, hg_span* out,
+                                          uint64_t cut, uint32_t& count, uint64_t& exit) {
+    if (threadIdx.x == 0) {
+        ++s.lw_nser;
+        uint32_t n = 0;
+        uint64_t cur = X, first = ~0ull;
+        bool ok = true;
+        while (cur < base + clen) {
+            if (cur + 16 > a.len) {
+                ok = false;
+                break;
+            }
+            uint32_t k0, k1, v0, v1;
+            lds_header32(data, (uint32_t)(cur - base), k0, k1, v0, v1);
+            const uint64_t body = (uint64_t)k0 + v0;
+            if ((k1 | v1) || body > a.len - cur - 16) {
+                ok = false;
+                break;
+            }
+            if (out) write_span(out, n, cur, k0, v0);
+            if (cur >= cut && first == ~0ull) first = cur;
+            ++n;
+            cur += 16 + body;
+        }
+        if (!out && first == ~0ull) first = cur;  // the first start at or after the window
+        s.lw_cnt[0] = n;
+        s.lw_best = ok ? (out ? cur : first) : ~0ull;
+    }
+    lw_bar();
+    count = uni(s.lw_cnt[0]);
+    exit = uni((uint64_t)s.lw_best);
+    lw_bar();
+    return exit != ~0ull;
+}
+
+// The staged bytes at base (records start in [base, base + clen)) entered at
+// X (exact, absolute): spans to out[0, count) (absolute offsets), count and
+// exit.  With out == nullptr (probe) exit is instead the first record start
+// >= cut on that path.  False if the exact path cannot be resolved here.  All
+// threads; returns a block-uniform value.
+//
+// Relaxation is wave-local (DPP scans, no barriers): each wave covers 4 KiB;
+// the wave holding X starts there, every later wave speculates that it is
+// entered at its first lane guess.  One barrier publishes each wave's
+// (entry, exit, count); the waves are stitched in order, and a wave whose
+// speculated entry is not its predecessor's exit relaxes again from that exit
+// (rare: a record start that no lane guessed), behind one more barrier.
+__device__ __forceinline__ bool lw_piece(SpecSmem& s, const DecodeArgs& a, const uint8_t* data,
+                                         uint64_t base, uint32_t clen, uint64_t X, hg_span* out,
+                                         uint32_t& count, uint64_t& exit, uint64_t cut = 0) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint64_t rem = a.len - base;
+    if (X >= base + clen) {  // a record spans the whole piece
+        count = 0;
+        exit = X;
+        return true;
+    }
+    const uint32_t seg0 = tid * SEG, segend = min(seg0 + SEG, clen);
+    const uint32_t xr = (uint32_t)(X - base);
+    const uint32_t je = xr / SEG, wje = je >> 6;
+    const uint32_t wq0 = wid * LW_WSPAN;
+    const uint32_t wq1 = min(wq0 + LW_WSPAN, clen);
+    const bool in_piece = seg0 < clen && tid >= je;
+    uint64_t cm0, nb;
+    lw_masks(s, seg0, clen, rem, a.hz, cm0, nb);
+    uint32_t g = NO_GUESS;
+    Walk w;
+    w.dead = true;
+    w.exit = 0;
+    w.cnt = 0;
+    w.p01 = w.p23 = 0;
+    if (tid == je) g = xr;
+    else if (in_piece) g = lw_guess(data, seg0, segend, clen, rem, a.hz, cm0, nb);
+    if (in_piece && g != NO_GUESS) lane_walk(data, base, a.len, g, segend, w);
+    LW_STAMP(1);
+    auto rel = [&](uint64_t e) -> uint32_t {
+        const uint64_t d = e - base;
+        return d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
+    };
+    // Chain lanes (wave-local): a lane whose guess another lane's walk in the
+    // same wave exits on.  Only they (and the entry lane) seed the first
+    // round, so a wrong guess in a segment without a record start cannot push
+    // the lanes after it past their true entries.
+    const bool valid0 = in_piece && g != NO_GUESS && !w.dead;
+    s.lw_sg[tid] = valid0 ? g : NO_GUESS;
+    s.lw_tg[tid] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (valid0) {
+        const uint32_t u = rel(w.exit);
+        if (u >= wq0 && u < wq1 && s.lw_sg[u / SEG] == u) s.lw_tg[u / SEG] = 1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const bool chain = s.lw_tg[tid] != 0;
+    // this wave's entry: lane jl (64 = none walks) at piece-relative xw
+    // (absolute xa; ~0: no guess in the wave)
+    uint32_t jl = 64, xw = 0xFFFFFFFFu;
+    uint64_t xa = ~0ull;
+    if (wq0 < clen && wid >= wje) {
+        if (wid == wje) {
+            jl = je & 63u;
+            xw = xr;
+            xa = X;
+        } else {
+            const unsigned long long vb = __ballot(valid0);
+            if (vb) {
+                jl = (uint32_t)__ffsll((long long)vb) - 1;
+                xw = __shfl(g, (int)jl, 64);
+                xa = base + xw;
+            }
+        }
+    }
+    uint32_t st = 3;  // 0 walking from g, 1 passed through, 2 waiting, 3 not in this wave's path
+    uint32_t c = 0;
+    bool ok_all = true, redo = true, wbad = false;
+    uint32_t fin = 0, wcnt = 0;
+    uint64_t xfin = X, wexit = 0;
+    for (uint32_t att = 0;; ++att) {
+        // ---- wave-local relaxation from (jl, xw): the first time, and again
+        // for a wave whose speculated entry was wrong ----
+        if (redo && jl < 64) {
+            wbad = false;
+            const bool act = in_piece && lane >= jl;
+            uint32_t ev = (act && g != NO_GUESS && !w.dead && (lane == jl || chain)) ? rel(w.exit) : 0u;
+            if (lane == jl && g != xw) ev = 0;
+            st = act ? 0u : 3u;
+            bool conv = false;
+            for (uint32_t r = 0; r < LW_WROUNDS; ++r) {
+                if (a.sdiag && tid == 0) ++s.lw_prof[7];
+                const uint32_t m = dpp_max_incl(ev);
+                uint32_t excl = __shfl_up(m, 1, 64);
+                if (lane == 0) excl = 0;
+                const uint32_t seed = lane == jl ? xw : excl;
+                uint32_t nev = ev;
+                if (act) {
+                    if (lane != jl && seed >= segend) {  // jumped over by a record / the exit
+                        st = 1;
+                        nev = 0;
+                    } else if (lane != jl && seed < seg0) {  // not resolved yet: keep the exit
+                        st = 2;
+                    } else {
+                        if (st != 0 || g == NO_GUESS || seed != g) {
+                            g = seed;
+                            lane_walk(data, base, a.len, g, segend, w);
+                        }
+                        st = 0;
+                        nev = w.dead ? 0u : rel(w.exit);
+                    }
+                }
+                const bool changed = nev != ev;
+                ev = nev;
+                if (!__ballot(changed)) {
+                    conv = true;
+                    break;
+                }
+            }
+            const bool walking = act && st == 0;
+            wbad = __ballot(act && (st == 2 || (st == 0 && w.dead)) ) != 0 || !conv;
+            c = walking ? w.cnt : 0u;
+            const unsigned long long wm = __ballot(walking);
+            const uint32_t ll = wm ? 63u - (uint32_t)__clzll((long long)wm) : 0u;
+            const uint64_t le = w.exit;
+            wexit = wm ? (((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(le >> 32), ll) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)le, ll))
+                       : xa;
+            wcnt = __builtin_amdgcn_readlane((int)dpp_sum_incl(c), 63);
+        } else if (redo) {
+            st = 3;
+            c = 0;
+            wcnt = 0;
+            wbad = false;
+            wexit = xa;  // pass-through wave (entry past it) or no speculation (~0)
+        }
+        redo = false;
+        LW_STAMP(3);
+        fin = att & 1u;
+        if (lane == 0) {
+            s.lw_wx[fin][wid] = xa;
+            s.lw_wexit[fin][wid] = wexit;
+            s.lw_wcnt[fin][wid] = wcnt;
+            s.lw_wbad[fin][wid] = wbad ? 1u : 0u;
+        }
+        lw_bar();
+        // ---- stitch the waves in order (uniform in every wave) ----
+        uint64_t x = X;
+        uint32_t fix = NW;
+        for (uint32_t v = wje; v < NW; ++v) {
+            if (v * LW_WSPAN >= clen) break;
+            if (s.lw_wx[fin][v] != x || s.lw_wbad[fin][v]) {
+                fix = v;
+                break;
+            }
+            x = s.lw_wexit[fin][v];
+        }
+        if (fix == NW) {
+            xfin = x;
+            break;
+        }
+        if (att == NW || s.lw_wx[fin][fix] == x) {  // entered exactly and still unresolved
+            ok_all = false;
+            break;
+        }
+        if (wid == fix) {  // relax again from the exact entry
+            const uint64_t xe = x - base;
+            xa = x;
+            xw = xe < 0xFFFFFFFFull ? (uint32_t)xe : 0xFFFFFFFFu;
+            jl = xw >= wq1 ? 64u : (xw / SEG) - wid * 64u;
+            redo = true;
+        }
+    }
+    LW_STAMP(2);
+    if (!ok_all) {
+        lw_bar();
+        return lw_serial(s, a, data, base, clen, X, out, cut, count, exit);
+    }
+    uint32_t pre = dpp_sum_incl(c) - c, tot = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < NW; ++q) {
+        const bool live = q >= wje && q * LW_WSPAN < clen;
+        const uint32_t wc = live ? s.lw_wcnt[fin][q] : 0u;
+        pre += q < wid ? wc : 0u;
+        tot += wc;
+    }
+    count = tot;
+    exit = xfin;
+    LW_STAMP(4);
+    if (out) {
+        for (uint32_t i = 0; i < c; ++i) store_span(out, ~0ull, pre + i, data, base, walk_pos(w, i));
+        LW_STAMP(5);
+        return true;
+    }
+    // probe: the first start >= cut (or the exit if none lies in the window)
+    if (tid == 0) s.lw_best = ~0ull;
+    lw_bar();
+    for (uint32_t i = 0; i < c; ++i) {
+        const uint64_t q = base + walk_pos(w, i);
+        if (q >= cut) {
+            atomicMin(&s.lw_best, (unsigned long long)q);
+            break;
+        }
+    }
+    lw_bar();
+    const uint64_t f = uni((uint64_t)s.lw_best);
+    lw_bar();
+    exit = f != ~0ull ? f : xfin;
+    return true;
+}
+
+// Stage piece i of the batch (held in v) into LDS with its halo.
+__device__ __forceinline__ void spec_stage(SpecSmem& s, const uint4 (&v)[GPT], uint32_t i) {
+    uint8_t* data = reinterpret_cast<uint8_t*>(s.data64);
+#pragma unroll
+    for (uint32_t q = 0; q < GPT; ++q)
+        *reinterpret_cast<uint4*>(data + (q * THREADS + threadIdx.x) * 16) = v[q];
+    if (threadIdx.x < 4)  // thread 0 reads back its own halo write when i == 0
+        *reinterpret_cast<uint4*>(data + PIECE + threadIdx.x * 16) =
+            threadIdx.x == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
+}
+
+// The lane-walk batch [p0, p0 + np): piece 0 is staged, v holds piece 1's
+// loads.  On success fills sp[] (SP_HOP pieces: entry, count; spans in the
+// piece's scratch slot) and returns true with X0 = entry, X = exit, total.
+// All threads call it.
+__device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const DecodeArgs& a,
+                                         uint32_t p0, uint32_t np, SpecPiece* sp, uint4 (&v)[GPT],
+                                         uint64_t& X0, uint64_t& X, uint64_t& total) {
+    const uint32_t tid = threadIdx.x;
+    const uint64_t base0 = (uint64_t)p0 * PIECE;
+    uint8_t* const buf0 = reinterpret_cast<uint8_t*>(s.data64);
+    uint8_t* const buf1 = reinterpret_cast<uint8_t*>(alt);
+    if (tid == 0) {
+        s.lw_nser = 0;
+        for (uint32_t k = 0; k < LW_PROF; ++k) s.lw_prof[k] = 0;
+        s.lw_last = __builtin_amdgcn_s_memtime();
+    }
+    // piece 1's loads are in v (the caller put them in flight): into buf1
+    if (np > 1) {
+#pragma unroll
+        for (uint32_t q = 0; q < GPT; ++q)
+            *reinterpret_cast<uint4*>(buf1 + (q * THREADS + tid) * 16) = v[q];
+        if (tid < 4)
+            *reinterpret_cast<uint4*>(buf1 + PIECE + tid * 16) =
+                tid == 0 ? s.halo[1] : make_uint4(0, 0, 0, 0);
+    }
+    __syncthreads();
+    uint64_t x = a.entry;
+    total = 0;
+    bool ok = true;
+    // Piece i lives in buf(i & 1); piece i + 1 is DMA'd into the other buffer
+    // while piece i is walked.  Step -1 (batches after the first) is the entry
+    // guess through a lead-in: the window [base0 - LW_LEAD, +PIECE) is staged
+    // in buf0 (L2-warm bytes), a guess in it is walked exactly to the first
+    // start >= base0 -- a wrong lead-in guess has re-joined the true path by
+    // then almost always, where a guess made at base0 itself is wrong about
+    // once per thousand batches (each costs the batch its pre-pass).  Piece 0
+    // is then staged again.  One call site of lw_piece for both uses.
+    for (int i = p0 > 0 ? -1 : 0; i < (int)np; ++i) {
+        const uint64_t base = i < 0 ? base0 - LW_LEAD : (uint64_t)(p0 + i) * PIECE;
+        uint8_t* const cur = (i > 0 && (i & 1)) ? buf1 : buf0;  // the window (i = -1): buf0
+        if (i < 0 || (i == 0 && p0 > 0)) {  // window / piece 0 again (L2-warm), plain loads
+            lw_bar();
+            lw_plain_stage(a, base, cur);
+        } else if (i >= 2) {  // DMA'd during piece i - 1 (the table's last piece: plain)
+            lw_wait_vm();
+            if (base + PIECE > a.rlen) lw_plain_stage(a, base, cur);
+        }
+        lw_bar();  // staged bytes visible
+        lw_zm_from_lds(s, cur);
+        if (i >= 1 && (uint32_t)i + 1 < np) {  // piece i + 1 into the other buffer
+            const uint64_t nbase = base + PIECE;
+            uint8_t* const nxt = (i & 1) ? buf0 : buf1;
+            if (nbase + PIECE <= a.rlen) lw_dma_piece(a, nbase, nxt);
+            if (tid < 4)
+                *reinterpret_cast<uint4*>(nxt + PIECE + tid * 16) =
+                    tid == 0 ? s.halo[i + 1] : make_uint4(0, 0, 0, 0);
+        }
+        lw_bar();  // masks visible
+        LW_STAMP(0);
+        const uint32_t clen = piece_clen(a, base);
+        if (i < 0) {
+            x = lw_entry_guess(s, a, cur, base, clen);
+            if (x == ~0ull) {
+                ok = false;
+                break;
+            }
+        }
+        uint32_t cnt = 0;
+        uint64_t ex = 0;
+        hg_span* out = i < 0 ? nullptr : a.scratch + (size_t)(p0 + i) * MAX_REC_PIECE;
+        if (!lw_piece(s, a, cur, base, clen, x, out, cnt, ex, base0)) {
+            ok = false;
+            break;
+        }
+        if (i < 0) LW_STAMP(6);
+        if (i >= 0) {
+            if (tid == 0) {
+                SpecPiece o;
+                o.x = x;
+                o.R = 0;
+                o.kl = o.vl = 0;
+                o.count = cnt;
+                o.pad = SP_HOP;
+                sp[p0 + i] = o;
+            }
+            total += cnt;
+        } else {
+            X0 = ex;
+        }
+        if (i == 0) X0 = x;
+        x = ex;
+    }
+    lw_wait_vm();  // no DMA may land after this batch is done with the buffers
+    X = x;
+    if (ok && a.sdiag && tid == 0)
+        for (uint32_t k = 0; k < LW_PROF; ++k) a.sdiag[(size_t)(p0 / a.sbp) * LW_PROF + k] = s.lw_prof[k];
+    return ok;
+}
+
 // Stride check of one staged piece without a barrier: the run's geometry
 // (entry, R, count) follows from the uniform header at X alone, so the exit
 // is known at once; the per-lane compares only decide whether the batch is
@@ -1880,6 +2459,7 @@ __device__ __forceinline__ bool stride_geom(const uint8_t* data, uint64_t base, 
 
 __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
     __shared__ SpecSmem s;
+    __shared__ uint64_t lw_alt[(PIECE + 64) / 8];  // lane-walk mode's second piece buffer
     const uint32_t tid = threadIdx.x;
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     const uint32_t b = blk;
@@ -1901,13 +2481,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         const uint32_t clen = piece_clen(a, base);
         __syncthreads();  // (A)
         if (i == 0 && tid < np) s.halo[tid] = h;
-#pragma unroll
-        for (uint32_t q = 0; q < GPT; ++q)
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s.data64) +
-                                      (q * THREADS + tid) * 16) = v[q];
-        if (tid < 4)  // thread 0 reads back its own halo write when i == 0
-            *reinterpret_cast<uint4*>(reinterpret_cast<uint8_t*>(s.data64) + PIECE + tid * 16) =
-                tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
+        spec_stage(s, v, i);
         if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
         __syncthreads();  // (B)
         if (i == 0 && b == 0) {
@@ -1950,6 +2524,10 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     if (hop) {
         bad = 0;
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
+        if (!ok && s.hcode == SB_HOP_SMALL) {  // small records: lane walks over the staged pieces
+            ok = lw_batch(s, lw_alt, a, p0, np, sp, v, X0, X, total);
+            if (tid == 0) s.hcode = ok ? SB_LW : SB_LW_DEAD;
+        }
     }
     if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
 
@@ -1962,6 +2540,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         o.count = (uint32_t)total;
         o.ok = ok ? 1u : 0u;
         o.pad = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
+        if (hop && (s.hcode == SB_LW || s.hcode == SB_LW_DEAD)) o.pad |= (uint64_t)s.lw_nser << 32;
         sb[b] = o;
         atomicAdd(&a.gsum[b / SPEC_GROUP], (unsigned long long)total);
         if (!ok || (b == 0 && X0 != a.entry)) mark_bad(a.ctl, a.nspec, b);
@@ -1970,7 +2549,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     }
 }
 
-__global__ __launch_bounds__(THREADS) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
+__global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
                                                               SpecPiece* sp) {
     spec_body(a, sb, sp, blockIdx.x);
 }
@@ -2010,7 +2589,7 @@ __global__ __launch_bounds__(THREADS) void decode_zero_multi(const DecodeArgs* t
     }
 }
 
-__global__ __launch_bounds__(THREADS) void decode_spec_multi(const DecodeArgs* tabs,
+__global__ __launch_bounds__(THREADS, 4) void decode_spec_multi(const DecodeArgs* tabs,
                                                              const uint32_t* pre, uint32_t ntab) {
     const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
     const DecodeArgs a = tabs[t];
@@ -2177,6 +2756,7 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     a.npieces = (uint32_t)l.npieces;
     a.hz = 8 - nb;
     a.diag = d_diag;
+    a.sdiag = d_diag ? d_diag + (size_t)l.nbatches * DIAG_WORDS : nullptr;
     a.sbatch = reinterpret_cast<SpecBatch*>(ws + l.sbatch_off);
     a.spiece = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);

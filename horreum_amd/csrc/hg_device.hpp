@@ -73,6 +73,34 @@ __device__ __forceinline__ void lds_header32(const uint8_t* lds, uint32_t p, uin
     v1 = __builtin_amdgcn_alignbyte(a4, a3, sh);
 }
 
+// Wave-level inclusive max / sum scans over u32 by DPP (row shifts 1, 2, 4, 8
+// inside each 16-lane row, then the row totals by row_bcast 15 / 31): six
+// VALU steps, no LDS round trips (a __shfl_up chain is six ds_bpermutes).
+__device__ __forceinline__ uint32_t dpp_max_incl(uint32_t v) {
+#define HG_DPP_MAX(ctrl, rmask) \
+    v = max(v, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, rmask, 0xf, false))
+    HG_DPP_MAX(0x111, 0xf);
+    HG_DPP_MAX(0x112, 0xf);
+    HG_DPP_MAX(0x114, 0xf);
+    HG_DPP_MAX(0x118, 0xf);
+    HG_DPP_MAX(0x142, 0xa);
+    HG_DPP_MAX(0x143, 0xc);
+#undef HG_DPP_MAX
+    return v;
+}
+__device__ __forceinline__ uint32_t dpp_sum_incl(uint32_t v) {
+#define HG_DPP_ADD(ctrl, rmask) \
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, rmask, 0xf, false)
+    HG_DPP_ADD(0x111, 0xf);
+    HG_DPP_ADD(0x112, 0xf);
+    HG_DPP_ADD(0x114, 0xf);
+    HG_DPP_ADD(0x118, 0xf);
+    HG_DPP_ADD(0x142, 0xa);
+    HG_DPP_ADD(0x143, 0xc);
+#undef HG_DPP_ADD
+    return v;
+}
+
 // Wave-level inclusive scan (64 lanes).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
     const uint32_t lane = threadIdx.x & 63u;

@@ -402,3 +402,56 @@ def test_batch_decode_guess_shapes(engine):
         off = int(r[24 * i + 16:24 * i + 24].view("<u8")[0])
         assert (n, kind, off if kind else 0) == (wn, wk, wo if wk else 0), i
         assert np.array_equal(engine.spans_to_numpy(spans[i], min(n, caps[i])), ws), i
+
+
+def _shape_table(n, kr, vr, seed):
+    """decode_variants-style table built vectorised: n records, key lengths in
+    [kr[0], kr[1]), value lengths in [vr[0], vr[1]) (5 % tombstones), random
+    payload bytes."""
+    rng = np.random.default_rng(seed)
+    kl = rng.integers(*kr, n)
+    vl = rng.integers(*vr, n)
+    vl[rng.random(n) < 0.05] = 0
+    offs = np.concatenate([[0], np.cumsum(16 + kl + vl)])
+    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(n, 16)
+    for i in range(16):
+        buf[offs[:-1] + i] = hdr[:, i]
+    return buf
+
+
+_SB = np.dtype([("x0", "<u8"), ("exit", "<u8"), ("count", "<u4"), ("ok", "<u4"), ("pad", "<u8")])
+
+
+def _prepass_codes(engine):
+    """SpecBatch codes of the context's last decode (hg_decode.hip SB_*)."""
+    import ctypes
+    lib = engine.lib
+    lib.hgk_ctx_workspace.restype = ctypes.c_void_p
+    lib.hgk_ctx_workspace.argtypes = [ctypes.c_void_p]
+    lib.hgk_debug_d2h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    lay = (ctypes.c_uint64 * 8)()
+    lib.hgk_decode_last_layout(lay)
+    sb_off, nspec = int(lay[0]), int(lay[2])
+    sb = np.zeros(nspec, _SB)
+    ws = lib.hgk_ctx_workspace(engine.ctx)
+    lib.hgk_debug_d2h(sb.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws + sb_off), sb.nbytes)
+    return sb["pad"] & 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("shape", [("small", 1_200_000, (0, 24), (0, 64)),
+                                   ("medium", 220_000, (8, 65), (64, 513))])
+def test_lane_walk_mode_at_scale(engine, shape):
+    """Small / medium records over many pre-pass batches: the lane-walk mode
+    (decode_spec_kernel, SB_LW) must resolve every batch itself -- its
+    fallback to decode_kernel's engine is exact too, so parity alone would
+    not notice a lane-walk regression -- and the spans must be bit-exact vs
+    the oracle, whole and cut mid-record / at a piece edge."""
+    _, n, kr, vr = shape
+    data = _shape_table(n, kr, vr, seed=7)
+    assert data.size > 48 * (1 << 20)
+    assert_same(engine, data)
+    codes = _prepass_codes(engine)
+    assert np.mean(codes == 6) >= 0.99, np.unique(codes, return_counts=True)
+    assert_same(engine, data[: data.size - 5])
+    assert_same(engine, data[: (data.size // CHUNK - 5) * CHUNK + 3])

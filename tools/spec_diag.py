@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Pre-pass diagnostics: how each decode_spec_kernel batch went (SpecBatch.pad:
 1 stride, 2 stride broke, 3 hop: small records, 4 hop: unreadable record,
-5 hop ok) and the resolved prefix, for the decode_variants workloads."""
+5 hop ok, 6 lane walks ok, 7 lane walks: unresolved) and the resolved prefix, for the decode_variants workloads."""
 import ctypes
 import os
 import sys
@@ -56,7 +56,7 @@ def main():
         links = int(np.sum(sb["x0"][1:] != sb["exit"][:-1]))
         print(f"{label}: n={out.n} kind={out.kind} nspec={nspec} sbp={sbp} bp={bp} "
               f"first_bad={fb} codes={dict(sorted(codes.items()))} link_mismatch={links} "
-              f"ok={int(sb['ok'].sum())}", flush=True)
+              f"ok={int(sb['ok'].sum())} lw_serial={int((sb['pad'] >> 32).sum())}", flush=True)
         bad = np.nonzero(sb["x0"][1:] != sb["exit"][:-1])[0][:5]
         for j in bad:
             print(f"   link {j}->{j+1}: exit {sb['exit'][j]} x0 {sb['x0'][j+1]} "
