@@ -1598,8 +1598,9 @@ constexpr uint32_t HOP_MAX_REDO = 2;    // stitch re-walks per batch before givi
 constexpr uint32_t HOP_TRIES = 8;                         // candidates tried per lane
 constexpr uint64_t NO_HOP = ~0ull;
 
+constexpr uint32_t LW_ZM_WORDS = 64 * 64 / 16 + 8;  // granule masks per lane-walk chunk (+ halo)
 struct SpecSmem {
-    uint64_t data64[(PIECE + 64) / 8];  // a piece, or four HOP_WIN + 16 byte windows
+    uint64_t data64[(PIECE + 512) / 8];  // a piece, four HOP_WIN + 16 byte windows, or lane-walk chunk buffers
     uint4 halo[SPEC_BP];
     uint32_t guess;
     uint64_t hg[HOP_SEGS];    // guessed segment entries (NO_HOP: none)
@@ -1610,18 +1611,15 @@ struct SpecSmem {
     uint32_t hok;
     uint64_t hx, ht;          // batch exit and records after stitching
     uint32_t hcode;           // SpecBatch.pad: how the batch went (SB_*)
-    // lane-walk mode (lw_piece): per-wave exit maxima / change flags / record
-    // counts of the last two relaxation rounds, lane guesses, the entry guess
-    uint64_t lw_wx[2][NW];    // per wave: entry used, exit, records, unresolved (two rounds)
+    // lane-walk mode (lw_batch): per-wave chunk masks and guess / chain
+    // scratch, quarter summaries of the last two stitching rounds
+    alignas(8) uint16_t lw_zm[NW][LW_ZM_WORDS];
+    uint32_t lw_sg[THREADS];
+    uint8_t lw_tg[THREADS];
+    uint64_t lw_wx[2][NW];
     uint64_t lw_wexit[2][NW];
     uint32_t lw_wcnt[2][NW];
     uint32_t lw_wbad[2][NW];
-    uint32_t lw_cnt[NW];
-    uint32_t lw_sg[THREADS];
-    uint8_t lw_tg[THREADS];
-    uint16_t lw_zm[NGRAN + 8];  // 16-bit zero mask per granule of the staged piece (+ halo)
-    unsigned long long lw_best, best_any;
-    uint32_t lw_nser;         // serial fallbacks of the batch (SpecBatch.pad >> 32, diagnostics)
     uint32_t lw_prof[8];      // diagnostics (a.sdiag): cycles per lane-walk phase, see LW_STAMP
     uint64_t lw_last;
 };
@@ -1860,33 +1858,51 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
 
 // ---- lane-walk mode (small and medium records) ----------------------------------
 // A pre-pass batch whose records are too small to hop (hop_batch: more than
-// HOP_MAX_CAND candidate run ends in piece 0) is resolved here, piece by piece
-// from the batch's entry, each piece staged in LDS as in the stride path (the
-// next piece's loads in flight meanwhile).  A piece with entry X:
-//   - every lane owns 64 bytes; the lane holding X starts there, every later
-//     lane guesses its first record start: the first candidate that ENDS a
-//     run of zero-mask candidates (a short header also passes the filter 1-3
-//     bytes to its left), reads as a record shorter than HG_FAR_CAND that fits
-//     the file and whose next header (if inside the piece) is readable; then it
-//     walks <= 4 records to its segment end;
-//   - relaxation: a lane's entry is the largest exit of the lanes before it
-//     (block max-scan: wave scans + one word per wave), a segment that entry
-//     jumps over is passed through, a lane entered off its guess walks again;
-//     rounds repeat until no exit changes -- that fixed point is exact from X
-//     by induction over the lanes;
+// HOP_MAX_CAND candidate run ends in piece 0) is resolved here.  Each of the
+// four waves owns a quarter of the batch's pieces and streams it on its own,
+// 4 KiB CHUNK by chunk, with no workgroup barrier until the end: chunk k + 1
+// is DMA'd global -> LDS (wave-private double buffer, no registers) while
+// chunk k is walked, and a chunk's entry is the exact exit of the one before.
+// A chunk entered at X:
+//   - zero masks: one 16-bit mask per 16-byte granule, computed by the wave
+//     from LDS in a conflict-free pattern; every lane owns 64 bytes and takes
+//     its candidate bits from 80 mask bits (one aligned 8-byte LDS read);
+//   - the lane holding X starts there, every later lane guesses its first
+//     record start: the first candidate that ENDS a run of zero-mask
+//     candidates (a short header also passes the filter 1-3 bytes to its
+//     left), reads as a record shorter than HG_FAR_CAND that fits the file and
+//     whose next header (if inside the chunk) is readable; it walks <= 4
+//     records to its segment end;
+//   - relaxation (DPP max-scans, wave-local): a lane's entry is the largest
+//     exit of the CHAIN lanes before it (the entry lane, or a lane whose guess
+//     another lane's walk exits on -- a wrong guess in a segment without a
+//     record start rarely lies on another lane's exit, so it cannot push the
+//     lanes after it past their true entries), a segment that entry jumps over
+//     is passed through, a lane entered off its guess walks again; rounds
+//     repeat until no exit changes -- that fixed point is exact from X by
+//     induction over the lanes; no convergence: lane 0 walks the chunk;
 //   - spans go to the piece's scratch slot (decode_kernel copies them, as for
-//     hop segments), the count and exit to the piece record.
-// Any unreadable record on the exact path, or no convergence, leaves the batch
-// to decode_kernel's engine, which reports errors exactly.
-constexpr uint32_t LW_WROUNDS = 64;   // wave-local relaxation rounds before the serial fallback
-constexpr uint32_t LW_WSPAN = 64 * SEG;  // bytes per wave
-constexpr uint32_t LW_LEAD = 1024;     // lead-in bytes walked before a batch's first piece
-constexpr uint32_t LW_TRIES = 3;       // candidates a lane examines for its guess
+//     hop segments), counts and entries to the piece records.
+// A wave's first chunk is entered at the exit of a LEAD-IN chunk (the 4 KiB
+// before its quarter, entered at its first lane guess whose walk lands on
+// another guess): a wrong lead-in guess has re-joined the true path by the
+// quarter's start almost always.  The quarters are stitched once at the end;
+// a quarter entered off its predecessor's exit is streamed again from it.
+// Any unreadable record on the exact path leaves the batch to decode_kernel's
+// engine, which reports errors exactly.
+constexpr uint32_t LW_CHUNK = 64 * SEG;         // bytes per chunk: one wave, 64 x 64 B
+constexpr uint32_t LW_CBUF = LW_CHUNK + 128;    // chunk + halo + read slack
+constexpr uint32_t LW_CPP = PIECE / LW_CHUNK;   // chunks per piece
+static_assert(LW_ZM_WORDS == LW_CHUNK / 16 + 8, "lane-walk mask rows");
+static_assert(4 * LW_CBUF <= PIECE + 512, "two waves' chunk buffers per piece buffer");
+constexpr uint32_t LW_WROUNDS = 64;             // relaxation rounds before lane 0 walks it
+constexpr uint32_t LW_TRIES = 3;                // candidates a lane examines for its guess
 constexpr uint32_t LW_PROF = 8;
-// Diagnostics (a.sdiag != null, tools/lw_diag.py): thread 0 charges the cycles
-// since the last stamp to phase k (0 staging, 1 masks + guesses + walks,
-// 2 chain marks, 3 relaxation rounds, 4 count scan, 5 span stores, 6 lead-in
-// probe, 7 rounds run).
+constexpr uint64_t LW_GUESS = ~0ull;            // "enter at the first linked lane guess"
+// Diagnostics (a.sdiag != null, tools/lw_diag.py): lane 0 of wave 0 charges the
+// cycles since the last stamp to phase k (0 waiting for a chunk + its masks,
+// 1 guesses + walks, 2 chain marks, 3 relaxation, 4 span stores, 5 stitching,
+// 6 lead-in chunks, 7 relaxation rounds run).
 #define LW_STAMP(k)                                                   \
     do {                                                              \
         if (a.sdiag && threadIdx.x == 0) {                            \
@@ -1896,39 +1912,110 @@ constexpr uint32_t LW_PROF = 8;
         }                                                             \
     } while (0)
 
-// Workgroup barrier for LDS only: waits this wave's LDS operations, not its
-// vector memory ones, so a global->LDS prefetch of the next piece stays in
-// flight across it (__syncthreads() would drain it with vmcnt(0)).
-__device__ __forceinline__ void lw_bar() {
-    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+// LDS written by some lanes of this wave, read by others: DS operations of one
+// wave execute in order; this keeps the compiler from reordering them.
+__device__ __forceinline__ void lw_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
 }
-__device__ __forceinline__ void lw_wait_vm() { __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// Global -> LDS DMA of the whole piece at base (base + PIECE <= rlen): one
-// 16-byte global_load_lds per thread and granule column; each wave
-// instruction fills 1 KiB of dst contiguously (lane-linear).  No registers
-// hold the bytes, so the lane walks of the current piece keep their VGPRs.
-__device__ __forceinline__ void lw_dma_piece(const DecodeArgs& a, uint64_t base, uint8_t* dst) {
-    const uint32_t tid = threadIdx.x, wid = tid >> 6;
-#pragma unroll
-    for (uint32_t q = 0; q < GPT; ++q) {
-        const uint32_t g0 = q * THREADS + wid * 64;  // the wave's first granule
-        __builtin_amdgcn_global_load_lds(
-            static_cast<const void*>(a.sst + base + (uint64_t)(g0 + (tid & 63u)) * 16),
-            (__attribute__((address_space(3))) void*)(dst + g0 * 16), 16, 0, 0);
+// s_waitcnt vmcnt(min(n, 8)): the wave's vector memory operations complete in
+// issue order, so with the chunk DMA issued before n span stores this waits
+// for the DMA only (fewer than n allowed outstanding is merely conservative).
+__device__ __forceinline__ void lw_wait_vm(uint32_t n) {
+    switch (n) {
+        case 0: __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: __asm__ volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: __asm__ volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: __asm__ volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: __asm__ volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: __asm__ volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: __asm__ volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     }
 }
 
-// Plain staging of [base, base + PIECE) + halo (zero past rlen) into dst.
-__device__ __forceinline__ void lw_plain_stage(const DecodeArgs& a, uint64_t base, uint8_t* dst) {
-    const uint32_t tid = threadIdx.x;
+// Chunk at cb (relative to a.sst) into the wave buffer dst: bytes [cb, cb +
+// LW_CHUNK + 64).  In bounds: five global_load_lds instructions (4 x 1 KiB,
+// lane-linear, + the halo by lanes 0-3); near the end of the bytes present:
+// plain 16-byte loads with zero fill (returns after they landed).  Returns the
+// vector memory instructions left in flight.
+__device__ __forceinline__ uint32_t lw_fetch_chunk(const DecodeArgs& a, uint64_t cb, uint8_t* dst) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (cb + LW_CHUNK + 64 <= a.rlen) {
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            __builtin_amdgcn_global_load_lds(
+                static_cast<const void*>(a.sst + cb + (uint64_t)(q * 64 + lane) * 16),
+                (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
+        if (lane < 4)
+            __builtin_amdgcn_global_load_lds(
+                static_cast<const void*>(a.sst + cb + LW_CHUNK + lane * 16),
+                (__attribute__((address_space(3))) void*)(dst + LW_CHUNK), 16, 0, 0);
+        return 5;
+    }
 #pragma unroll 1
-    for (uint32_t q = 0; q < GPT; ++q)  // rolled: few registers
-        *reinterpret_cast<uint4*>(dst + (q * THREADS + tid) * 16) =
-            load16(a, base + (q * THREADS + tid) * 16);
-    if (tid < 4)
-        *reinterpret_cast<uint4*>(dst + PIECE + tid * 16) =
-            tid == 0 ? load16(a, base + PIECE) : make_uint4(0, 0, 0, 0);
+    for (uint32_t q = 0; q < 4; ++q)
+        *reinterpret_cast<uint4*>(dst + (q * 64 + lane) * 16) = load16(a, cb + (q * 64 + lane) * 16);
+    if (lane < 4)
+        *reinterpret_cast<uint4*>(dst + LW_CHUNK + lane * 16) = load16(a, cb + LW_CHUNK + lane * 16);
+    return 0;
+}
+
+// Granule zero masks of the staged chunk into zm (conflict-free: lane l reads
+// granules l, l+64, l+128, l+192 and the halo's).
+__device__ __forceinline__ void lw_chunk_masks(const uint8_t* buf, uint16_t* zm) {
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q)
+        zm[q * 64 + lane] = (uint16_t)zmask16(*reinterpret_cast<const uint4*>(buf + (q * 64 + lane) * 16));
+    if (lane < 4)
+        zm[256 + lane] = (uint16_t)zmask16(*reinterpret_cast<const uint4*>(buf + LW_CHUNK + lane * 16));
+    lw_wave_sync();
+}
+
+// Candidate mask of this lane's segment and the next lane's first bit from
+// the granule masks: bit j of the 80 zero-mask bits z1:z0 <=> byte j is zero,
+// candidate j <=> bytes [j+8-hz, j+8) and [j+16-hz, j+16) are zero.
+__device__ __forceinline__ void lw_masks(const uint16_t* zm, uint32_t seg0, uint32_t clen,
+                                         uint64_t rem, uint32_t hz, uint64_t& cm0,
+                                         uint64_t& nextbit) {
+    cm0 = 0;
+    nextbit = 0;
+    if (seg0 >= clen || rem < 16) return;
+    const uint32_t gi = seg0 / 16;
+    const uint64_t z0 = *reinterpret_cast<const uint64_t*>(&zm[gi]);
+    const uint32_t z1 = zm[gi + 4];
+    uint64_t c, c64;
+    if (hz == 0) {
+        c = ~0ull;
+        c64 = 1;
+    } else {  // 80-bit shifts as 64 + 16 bits
+        const uint32_t hi = z1 & 0xFFFFu;
+        uint64_t alo = z0;
+        uint32_t ahi = hi;
+        for (uint32_t k = 1; k < hz; ++k) {  // bit i of A: bytes i .. i+hz-1 are zero
+            alo &= (z0 >> k) | ((uint64_t)hi << (64 - k));
+            ahi &= hi >> k;
+        }
+        const uint32_t s1 = 8 - hz, s2 = 16 - hz;  // s1 in [0, 7], s2 in [8, 15]
+        const uint64_t a1 = s1 ? ((alo >> s1) | ((uint64_t)ahi << (64 - s1))) : alo;
+        const uint64_t a2 = (alo >> s2) | ((uint64_t)ahi << (64 - s2));
+        c = a1 & a2;
+        c64 = ((ahi >> s1) & (ahi >> s2)) & 1u;
+    }
+    const uint32_t n = min(seg0 + SEG, clen) - seg0;  // positions where records may start
+    if (n < 64) c &= (1ull << n) - 1ull;
+    const uint64_t plim = rem - 16;  // last readable header position
+    if (plim < seg0) {
+        c = 0;
+    } else if (plim - seg0 < 63) {
+        c &= (2ull << (plim - seg0)) - 1ull;
+    }
+    const uint32_t q = seg0 + SEG;
+    nextbit = (q < clen && (uint64_t)q <= plim) ? c64 : 0ull;
+    cm0 = c;
 }
 
 // This lane's guess in [seg0, segend) (piece-relative) or NO_GUESS; cm0 / the
@@ -1962,353 +2049,228 @@ __device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, uint32_t seg0,
     return NO_GUESS;
 }
 
-// Zero masks of the staged piece: one 16-bit mask per 16-byte granule (plus
-// the halo and the zero slack after it) in s.lw_zm, from registers while
-// staging (lw_stage) or from LDS.
-__device__ __forceinline__ void lw_zm_from_lds(SpecSmem& s, const uint8_t* data) {
-#pragma unroll
-    for (uint32_t q = 0; q < GPT; ++q) {
-        const uint32_t gi = q * THREADS + threadIdx.x;
-        s.lw_zm[gi] = (uint16_t)zmask16(*reinterpret_cast<const uint4*>(data + gi * 16));
-    }
-    if (threadIdx.x < 4)
-        s.lw_zm[NGRAN + threadIdx.x] =
-            (uint16_t)zmask16(*reinterpret_cast<const uint4*>(data + PIECE + threadIdx.x * 16));
-}
-
-// Candidate mask of this lane's segment and the next lane's first bit, from
-// the granule masks (one aligned 8-byte LDS read + one 2-byte read): bit j of
-// the 80 zero-mask bits z1:z0 <=> byte j is zero, candidate j <=> bytes
-// [j+8-hz, j+8) and [j+16-hz, j+16) are zero.
-__device__ __forceinline__ void lw_masks(const SpecSmem& s, uint32_t seg0, uint32_t clen,
-                                         uint64_t rem, uint32_t hz, uint64_t& cm0,
-                                         uint64_t& nextbit) {
-    cm0 = 0;
-    nextbit = 0;
-    if (seg0 >= clen || rem < 16) return;
-    const uint32_t gi = seg0 / 16;
-    const uint64_t z0 = *reinterpret_cast<const uint64_t*>(&s.lw_zm[gi]);
-    const uint32_t z1 = s.lw_zm[gi + 4];
-    uint64_t c = 0, c64 = 0;
-    if (hz == 0) {
-        c = ~0ull;
-        c64 = 1;
-    } else {  // 80-bit shifts as 64 + 16 bits (a switch over templated HZ spilled registers)
-        const uint32_t hi = z1 & 0xFFFFu;
-        uint64_t alo = z0;
-        uint32_t ahi = hi;
-        for (uint32_t k = 1; k < hz; ++k) {  // bit i of A: bytes i .. i+hz-1 are zero
-            alo &= (z0 >> k) | ((uint64_t)hi << (64 - k));
-            ahi &= hi >> k;
-        }
-        const uint32_t s1 = 8 - hz, s2 = 16 - hz;  // s1 in [0, 7], s2 in [8, 15]
-        const uint64_t a1 = s1 ? ((alo >> s1) | ((uint64_t)ahi << (64 - s1))) : alo;
-        const uint64_t a2 = (alo >> s2) | ((uint64_t)ahi << (64 - s2));
-        c = a1 & a2;
-        c64 = ((ahi >> s1) & (ahi >> s2)) & 1u;
-    }
-    const uint32_t n = min(seg0 + SEG, clen) - seg0;  // positions where records may start
-    if (n < 64) c &= (1ull << n) - 1ull;
-    const uint64_t plim = rem - 16;  // last readable header position
-    if (plim < seg0) {
-        c = 0;
-    } else if (plim - seg0 < 63) {
-        c &= (2ull << (plim - seg0)) - 1ull;
-    }
-    const uint32_t q = seg0 + SEG;
-    nextbit = (q < clen && (uint64_t)q <= plim) ? c64 : 0ull;
-    cm0 = c;
-}
-
-// Entry guess of the staged bytes at base (clen bytes where records may
-// start) when nothing is known: the first lane guess whose walk exits exactly
-// on another lane's guess, else the first lane guess; ~0 if no lane has one.
-// All threads.
-__device__ __forceinline__ uint64_t lw_entry_guess(SpecSmem& s, const DecodeArgs& a,
-                                                   const uint8_t* data, uint64_t base, uint32_t clen) {
-    const uint32_t tid = threadIdx.x;
-    const uint64_t rem = a.len - base;
-    const uint32_t seg0 = tid * SEG, segend = min(seg0 + SEG, clen);
-    uint64_t cm0, nb;
-    lw_masks(s, seg0, clen, rem, a.hz, cm0, nb);
-    uint32_t g = NO_GUESS;
-    Walk w;
-    w.dead = true;
-    w.exit = 0;
-    if (seg0 < clen) g = lw_guess(data, seg0, segend, clen, rem, a.hz, cm0, nb);
-    if (g != NO_GUESS) lane_walk(data, base, a.len, g, segend, w);
-    const bool valid = g != NO_GUESS && !w.dead;
-    s.lw_sg[tid] = valid ? g : NO_GUESS;
-    if (tid == 0) {
-        s.lw_best = ~0ull;
-        s.best_any = ~0ull;
-    }
-    lw_bar();
-    bool linked = false;
-    if (valid && w.exit < base + clen) {
-        const uint32_t u = (uint32_t)(w.exit - base);
-        linked = s.lw_sg[u / SEG] == u;
-    }
-    if (linked) atomicMin(&s.lw_best, (unsigned long long)(base + g));
-    if (valid) atomicMin(&s.best_any, (unsigned long long)(base + g));
-    lw_bar();
-    const uint64_t b1 = uni((uint64_t)s.lw_best), b2 = uni((uint64_t)s.best_any);
-    lw_bar();
-    return b1 != ~0ull ? b1 : b2;
-}
-
-// Exact serial walk of the staged bytes from X by thread 0 (the relaxation
-// did not converge: rare, e.g. a wrong guess that links and pushes a long run
-// of lanes past their entries).  Emits to out, or (out == nullptr) finds the
-// first start >= cut.  False if a record on the path cannot be read.
-__device__ __forceinline__ bool lw_serial(SpecSmem& s, const DecodeArgs& a, const uint8_t* data,
-                                          uint64_t base, uint32_t clen, uint64_t X, hg_span* out,
-                                          uint64_t cut, uint32_t& count, uint64_t& exit) {
-    if (threadIdx.x == 0) {
-        ++s.lw_nser;
-        uint32_t n = 0;
-        uint64_t cur = X, first = ~0ull;
-        bool ok = true;
-        while (cur < base + clen) {
+// Lane 0 walks the staged chunk exactly from X (the relaxation did not
+// converge: rare, e.g. a wrong guess that links and pushes a long run of
+// lanes past their entries): spans to out (if any).  False if a record on
+// the path cannot be read.  Wave-level; every lane returns the same values.
+__device__ __forceinline__ bool lw_chunk_serial(const DecodeArgs& a, const uint8_t* data,
+                                                uint64_t cb, uint32_t clen, uint64_t X,
+                                                hg_span* out, uint32_t& count, uint64_t& exit,
+                                                uint32_t& nstores) {
+    uint32_t n = 0, ok = 1;
+    uint64_t cur = X;
+    if ((threadIdx.x & 63u) == 0) {
+        while (cur < cb + clen) {
             if (cur + 16 > a.len) {
-                ok = false;
+                ok = 0;
                 break;
             }
             uint32_t k0, k1, v0, v1;
-            lds_header32(data, (uint32_t)(cur - base), k0, k1, v0, v1);
+            lds_header32(data, (uint32_t)(cur - cb), k0, k1, v0, v1);
             const uint64_t body = (uint64_t)k0 + v0;
             if ((k1 | v1) || body > a.len - cur - 16) {
-                ok = false;
+                ok = 0;
                 break;
             }
             if (out) write_span(out, n, cur, k0, v0);
-            if (cur >= cut && first == ~0ull) first = cur;
             ++n;
             cur += 16 + body;
         }
-        if (!out && first == ~0ull) first = cur;  // the first start at or after the window
-        s.lw_cnt[0] = n;
-        s.lw_best = ok ? (out ? cur : first) : ~0ull;
     }
-    lw_bar();
-    count = uni(s.lw_cnt[0]);
-    exit = uni((uint64_t)s.lw_best);
-    lw_bar();
-    return exit != ~0ull;
+    count = __shfl(n, 0, 64);
+    exit = __shfl(cur, 0, 64);
+    nstores = out ? count : 0u;
+    return __shfl(ok, 0, 64) != 0;
 }
 
-// The staged bytes at base (records start in [base, base + clen)) entered at
-// X (exact, absolute): spans to out[0, count) (absolute offsets), count and
-// exit.  With out == nullptr (probe) exit is instead the first record start
-// >= cut on that path.  False if the exact path cannot be resolved here.  All
-// threads; returns a block-uniform value.
-//
-// Relaxation is wave-local (DPP scans, no barriers): each wave covers 4 KiB;
-// the wave holding X starts there, every later wave speculates that it is
-// entered at its first lane guess.  One barrier publishes each wave's
-// (entry, exit, count); the waves are stitched in order, and a wave whose
-// speculated entry is not its predecessor's exit relaxes again from that exit
-// (rare: a record start that no lane guessed), behind one more barrier.
-__device__ __forceinline__ bool lw_piece(SpecSmem& s, const DecodeArgs& a, const uint8_t* data,
-                                         uint64_t base, uint32_t clen, uint64_t X, hg_span* out,
-                                         uint32_t& count, uint64_t& exit, uint64_t cut = 0) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint64_t rem = a.len - base;
-    if (X >= base + clen) {  // a record spans the whole piece
-        count = 0;
-        exit = X;
+// The staged chunk at cb (records start in [cb, cb + clen)) entered at X
+// (exact; LW_GUESS: at its first lane guess whose walk lands on another
+// lane's guess): spans to out[0, count) (nullptr: none), entry = the entry
+// used, exit = the first start at or after cb + clen, nstores = span store
+// instructions issued.  Wave-level; every lane returns the same values.
+__device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const uint8_t* data,
+                                         const uint16_t* zm, uint32_t* sg, uint8_t* tg,
+                                         uint64_t cb, uint32_t clen, uint64_t X, hg_span* out,
+                                         uint64_t& entry, uint32_t& count, uint64_t& exit,
+                                         uint32_t& nstores) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool guess = X == LW_GUESS;
+    nstores = 0;
+    count = 0;
+    if (!guess && (clen == 0 || X >= cb + clen)) {  // past stop, or a record spans the chunk
+        entry = exit = X;
         return true;
     }
-    const uint32_t seg0 = tid * SEG, segend = min(seg0 + SEG, clen);
-    const uint32_t xr = (uint32_t)(X - base);
-    const uint32_t je = xr / SEG, wje = je >> 6;
-    const uint32_t wq0 = wid * LW_WSPAN;
-    const uint32_t wq1 = min(wq0 + LW_WSPAN, clen);
-    const bool in_piece = seg0 < clen && tid >= je;
+    const uint64_t rem = a.len - cb;
+    const uint32_t seg0 = lane * SEG, segend = min(seg0 + SEG, clen);
+    const uint32_t je = guess ? 0u : (uint32_t)((X - cb) / SEG);
+    const bool in_chunk = seg0 < clen && lane >= je;
     uint64_t cm0, nb;
-    lw_masks(s, seg0, clen, rem, a.hz, cm0, nb);
+    lw_masks(zm, seg0, clen, rem, a.hz, cm0, nb);
     uint32_t g = NO_GUESS;
     Walk w;
     w.dead = true;
     w.exit = 0;
     w.cnt = 0;
     w.p01 = w.p23 = 0;
-    if (tid == je) g = xr;
-    else if (in_piece) g = lw_guess(data, seg0, segend, clen, rem, a.hz, cm0, nb);
-    if (in_piece && g != NO_GUESS) lane_walk(data, base, a.len, g, segend, w);
+    if (!guess && lane == je) g = (uint32_t)(X - cb);
+    else if (in_chunk) g = lw_guess(data, seg0, segend, clen, rem, a.hz, cm0, nb);
+    if (in_chunk && g != NO_GUESS) lane_walk(data, cb, a.len, g, segend, w);
     LW_STAMP(1);
     auto rel = [&](uint64_t e) -> uint32_t {
-        const uint64_t d = e - base;
+        const uint64_t d = e - cb;
         return d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
     };
-    // Chain lanes (wave-local): a lane whose guess another lane's walk in the
-    // same wave exits on.  Only they (and the entry lane) seed the first
-    // round, so a wrong guess in a segment without a record start cannot push
-    // the lanes after it past their true entries.
-    const bool valid0 = in_piece && g != NO_GUESS && !w.dead;
-    s.lw_sg[tid] = valid0 ? g : NO_GUESS;
-    s.lw_tg[tid] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
+    // chain marks: which lane guesses some lane's walk exits on
+    const bool valid0 = in_chunk && g != NO_GUESS && !w.dead;
+    sg[lane] = valid0 ? g : NO_GUESS;
+    tg[lane] = 0;
+    lw_wave_sync();
+    bool links = false;
     if (valid0) {
         const uint32_t u = rel(w.exit);
-        if (u >= wq0 && u < wq1 && s.lw_sg[u / SEG] == u) s.lw_tg[u / SEG] = 1;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    const bool chain = s.lw_tg[tid] != 0;
-    // this wave's entry: lane jl (64 = none walks) at piece-relative xw
-    // (absolute xa; ~0: no guess in the wave)
-    uint32_t jl = 64, xw = 0xFFFFFFFFu;
-    uint64_t xa = ~0ull;
-    if (wq0 < clen && wid >= wje) {
-        if (wid == wje) {
-            jl = je & 63u;
-            xw = xr;
-            xa = X;
-        } else {
-            const unsigned long long vb = __ballot(valid0);
-            if (vb) {
-                jl = (uint32_t)__ffsll((long long)vb) - 1;
-                xw = __shfl(g, (int)jl, 64);
-                xa = base + xw;
-            }
+        if (u < clen && sg[u / SEG] == u) {
+            tg[u / SEG] = 1;
+            links = true;
         }
     }
-    uint32_t st = 3;  // 0 walking from g, 1 passed through, 2 waiting, 3 not in this wave's path
-    uint32_t c = 0;
-    bool ok_all = true, redo = true, wbad = false;
-    uint32_t fin = 0, wcnt = 0;
-    uint64_t xfin = X, wexit = 0;
-    for (uint32_t att = 0;; ++att) {
-        // ---- wave-local relaxation from (jl, xw): the first time, and again
-        // for a wave whose speculated entry was wrong ----
-        if (redo && jl < 64) {
-            wbad = false;
-            const bool act = in_piece && lane >= jl;
-            uint32_t ev = (act && g != NO_GUESS && !w.dead && (lane == jl || chain)) ? rel(w.exit) : 0u;
-            if (lane == jl && g != xw) ev = 0;
-            st = act ? 0u : 3u;
-            bool conv = false;
-            for (uint32_t r = 0; r < LW_WROUNDS; ++r) {
-                if (a.sdiag && tid == 0) ++s.lw_prof[7];
-                const uint32_t m = dpp_max_incl(ev);
-                uint32_t excl = __shfl_up(m, 1, 64);
-                if (lane == 0) excl = 0;
-                const uint32_t seed = lane == jl ? xw : excl;
-                uint32_t nev = ev;
-                if (act) {
-                    if (lane != jl && seed >= segend) {  // jumped over by a record / the exit
-                        st = 1;
-                        nev = 0;
-                    } else if (lane != jl && seed < seg0) {  // not resolved yet: keep the exit
-                        st = 2;
-                    } else {
-                        if (st != 0 || g == NO_GUESS || seed != g) {
-                            g = seed;
-                            lane_walk(data, base, a.len, g, segend, w);
-                        }
-                        st = 0;
-                        nev = w.dead ? 0u : rel(w.exit);
-                    }
-                }
-                const bool changed = nev != ev;
-                ev = nev;
-                if (!__ballot(changed)) {
-                    conv = true;
-                    break;
-                }
-            }
-            const bool walking = act && st == 0;
-            wbad = __ballot(act && (st == 2 || (st == 0 && w.dead)) ) != 0 || !conv;
-            c = walking ? w.cnt : 0u;
-            const unsigned long long wm = __ballot(walking);
-            const uint32_t ll = wm ? 63u - (uint32_t)__clzll((long long)wm) : 0u;
-            const uint64_t le = w.exit;
-            wexit = wm ? (((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(le >> 32), ll) << 32) |
-                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)le, ll))
-                       : xa;
-            wcnt = __builtin_amdgcn_readlane((int)dpp_sum_incl(c), 63);
-        } else if (redo) {
-            st = 3;
-            c = 0;
-            wcnt = 0;
-            wbad = false;
-            wexit = xa;  // pass-through wave (entry past it) or no speculation (~0)
-        }
-        redo = false;
-        LW_STAMP(3);
-        fin = att & 1u;
-        if (lane == 0) {
-            s.lw_wx[fin][wid] = xa;
-            s.lw_wexit[fin][wid] = wexit;
-            s.lw_wcnt[fin][wid] = wcnt;
-            s.lw_wbad[fin][wid] = wbad ? 1u : 0u;
-        }
-        lw_bar();
-        // ---- stitch the waves in order (uniform in every wave) ----
-        uint64_t x = X;
-        uint32_t fix = NW;
-        for (uint32_t v = wje; v < NW; ++v) {
-            if (v * LW_WSPAN >= clen) break;
-            if (s.lw_wx[fin][v] != x || s.lw_wbad[fin][v]) {
-                fix = v;
-                break;
-            }
-            x = s.lw_wexit[fin][v];
-        }
-        if (fix == NW) {
-            xfin = x;
-            break;
-        }
-        if (att == NW || s.lw_wx[fin][fix] == x) {  // entered exactly and still unresolved
-            ok_all = false;
-            break;
-        }
-        if (wid == fix) {  // relax again from the exact entry
-            const uint64_t xe = x - base;
-            xa = x;
-            xw = xe < 0xFFFFFFFFull ? (uint32_t)xe : 0xFFFFFFFFu;
-            jl = xw >= wq1 ? 64u : (xw / SEG) - wid * 64u;
-            redo = true;
-        }
+    lw_wave_sync();
+    const bool chain = tg[lane] != 0;
+    uint32_t jl = je, xw = 0;
+    if (guess) {
+        const unsigned long long lm = __ballot(valid0 && links);
+        const unsigned long long vm = __ballot(valid0);
+        if (!vm) return false;  // nothing that reads as a record: no entry
+        jl = (uint32_t)__ffsll((long long)(lm ? lm : vm)) - 1;
+        xw = __shfl(g, (int)jl, 64);
+        X = cb + xw;
+    } else {
+        xw = (uint32_t)(X - cb);
     }
+    entry = X;
     LW_STAMP(2);
-    if (!ok_all) {
-        lw_bar();
-        return lw_serial(s, a, data, base, clen, X, out, cut, count, exit);
-    }
-    uint32_t pre = dpp_sum_incl(c) - c, tot = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < NW; ++q) {
-        const bool live = q >= wje && q * LW_WSPAN < clen;
-        const uint32_t wc = live ? s.lw_wcnt[fin][q] : 0u;
-        pre += q < wid ? wc : 0u;
-        tot += wc;
-    }
-    count = tot;
-    exit = xfin;
-    LW_STAMP(4);
-    if (out) {
-        for (uint32_t i = 0; i < c; ++i) store_span(out, ~0ull, pre + i, data, base, walk_pos(w, i));
-        LW_STAMP(5);
-        return true;
-    }
-    // probe: the first start >= cut (or the exit if none lies in the window)
-    if (tid == 0) s.lw_best = ~0ull;
-    lw_bar();
-    for (uint32_t i = 0; i < c; ++i) {
-        const uint64_t q = base + walk_pos(w, i);
-        if (q >= cut) {
-            atomicMin(&s.lw_best, (unsigned long long)q);
+    // ---- relaxation from (jl, xw) ----
+    const bool act = in_chunk && lane >= jl;
+    uint32_t ev = (act && valid0 && (lane == jl || chain)) ? rel(w.exit) : 0u;
+    uint32_t st = act ? 0u : 3u;  // 0 walking from g, 1 passed through, 2 waiting, 3 not on the path
+    bool conv = false;
+    for (uint32_t r = 0; r < LW_WROUNDS; ++r) {
+        if (a.sdiag && threadIdx.x == 0) ++s.lw_prof[7];
+        const uint32_t m = dpp_max_incl(ev);
+        uint32_t excl = __shfl_up(m, 1, 64);
+        if (lane == 0) excl = 0;
+        const uint32_t seed = lane == jl ? xw : excl;
+        uint32_t nev = ev;
+        if (act) {
+            if (lane != jl && seed >= segend) {  // jumped over by a record / the exit
+                st = 1;
+                nev = 0;
+            } else if (lane != jl && seed < seg0) {  // not resolved yet: keep the exit
+                st = 2;                              // (resetting it would cost the lanes
+            } else {                                 // after it one round each)
+                if (st != 0 || g == NO_GUESS || seed != g) {
+                    g = seed;
+                    lane_walk(data, cb, a.len, g, segend, w);
+                }
+                st = 0;
+                nev = w.dead ? 0u : rel(w.exit);
+            }
+        }
+        const bool changed = nev != ev;
+        ev = nev;
+        if (!__ballot(changed)) {
+            conv = true;
             break;
         }
     }
-    lw_bar();
-    const uint64_t f = uni((uint64_t)s.lw_best);
-    lw_bar();
-    exit = f != ~0ull ? f : xfin;
+    LW_STAMP(3);
+    const bool walking = act && st == 0;
+    if (!conv || __ballot(act && (st == 2 || (st == 0 && w.dead))))
+        return lw_chunk_serial(a, data, cb, clen, X, out, count, exit, nstores);
+    const uint32_t c = walking ? w.cnt : 0u;
+    const uint32_t incl = dpp_sum_incl(c);
+    count = __builtin_amdgcn_readlane((int)incl, 63);
+    const unsigned long long wm = __ballot(walking);  // the chain's last lane holds the exit
+    const uint32_t ll = 63u - (uint32_t)__clzll((long long)wm);
+    exit = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(w.exit >> 32), ll) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w.exit, ll);
+    if (out) {
+        const uint32_t cmax = __builtin_amdgcn_readlane((int)dpp_max_incl(c), 63);
+        const uint32_t pre = incl - c;
+        for (uint32_t i = 0; i < cmax; ++i)  // one store instruction per step
+            if (i < c) store_span(out, ~0ull, pre + i, data, cb, walk_pos(w, i));
+        nstores = cmax;
+    }
+    LW_STAMP(4);
     return true;
+}
+
+// This wave's quarter [pb, pe) of the batch's pieces, entered at X (exact;
+// LW_GUESS: through the lead-in chunk before pb), streamed chunk by chunk
+// through the wave's two LDS chunk buffers: piece records into sp[], spans
+// into the pieces' scratch slots.  Wave-level; returns ok with the entry
+// used, the exit and the records.
+__device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint8_t* bufs,
+                                          uint16_t* zm, uint32_t* sg, uint8_t* tg, uint32_t pb,
+                                          uint32_t pe, uint64_t X, SpecPiece* sp, uint64_t& entry,
+                                          uint64_t& exit, uint64_t& total) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool lead = X == LW_GUESS;
+    const uint64_t k0 = (uint64_t)pb * LW_CPP - (lead ? 1u : 0u);
+    const uint64_t k1 = (uint64_t)pe * LW_CPP;
+    lw_fetch_chunk(a, k0 * LW_CHUNK, bufs);
+    lw_wait_vm(0);
+    uint64_t x = X, pentry = X;
+    uint32_t pcount = 0;
+    bool ok = true;
+    total = 0;
+    entry = X;
+    for (uint64_t k = k0; k < k1; ++k) {
+        uint8_t* const cur = bufs + ((k - k0) & 1u) * LW_CBUF;
+        uint8_t* const nxt = bufs + ((k - k0 + 1) & 1u) * LW_CBUF;
+        if (k + 1 < k1) lw_fetch_chunk(a, (k + 1) * LW_CHUNK, nxt);  // in flight meanwhile
+        lw_chunk_masks(cur, zm);
+        LW_STAMP(0);
+        const uint64_t cb = k * LW_CHUNK;
+        const uint32_t clen = a.stop > cb ? (uint32_t)min((uint64_t)LW_CHUNK, a.stop - cb) : 0u;
+        const bool is_lead = lead && k == k0;
+        const uint64_t piece = k / LW_CPP;
+        hg_span* out = is_lead ? nullptr : a.scratch + (size_t)piece * MAX_REC_PIECE + pcount;
+        uint64_t en = 0, ex = 0;
+        uint32_t cnt = 0, nst = 0;
+        if (!lw_chunk(s, a, cur, zm, sg, tg, cb, clen, x, out, en, cnt, ex, nst)) {
+            ok = false;
+            break;
+        }
+        if (is_lead) {
+            entry = ex;
+            x = ex;
+            LW_STAMP(6);
+        } else {
+            if (k % LW_CPP == 0) pentry = x;
+            pcount += cnt;
+            total += cnt;
+            if (k % LW_CPP == LW_CPP - 1 || k + 1 == k1) {
+                if (lane == 0) {
+                    SpecPiece o;
+                    o.x = pentry;
+                    o.R = 0;
+                    o.kl = o.vl = 0;
+                    o.count = pcount;
+                    o.pad = SP_HOP;
+                    sp[piece] = o;
+                }
+                pcount = 0;
+            }
+            x = ex;
+        }
+        // chunk k + 1 landed: its DMA was issued before nst span stores and
+        // (at a piece end) the piece record
+        lw_wait_vm(nst + ((!is_lead && (k % LW_CPP == LW_CPP - 1 || k + 1 == k1)) ? 1u : 0u));
+    }
+    lw_wait_vm(0);  // no DMA may land after the stream is done with its buffers
+    exit = x;
+    return ok;
 }
 
 // Stage piece i of the batch (held in v) into LDS with its halo.
@@ -2322,99 +2284,76 @@ __device__ __forceinline__ void spec_stage(SpecSmem& s, const uint4 (&v)[GPT], u
             threadIdx.x == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
 }
 
-// The lane-walk batch [p0, p0 + np): piece 0 is staged, v holds piece 1's
-// loads.  On success fills sp[] (SP_HOP pieces: entry, count; spans in the
-// piece's scratch slot) and returns true with X0 = entry, X = exit, total.
-// All threads call it.
+// The lane-walk batch [p0, p0 + np): wave w streams pieces [p0 + w*q, +q)
+// (q = ceil(np / 4)); the first wave enters at the batch's entry (the table's
+// for the first batch, else through its lead-in), the others through their
+// lead-ins; then the quarters are stitched (a quarter entered off its
+// predecessor's exit is streamed again from it).  On success X0 = entry, X =
+// exit, total = records.  All threads call it (the pieces staged by the
+// caller are not used: every chunk is fetched again, L2-warm).
 __device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const DecodeArgs& a,
-                                         uint32_t p0, uint32_t np, SpecPiece* sp, uint4 (&v)[GPT],
-                                         uint64_t& X0, uint64_t& X, uint64_t& total) {
-    const uint32_t tid = threadIdx.x;
-    const uint64_t base0 = (uint64_t)p0 * PIECE;
-    uint8_t* const buf0 = reinterpret_cast<uint8_t*>(s.data64);
-    uint8_t* const buf1 = reinterpret_cast<uint8_t*>(alt);
+                                         uint32_t p0, uint32_t np, SpecPiece* sp, uint64_t& X0,
+                                         uint64_t& X, uint64_t& total) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    uint8_t* const bufs = wid < 2 ? reinterpret_cast<uint8_t*>(s.data64) + wid * 2 * LW_CBUF
+                                  : reinterpret_cast<uint8_t*>(alt) + (wid - 2) * 2 * LW_CBUF;
+    uint16_t* const zm = s.lw_zm[wid];
+    uint32_t* const sg = s.lw_sg + wid * 64;
+    uint8_t* const tg = s.lw_tg + wid * 64;
     if (tid == 0) {
-        s.lw_nser = 0;
         for (uint32_t k = 0; k < LW_PROF; ++k) s.lw_prof[k] = 0;
         s.lw_last = __builtin_amdgcn_s_memtime();
     }
-    // piece 1's loads are in v (the caller put them in flight): into buf1
-    if (np > 1) {
-#pragma unroll
-        for (uint32_t q = 0; q < GPT; ++q)
-            *reinterpret_cast<uint4*>(buf1 + (q * THREADS + tid) * 16) = v[q];
-        if (tid < 4)
-            *reinterpret_cast<uint4*>(buf1 + PIECE + tid * 16) =
-                tid == 0 ? s.halo[1] : make_uint4(0, 0, 0, 0);
-    }
-    __syncthreads();
-    uint64_t x = a.entry;
-    total = 0;
+    __syncthreads();  // the caller is done with the staged piece (data64)
+    const uint32_t q = (np + NW - 1) / NW;
+    const uint32_t pb = p0 + min(wid * q, np), pe = p0 + min((wid + 1) * q, np);
+    uint64_t xin = (wid == 0 && p0 == 0) ? a.entry : LW_GUESS;
+    bool exact = xin != LW_GUESS;
+    uint64_t en = 0, ex = 0, tot = 0;
+    bool okw = true, run = pb < pe;
     bool ok = true;
-    // Piece i lives in buf(i & 1); piece i + 1 is DMA'd into the other buffer
-    // while piece i is walked.  Step -1 (batches after the first) is the entry
-    // guess through a lead-in: the window [base0 - LW_LEAD, +PIECE) is staged
-    // in buf0 (L2-warm bytes), a guess in it is walked exactly to the first
-    // start >= base0 -- a wrong lead-in guess has re-joined the true path by
-    // then almost always, where a guess made at base0 itself is wrong about
-    // once per thousand batches (each costs the batch its pre-pass).  Piece 0
-    // is then staged again.  One call site of lw_piece for both uses.
-    for (int i = p0 > 0 ? -1 : 0; i < (int)np; ++i) {
-        const uint64_t base = i < 0 ? base0 - LW_LEAD : (uint64_t)(p0 + i) * PIECE;
-        uint8_t* const cur = (i > 0 && (i & 1)) ? buf1 : buf0;  // the window (i = -1): buf0
-        if (i < 0 || (i == 0 && p0 > 0)) {  // window / piece 0 again (L2-warm), plain loads
-            lw_bar();
-            lw_plain_stage(a, base, cur);
-        } else if (i >= 2) {  // DMA'd during piece i - 1 (the table's last piece: plain)
-            lw_wait_vm();
-            if (base + PIECE > a.rlen) lw_plain_stage(a, base, cur);
+    uint64_t x = 0;
+    uint32_t flast = 0;
+    for (uint32_t att = 0;; ++att) {  // one call site of lw_stream (first pass and re-streams)
+        if (run) okw = lw_stream(s, a, bufs, zm, sg, tg, pb, pe, xin, sp, en, ex, tot);
+        run = false;
+        const uint32_t f = att & 1u;
+        flast = f;
+        if (lane == 0) {
+            s.lw_wx[f][wid] = en;
+            s.lw_wexit[f][wid] = ex;
+            s.lw_wcnt[f][wid] = (uint32_t)tot;
+            s.lw_wbad[f][wid] = (okw ? 0u : 1u) | (exact ? 2u : 0u) | (pb < pe ? 4u : 0u);
         }
-        lw_bar();  // staged bytes visible
-        lw_zm_from_lds(s, cur);
-        if (i >= 1 && (uint32_t)i + 1 < np) {  // piece i + 1 into the other buffer
-            const uint64_t nbase = base + PIECE;
-            uint8_t* const nxt = (i & 1) ? buf0 : buf1;
-            if (nbase + PIECE <= a.rlen) lw_dma_piece(a, nbase, nxt);
-            if (tid < 4)
-                *reinterpret_cast<uint4*>(nxt + PIECE + tid * 16) =
-                    tid == 0 ? s.halo[i + 1] : make_uint4(0, 0, 0, 0);
-        }
-        lw_bar();  // masks visible
-        LW_STAMP(0);
-        const uint32_t clen = piece_clen(a, base);
-        if (i < 0) {
-            x = lw_entry_guess(s, a, cur, base, clen);
-            if (x == ~0ull) {
-                ok = false;
+        __syncthreads();
+        // stitch in order (uniform in every wave)
+        uint32_t fix = NW;
+        total = 0;
+        for (uint32_t v = 0; v < NW; ++v) {
+            const uint32_t fl = s.lw_wbad[f][v];
+            if (!(fl & 4u)) continue;  // no pieces
+            const bool entered = v == 0 || s.lw_wx[f][v] == x;
+            if ((fl & 1u) || !entered) {  // unresolved, or entered off the exact exit
+                if (v == 0 || (fl & 2u)) ok = false;  // exact entry and still unresolved
+                else fix = v;
                 break;
             }
+            x = s.lw_wexit[f][v];
+            total += s.lw_wcnt[f][v];
         }
-        uint32_t cnt = 0;
-        uint64_t ex = 0;
-        hg_span* out = i < 0 ? nullptr : a.scratch + (size_t)(p0 + i) * MAX_REC_PIECE;
-        if (!lw_piece(s, a, cur, base, clen, x, out, cnt, ex, base0)) {
-            ok = false;
+        if (!ok || fix == NW || att == NW) {
+            if (fix != NW) ok = false;
             break;
         }
-        if (i < 0) LW_STAMP(6);
-        if (i >= 0) {
-            if (tid == 0) {
-                SpecPiece o;
-                o.x = x;
-                o.R = 0;
-                o.kl = o.vl = 0;
-                o.count = cnt;
-                o.pad = SP_HOP;
-                sp[p0 + i] = o;
-            }
-            total += cnt;
-        } else {
-            X0 = ex;
+        if (wid == fix) {  // stream the quarter again from the exact entry
+            exact = true;
+            xin = x;
+            run = true;
         }
-        if (i == 0) X0 = x;
-        x = ex;
+        x = 0;
     }
-    lw_wait_vm();  // no DMA may land after this batch is done with the buffers
+    LW_STAMP(5);
+    X0 = s.lw_wx[flast][0];
     X = x;
     if (ok && a.sdiag && tid == 0)
         for (uint32_t k = 0; k < LW_PROF; ++k) a.sdiag[(size_t)(p0 / a.sbp) * LW_PROF + k] = s.lw_prof[k];
@@ -2459,7 +2398,7 @@ __device__ __forceinline__ bool stride_geom(const uint8_t* data, uint64_t base, 
 
 __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
     __shared__ SpecSmem s;
-    __shared__ uint64_t lw_alt[(PIECE + 64) / 8];  // lane-walk mode's second piece buffer
+    __shared__ uint64_t lw_alt[(PIECE + 512) / 8];  // lane-walk chunk buffers of waves 2 and 3
     const uint32_t tid = threadIdx.x;
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     const uint32_t b = blk;
@@ -2525,7 +2464,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         bad = 0;
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
         if (!ok && s.hcode == SB_HOP_SMALL) {  // small records: lane walks over the staged pieces
-            ok = lw_batch(s, lw_alt, a, p0, np, sp, v, X0, X, total);
+            ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total);
             if (tid == 0) s.hcode = ok ? SB_LW : SB_LW_DEAD;
         }
     }
@@ -2540,7 +2479,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         o.count = (uint32_t)total;
         o.ok = ok ? 1u : 0u;
         o.pad = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
-        if (hop && (s.hcode == SB_LW || s.hcode == SB_LW_DEAD)) o.pad |= (uint64_t)s.lw_nser << 32;
         sb[b] = o;
         atomicAdd(&a.gsum[b / SPEC_GROUP], (unsigned long long)total);
         if (!ok || (b == 0 && X0 != a.entry)) mark_bad(a.ctl, a.nspec, b);

@@ -23,7 +23,7 @@ from horreum_amd import abi  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
 
 PIECE, BATCH_MIN, SPEC_BP_MIN, DIAG_WORDS, LW_PROF = 16384, 16, 4, 24, 8
-NAMES = ["stage", "guess_walk", "chain", "rounds", "scan", "store", "leadin", "nrounds"]
+NAMES = ["fetch_masks", "guess_walk", "chain", "relax", "store", "stitch", "leadin", "nrounds"]
 
 
 def main():
