@@ -1620,6 +1620,8 @@ struct SpecSmem {
     uint64_t lw_wexit[2][NW];
     uint32_t lw_wcnt[2][NW];
     uint32_t lw_wbad[2][NW];
+    uint64_t lw_px[NW][SPEC_BP / NW];  // per wave: entries / records of its quarter's pieces
+    uint32_t lw_pc[NW][SPEC_BP / NW];
     uint32_t lw_prof[8];      // diagnostics (a.sdiag): cycles per lane-walk phase, see LW_STAMP
     uint64_t lw_last;
 };
@@ -1896,7 +1898,7 @@ constexpr uint32_t LW_CPP = PIECE / LW_CHUNK;   // chunks per piece
 static_assert(LW_ZM_WORDS == LW_CHUNK / 16 + 8, "lane-walk mask rows");
 static_assert(4 * LW_CBUF <= PIECE + 512, "two waves' chunk buffers per piece buffer");
 constexpr uint32_t LW_WROUNDS = 64;             // relaxation rounds before lane 0 walks it
-constexpr uint32_t LW_TRIES = 3;                // candidates a lane examines for its guess
+constexpr uint32_t LW_TRIES = 2;                // candidates a lane examines for its guess
 constexpr uint32_t LW_PROF = 8;
 constexpr uint64_t LW_GUESS = ~0ull;            // "enter at the first linked lane guess"
 // Diagnostics (a.sdiag != null, tools/lw_diag.py): lane 0 of wave 0 charges the
@@ -2215,6 +2217,10 @@ __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint
                                           uint32_t pe, uint64_t X, SpecPiece* sp, uint64_t& entry,
                                           uint64_t& exit, uint64_t& total) {
     const uint32_t lane = threadIdx.x & 63u;
+    // piece records of the quarter, kept in LDS until the stream ends so the
+    // chunk loop issues no vector memory operations besides its span stores
+    uint64_t* const px = s.lw_px[threadIdx.x >> 6];
+    uint32_t* const pc = s.lw_pc[threadIdx.x >> 6];
     const bool lead = X == LW_GUESS;
     const uint64_t k0 = (uint64_t)pb * LW_CPP - (lead ? 1u : 0u);
     const uint64_t k1 = (uint64_t)pe * LW_CPP;
@@ -2250,25 +2256,30 @@ __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint
             if (k % LW_CPP == 0) pentry = x;
             pcount += cnt;
             total += cnt;
-            if (k % LW_CPP == LW_CPP - 1 || k + 1 == k1) {
+            if (k % LW_CPP == LW_CPP - 1 || k + 1 == k1) {  // piece record: written at the end
                 if (lane == 0) {
-                    SpecPiece o;
-                    o.x = pentry;
-                    o.R = 0;
-                    o.kl = o.vl = 0;
-                    o.count = pcount;
-                    o.pad = SP_HOP;
-                    sp[piece] = o;
+                    px[piece - pb] = pentry;
+                    pc[piece - pb] = pcount;
                 }
                 pcount = 0;
             }
             x = ex;
         }
-        // chunk k + 1 landed: its DMA was issued before nst span stores and
-        // (at a piece end) the piece record
-        lw_wait_vm(nst + ((!is_lead && (k % LW_CPP == LW_CPP - 1 || k + 1 == k1)) ? 1u : 0u));
+        lw_wait_vm(nst);  // chunk k + 1 landed: its DMA was issued before the nst span stores
     }
     lw_wait_vm(0);  // no DMA may land after the stream is done with its buffers
+    if (ok) {
+        lw_wave_sync();
+        for (uint32_t i = lane; i < pe - pb; i += 64) {
+            SpecPiece o;
+            o.x = px[i];
+            o.R = 0;
+            o.kl = o.vl = 0;
+            o.count = pc[i];
+            o.pad = SP_HOP;
+            sp[pb + i] = o;
+        }
+    }
     exit = x;
     return ok;
 }
