@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""Time bench.py's config-5-scaled compaction leg alone (decode -> merge ->
+encode of 8 x 1 M-record tables in HBM) and print its JSON line; with
+--kernels also prints the merge's per-kernel split (hipEvents around the
+merge call are not split per kernel: use rocprofv3 for that)."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+from horreum_amd.engine import Engine  # noqa: E402
+
+
+def main():
+    eng = Engine(0)
+    dev = eng.device
+    eng.set_stream(torch.cuda.current_stream(dev))
+    line = bench.compaction_leg(torch, eng, dev, 1, 0)
+    line["merge_path"] = "k-way buckets" if os.environ.get("HG_MERGE_KWAY") == "1" else "pairwise rounds"
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
