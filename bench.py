@@ -637,8 +637,9 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     """BASELINE config 5 scaled to one GPU's share: 8 sorted tables of 1 M
     records (16 B keys / 100 B values, 132 MB each), 25 % of each table's keys
     shared by all tables.  Decode all, device merge (newest wins), encode the
-    merged table; the merge needs the record counts on the host, so the leg
-    is timed end to end with its two host syncs.  With `host`, also the
+    merged table: one hg_compact_dev call, timed end to end (its host sync
+    for the record counts -- the merge is launched from them -- and the final
+    one for the results included).  With `host`, also the
     end-to-end rate from host memory (cfg 5 asks for H2D/D2H included):
     hg_compact_host on pageable copies of the same tables (H2D of every
     table, decode, merge, encode, D2H of the compacted table), median of 3."""
@@ -660,25 +661,12 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     for o, b in zip(offs_b, bufs):
         arena[o:o + b.numel()] = b
     del bufs
-    caps = [sz // 16 for sz in sizes]
-    span_t = [eng.empty(c * 16) for c in caps]
-    nmax = sum(caps)
-    pairs = eng.empty(nmax * 24)
     out = eng.empty(total)
-    eng.reserve(max(sizes), nmax)
-
-    tabs = [arena[o:o + sz] for o, sz in zip(offs_b, sizes)]
-    dres = eng.empty(24 * ntab)
 
     def run():
-        # one batched decode chain for all tables, one sync for the counts
-        eng.decode_batch_dev_async(tabs, sizes, span_t, caps, dres)
-        r = dres.cpu().numpy()
-        counts = [int(r[24 * i:24 * i + 8].view("<u8")[0]) for i in range(ntab)]
-        assert all(int(r[24 * i + 8:24 * i + 12].view("<i4")[0]) == 0 for i in range(ntab))
-        m = eng.merge_dev(arena, offs_b, span_t, counts, pairs, nmax)
-        rc, out_len = eng.encode_dev(arena, pairs, m.n, out=out, cap=total)
-        return m, out_len
+        c = eng.compact_dev(arena, offs_b, sizes, out)
+        assert c.status == 0, c
+        return c, c.data.numel()
 
     run()
     torch.cuda.synchronize(device)
@@ -691,12 +679,12 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
         times.append(time.perf_counter() - t0)
     wall = max_over_ranks(sorted(times)[1], world, device)
     in_bytes = sum(sizes)
-    del arena, span_t, pairs, out, tabs, dres
+    del arena, out
     torch.cuda.empty_cache()
     line = {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
             "tables": ntab, "input_bytes_per_gpu": in_bytes, "merged_records": int(m.n),
             "merged_bytes": int(out_len), "ms": round(wall * 1e3, 3),
-            "status": int(m.status)}
+            "status": int(m.status), "api": "hg_compact_dev"}
     if hosts is not None:
         hout = np.empty(in_bytes, dtype=np.uint8)  # caller-owned output, reused
         eng.compact_host(hosts, out=hout)  # warm-up (staging buffers, workspaces)

@@ -117,6 +117,11 @@ _PROTOS = {
     "hg_host_is_pinned": (ctypes.c_int, [_vp]),
     "hg_compact_host": (ctypes.c_int, [_vp, _u32, _vp, _vp, _u8p, _u64, ctypes.POINTER(_u64),
                                        _u32, _vp, ctypes.POINTER(HgMergeResult)]),
+    # compact_dev(ctx, ntables, arena, arena_len, table_off*, lens*, out, cap, out_len*, stride,
+    #             blocks, result*)
+    "hg_compact_dev": (ctypes.c_int, [_vp, _u32, _u8p, _u64, _vp, _vp, _u8p, _u64,
+                                      ctypes.POINTER(_u64), _u32, _vp,
+                                      ctypes.POINTER(HgMergeResult)]),
     # range decode(ctx, sst, len, begin, stop, entry, spans, cap, [n*, exit*, err* | result])
     "hg_decode_range_dev_async": (ctypes.c_int, [_vp, _u8p, _u64, _u64, _u64, _u64, _vp, _u64,
                                                  _vp]),

@@ -397,9 +397,14 @@ struct LookbackOut {
 __device__ LookbackOut lookback(const DecodeArgs& a, uint32_t k, uint32_t& spins_out) {
     const uint32_t lane = threadIdx.x & 63u;
     LookbackOut r{0, 0, 0, HG_OK};
-    uint32_t spins = 0;
+    // The budget bounds each wait (a restart waits for a newer batch, so a
+    // legitimately long chain of restarts does not add up to a false error);
+    // spins_out reports the total.
+    uint32_t spins = 0, spins_done = 0;
     const uint32_t SPIN_LIMIT = 1u << 22;
 restart:
+    spins_done += spins;
+    spins = 0;
     int64_t j0 = (int64_t)k - 1;
     uint64_t acc = 0, xk = 0;
     bool first = true;
@@ -424,7 +429,7 @@ restart:
             if (!(notready & relevant)) break;
             if (++spins > SPIN_LIMIT) {
                 r.err = HG_ERR_INTERNAL;
-                spins_out = spins;
+                spins_out = spins_done + spins;
                 return r;
             }
             __builtin_amdgcn_s_sleep(1);
@@ -437,7 +442,7 @@ restart:
                 r.err = (int32_t)__shfl(st_aux(w0), fi, 64) - 16;
                 r.errpos = __shfl(E, fi, 64);
                 r.g = __shfl(st_val(w1), fi, 64);
-                spins_out = spins;
+                spins_out = spins_done + spins;
                 return r;
             }
         }
@@ -459,7 +464,7 @@ restart:
                 if (st_flag(v0) == st_flag(v1) && st_flag(v0) >= ST_INCL) break;
                 if (++spins > SPIN_LIMIT) {
                     r.err = HG_ERR_INTERNAL;
-                    spins_out = spins;
+                    spins_out = spins_done + spins;
                     return r;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -471,7 +476,7 @@ restart:
         if (fi < 64) {
             r.g = __shfl(st_val(w1), fi, 64) + acc;
             r.x = xk;
-            spins_out = spins;
+            spins_out = spins_done + spins;
             return r;
         }
         first = false;

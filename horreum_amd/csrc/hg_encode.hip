@@ -49,10 +49,16 @@ constexpr uint32_t ENC_PRE = HG_ENC_PRE;  // pieces per lane loaded before the l
 #define HG_ENC_NT 1
 #endif
 typedef uint32_t enc_u32x4 __attribute__((ext_vector_type(4)));
-// Arena bytes are read once and output bytes written once: nontemporal
-// (HG_ENC_NT=0: default policy, for A/B runs).
+// Output bytes are written once: nontemporal stores (HG_ENC_NT=0: default
+// policy, for A/B runs).  Arena bytes are read once when the pairs walk the
+// arena in order (a table's own records): nontemporal loads.  Pairs that
+// gather records from several tables (a compaction's merged order) read each
+// source line in two or more visits (a 132-byte record spans two lines, the
+// neighbouring records of its table come a few pieces later): default-policy
+// loads keep those lines in L2 (cfg 5 leg: encode 552 -> 420 us).
+template <bool NTL>
 __device__ __forceinline__ uint4 ld_stream16(const uint8_t* p) {
-    if (HG_ENC_NT) {
+    if (HG_ENC_NT && NTL) {
         const enc_u32x4 x = __builtin_nontemporal_load(reinterpret_cast<const enc_u32x4*>(p));
         return make_uint4(x.x, x.y, x.z, x.w);
     }
@@ -80,7 +86,12 @@ struct EncodeArgs {
     hg_encode_result* result;
     const uint64_t* tile_sum;    // output bytes of every tile (encode_sums_kernel)
     const uint64_t* group_base;  // output offset of every ENC_GROUP tiles (encode_bases_kernel)
+    const uint64_t* n_dev;       // optional: records = min(n, *n_dev) (a merge's device count)
 };
+
+__device__ __forceinline__ uint64_t enc_count(uint64_t n, const uint64_t* n_dev) {
+    return n_dev ? min(n, *n_dev) : n;
+}
 
 struct EncodeSmem {
     uint64_t key_off[ENC_TILE], val_off[ENC_TILE], off[ENC_TILE + 1];
@@ -260,10 +271,13 @@ __device__ __forceinline__ void enc_store(const EncodeSmem& s, const EncodeArgs&
     store_part(dst, w, (uint32_t)min((uint64_t)nb, room));
 }
 
+template <bool NTL>
 __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
     __shared__ EncodeSmem s;
     const uint32_t tid = threadIdx.x;
     const uint32_t t = blockIdx.x;
+    a.n = enc_count(a.n, a.n_dev);
+    if ((uint64_t)t * ENC_TILE >= a.n) return;  // grid sized for the upper bound
     const uint64_t r0 = (uint64_t)t * ENC_TILE + (uint64_t)tid * ENC_RPT;  // this thread's records
 
     // ---- 1. descriptors, sizes, piece counts ----------------------------------
@@ -361,7 +375,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
 #pragma unroll
     for (uint32_t k = 0; k < ENC_PRE; ++k) {
         pre[k] = enc_resolve(s, a, tid + k * ENC_THREADS, ptot, nrec, pscale, un);
-        vpre[k] = ld_stream16(pre[k].kind == 2 ? pre[k].src : safe);
+        vpre[k] = ld_stream16<NTL>(pre[k].kind == 2 ? pre[k].src : safe);
     }
     if (tid < 64) {
         const uint32_t g = t / ENC_GROUP, j = t % ENC_GROUP;
@@ -386,7 +400,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
 #pragma unroll
     for (uint32_t u = 0; u < ENC_U; ++u) {
         cur[u] = enc_resolve(s, a, p0 + u * ENC_THREADS, ptot, nrec, pscale, un);
-        vc[u] = ld_stream16(cur[u].kind == 2 ? cur[u].src : safe);
+        vc[u] = ld_stream16<NTL>(cur[u].kind == 2 ? cur[u].src : safe);
     }
 #pragma unroll
     for (uint32_t k = 0; k < ENC_PRE; ++k) enc_store(s, a, pre[k], vpre[k], tb);
@@ -394,7 +408,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
 #pragma unroll
         for (uint32_t u = 0; u < ENC_U; ++u) {
             n[u] = enc_resolve(s, a, pb + STEP + u * ENC_THREADS, ptot, nrec, pscale, un);
-            vnext[u] = ld_stream16(n[u].kind == 2 ? n[u].src : safe);
+            vnext[u] = ld_stream16<NTL>(n[u].kind == 2 ? n[u].src : safe);
         }
 #pragma unroll
         for (uint32_t u = 0; u < ENC_U; ++u) enc_store(s, a, c[u], vcur[u], tb);
@@ -411,9 +425,11 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
 // (gsum zeroed before launch).
 __global__ __launch_bounds__(ENC_THREADS) void encode_sums_kernel(const hg_pair* pairs,
                                                                   uint64_t n, uint64_t* tsum,
-                                                                  unsigned long long* gsum) {
+                                                                  unsigned long long* gsum,
+                                                                  const uint64_t* n_dev) {
     __shared__ uint64_t part[ENC_NW];
     const uint32_t tid = threadIdx.x, t = blockIdx.x;
+    n = enc_count(n, n_dev);
     uint64_t sz = 0;
 #pragma unroll
     for (uint32_t i = 0; i < ENC_RPT; ++i) {
@@ -490,9 +506,10 @@ __global__ __launch_bounds__(BASES_THREADS) void encode_bases_kernel(uint64_t* g
 // The table's total length comes from `res` (device) or, with res null, `total`.
 __global__ void blocks_kernel(const uint64_t* rec_off, uint64_t n, uint32_t stride,
                               const hg_encode_result* res, uint64_t total, hg_block* blocks,
-                              uint64_t nb) {
+                              uint64_t nb, const uint64_t* n_dev) {
     const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= nb) return;
+    n = enc_count(n, n_dev);
+    if (b >= nb || b * stride >= n) return;
     const uint64_t first = b * stride;
     const uint64_t nxt = first + stride;
     const uint64_t pos = rec_off[first];
@@ -517,11 +534,15 @@ extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t n) {
 // workspace).  Three launches: tile sums, their scan (+ the result), copy.
 // rec_base is added to every record offset written (0 for a whole table; the
 // chunk's output offset when a host encode runs the table in chunks).
-extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
-                                    uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
-                                    uint64_t rec_base, uint32_t block_stride, hg_block* d_blocks,
-                                    hg_encode_result* d_result, unsigned long long* d_status,
-                                    hipStream_t stream) {
+// d_n (optional): the record count is min(n, *d_n), read on the device -- a
+// merge's output count, so merge and encode run without a host round trip
+// (grids are sized for n).  gather: pairs point into several tables (merged
+// order), sources are read with the default cache policy.
+extern "C" int hgk_encode_launch_ex(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                                    const uint64_t* d_n, bool gather, uint8_t* d_out, uint64_t cap,
+                                    uint64_t* d_rec_off, uint64_t rec_base, uint32_t block_stride,
+                                    hg_block* d_blocks, hg_encode_result* d_result,
+                                    unsigned long long* d_status, hipStream_t stream) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
@@ -534,7 +555,7 @@ extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pai
     }
     if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_HIP_FAIL;
     hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
-                       d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum));
+                       d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum), d_n);
     if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng, cap,
                        d_result);
@@ -550,17 +571,30 @@ extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pai
     a.result = d_result;
     a.tile_sum = tsum;
     a.group_base = gsum;
-    hipLaunchKernelGGL(encode_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream, a);
+    a.n_dev = d_n;
+    if (gather)
+        hipLaunchKernelGGL(encode_kernel<false>, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream, a);
+    else
+        hipLaunchKernelGGL(encode_kernel<true>, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream, a);
     if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     if (d_blocks) {
         const uint64_t nb = (n + block_stride - 1) / block_stride;
         const uint32_t grid = (uint32_t)((nb + 255) / 256);
         hipLaunchKernelGGL(blocks_kernel, dim3(grid), dim3(256), 0, stream, d_rec_off, n,
                            block_stride, (const hg_encode_result*)d_result, (uint64_t)0, d_blocks,
-                           nb);
+                           nb, d_n);
         if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     }
     return HG_OK;
+}
+
+extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                                    uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
+                                    uint64_t rec_base, uint32_t block_stride, hg_block* d_blocks,
+                                    hg_encode_result* d_result, unsigned long long* d_status,
+                                    hipStream_t stream) {
+    return hgk_encode_launch_ex(d_arena, d_pairs, n, nullptr, false, d_out, cap, d_rec_off,
+                                rec_base, block_stride, d_blocks, d_result, d_status, stream);
 }
 
 extern "C" int hgk_encode_launch(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
@@ -582,7 +616,8 @@ extern "C" int hgk_encode_blocks_launch(const uint64_t* d_rec_off, uint64_t n,
     const uint64_t nb = (n + block_stride - 1) / block_stride;
     const uint32_t grid = (uint32_t)((nb + 255) / 256);
     hipLaunchKernelGGL(blocks_kernel, dim3(grid), dim3(256), 0, stream, d_rec_off, n, block_stride,
-                       (const hg_encode_result*)nullptr, total, d_blocks, nb);
+                       (const hg_encode_result*)nullptr, total, d_blocks, nb,
+                       (const uint64_t*)nullptr);
     return HG_LAUNCH_STATUS();
 }
 
@@ -602,7 +637,8 @@ extern "C" int hgk_encode_size_launch(const hg_pair* d_pairs, uint64_t n,
                    : HG_HIP_FAIL;
     if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_HIP_FAIL;
     hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
-                       d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum));
+                       d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum),
+                       (const uint64_t*)nullptr);
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng,
                        ~0ull, d_result);
     return HG_LAUNCH_STATUS();

@@ -28,6 +28,9 @@ extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t);
 extern "C" int hgk_encode_launch_at(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
                                     uint64_t*, uint64_t, uint32_t, hg_block*, hg_encode_result*,
                                     unsigned long long*, hipStream_t);
+extern "C" int hgk_encode_launch_ex(const uint8_t*, const hg_pair*, uint64_t, const uint64_t*, bool,
+                                    uint8_t*, uint64_t, uint64_t*, uint64_t, uint32_t, hg_block*,
+                                    hg_encode_result*, unsigned long long*, hipStream_t);
 extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
                                         hipStream_t);
 extern "C" int hgk_encode_size_launch(const hg_pair*, uint64_t, hg_encode_result*, unsigned long long*,
@@ -71,7 +74,7 @@ struct hg_ctx {
     hgi::DevBuf results;   // hg_decode_result + hg_encode_result
     hgi::PinBuf hres;      // pinned mirror of `results`
     // host-path staging (device side)
-    hgi::DevBuf d_in, d_out, d_aux;
+    hgi::DevBuf d_in, d_out, d_aux, d_blk;
     hgi::PinBuf h_stage[2];
     // merge: workspace, result, pinned argument staging and its reuse event
     hgi::DevBuf mws, mres, mspans, mpairs;
@@ -98,6 +101,9 @@ namespace hgi {
 int set_dev(hg_ctx* c);
 int ensure(hg_ctx* c, DevBuf& b, size_t bytes);
 int ensure_pin(PinBuf& b, size_t bytes);
+int rt_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                  uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
+                  hg_block* d_blocks, uint64_t* out_len, bool gather);
 int ensure_aux(hg_ctx* c, int want);
 bool host_pinned(const void* p);
 int h2d_pipelined(hg_ctx* c, void* dst, const void* src, size_t bytes);

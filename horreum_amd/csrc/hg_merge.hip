@@ -14,8 +14,8 @@
 // big-endian key prefix (one 128-bit compare decides almost every pair), the
 // key length and a (table, record) reference; only keys that agree on their
 // first 16 bytes and are both longer fetch the rest from HBM.
-//   1. merge_prep_kernel: one entry per record (runs laid out table by table).
-//   2. merge_check_kernel: each table strictly increasing (else step 5).
+//   1. merge_prep_kernel: one entry per record (runs laid out table by table),
+//   2. and in the same pass: each table strictly increasing (else step 5).
 //   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
 //      positions, takes its A/B split from merge_split_kernel (a binary
@@ -98,9 +98,7 @@ __device__ __forceinline__ uint32_t run_of(const MergeArgs& a, uint64_t g) {
     return lo;
 }
 
-__global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* e) {
-    const uint64_t g = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
-    if (g >= a.n) return;
+__device__ __forceinline__ MEnt make_ent(const MergeArgs& a, uint64_t g) {
     const uint32_t t = run_of(a, g);
     const uint64_t rec = g - a.run_off[t];
     // spans and key bytes are read once: nontemporal 16-byte loads
@@ -136,18 +134,31 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
     m.klen = sp.klen;
     m.tdead = t;
     m.rec = rec;
-    e[g] = m;
+    return m;
 }
 
-// ---- 2. each table strictly increasing ----------------------------------------------
-// err[0] = lowest offending global entry index (initialised to ~0).
-__global__ __launch_bounds__(THREADS) void merge_check_kernel(MergeArgs a, const MEnt* e,
-                                                              unsigned long long* err) {
-    const uint64_t g = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
-    if (g >= a.n || g == 0) return;
-    const MEnt cur = e[g], prev = e[g - 1];
-    if ((cur.tdead & ~DEAD) != (prev.tdead & ~DEAD)) return;  // first record of a table
-    if (key_cmp(a, prev, cur) >= 0) atomicMin(err, (unsigned long long)g);
+// One entry per record, and (step 2, fused) each table strictly increasing:
+// an entry is compared with its predecessor in the same table -- the
+// neighbouring thread's entry through LDS, or for the workgroup's first
+// entry the predecessor rebuilt.  err[0] = lowest offending global entry
+// index (initialised to ~0).
+__global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* e,
+                                                             unsigned long long* err) {
+    __shared__ MEnt sh[THREADS];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t g = (uint64_t)blockIdx.x * THREADS + tid;
+    const bool ok = g < a.n;
+    MEnt m;
+    if (ok) {
+        m = make_ent(a, g);
+        e[g] = m;
+        sh[tid] = m;
+    }
+    __syncthreads();
+    if (!ok || g == 0) return;
+    const MEnt prev = tid ? sh[tid - 1] : make_ent(a, g - 1);
+    if (prev.tdead != m.tdead) return;  // first record of a table
+    if (key_cmp(a, prev, m) >= 0) atomicMin(err, (unsigned long long)g);
 }
 
 // ---- 3. one merge round ---------------------------------------------------------------
@@ -189,9 +200,6 @@ __device__ uint64_t merge_path(const MergeArgs& a, const MEnt* A, uint64_t na, c
     return lo;
 }
 
-#ifndef HG_MERGE_SEQ
-#define HG_MERGE_SEQ 1  // 0: place every element by a binary search in the other segment
-#endif
 struct LevelSmem {
     MEnt seg[TILE + 2];      // A segment then B segment
     MEnt aprev;              // A element just before the tile's A segment
@@ -265,16 +273,81 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
     split[t] = i;
 }
 
+// The last round (two runs -> one) emits the hg_pairs itself (step 4 fused):
+// each tile counts its live entries, takes the live entries of the tiles
+// before it by a decoupled look-back over per-tile status words, and writes
+// its pairs at their final positions; the last tile writes the result.
+struct FinalArgs {
+    unsigned long long* st;  // [ntiles] look-back status (zeroed): flag << 62 | live count
+    hg_pair* out;
+    uint64_t cap;
+    hg_merge_result* result;
+    uint32_t ntiles;
+};
+constexpr unsigned long long LB_AGG = 1ull << 62, LB_INCL = 2ull << 62;
+constexpr unsigned long long LB_VAL = (1ull << 62) - 1;
+
+// Live entries of the tiles before tile t (wave 0; every lane gets it) and
+// publication of this tile's inclusive count.  A wait that exceeds its budget
+// flags the merge (err) so the exact loop redoes it: never an endless spin.
+__device__ uint64_t final_lookback(const FinalArgs& f, uint32_t t, uint64_t agg,
+                                   unsigned long long* err) {
+    const uint32_t lane = threadIdx.x & 63u;
+    if (t == 0) {
+        if (lane == 0) hgk::st_agent(&f.st[0], LB_INCL | agg);
+        return 0;
+    }
+    if (lane == 0) hgk::st_agent(&f.st[t], LB_AGG | agg);
+    uint64_t acc = 0;
+    int64_t j0 = (int64_t)t - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t j = j0 - (int64_t)lane;
+        unsigned long long w = j >= 0 ? hgk::ld_agent(&f.st[j]) : LB_INCL;
+        unsigned long long incl, rel;
+        for (;;) {
+            incl = __ballot((w >> 62) == 2);
+            const int fi = incl ? __ffsll((long long)incl) - 1 : 63;
+            rel = fi >= 63 ? ~0ull : ((1ull << (fi + 1)) - 1ull);
+            if (!(__ballot((w >> 62) == 0) & rel)) break;
+            if (++spins > (1u << 22)) {
+                if (lane == 0) {
+                    atomicMin(err, 0ull);
+                    hgk::st_agent(&f.st[t], LB_INCL | agg);
+                }
+                return 0;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            if (j >= 0 && (w >> 62) == 0) w = hgk::ld_agent(&f.st[j]);
+        }
+        acc += hgk::wave_sum<uint64_t>(((rel >> lane) & 1ull) ? (w & LB_VAL) : 0ull);
+        if (incl) break;
+        j0 -= 64;
+    }
+    if (lane == 0) hgk::st_agent(&f.st[t], LB_INCL | (acc + agg));
+    return acc;
+}
+
 // err: the order check's result; merging unsorted runs is meaningless (and
 // their merge paths are not monotone), so every round skips work once set.
+// FINAL: the last round, emitting pairs (f) instead of entries (out unused).
+template <bool FINAL>
 __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, LevelArgs l,
                                                               const MEnt* in, MEnt* out,
                                                               const uint64_t* split,
-                                                              unsigned long long* err) {
+                                                              unsigned long long* err,
+                                                              FinalArgs f) {
     __shared__ LevelSmem s;
+    __shared__ uint32_t fin_tmp[THREADS / 64];
+    __shared__ uint64_t fin_base;
     const uint32_t tid = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
     if (t0 >= a.n) return;
+    // A FINAL tile that stops early still publishes its status (count 0), so
+    // no later tile waits on it; the exact loop then redoes the merge.
+    auto fin_abort = [&]() {
+        if (FINAL && tid < 64) final_lookback(f, blockIdx.x, 0, err);
+    };
     // The error word is loaded with the splits (one round trip) and tested
     // before anything is staged: once the order check failed the splits are
     // all 0 and the segments they imply run past the runs' ends.
@@ -291,8 +364,11 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         const MEnt* A = in + o;
         const MEnt* B = in + amid;
         const uint64_t na = amid - o, nb = oend - amid;
-        if (nb == 0) {  // odd run out: copied as is
-            if (err0 != ~0ull) return;
+        if (nb == 0) {  // odd run out: copied as is (never in the FINAL round)
+            if (err0 != ~0ull) {
+                fin_abort();
+                return;
+            }
             for (uint64_t d = d0 + tid; d < d1; d += THREADS) out[d] = in[d];
             d0 = d1;
             __syncthreads();
@@ -303,11 +379,15 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         // is fetched with the segments
         const uint64_t i0 = d0 == t0 ? split[blockIdx.x] : 0;
         const uint64_t i1 = d1 == oend ? na : split[blockIdx.x + 1];
-        if (err0 != ~0ull) return;  // an earlier check or round found unsorted input
+        if (err0 != ~0ull) {  // an earlier check or round found unsorted input
+            fin_abort();
+            return;
+        }
         if (i1 < i0 || i0 > d0 - o || i1 > d1 - o || (d1 - o) - i1 < (d0 - o) - i0) {
             // splits of sorted runs are monotone; anything else means the
             // input was not sorted: flag it (the exact loop takes over) and stop
             if (tid == 0) atomicMin(err, (unsigned long long)o);
+            fin_abort();
             return;
         }
         const uint64_t j0 = (d0 - o) - i0, j1 = (d1 - o) - i1;
@@ -322,7 +402,6 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         const MEnt* SA = s.seg;
         const MEnt* SB = s.seg + nA;
         MEnt* dst = out + d0;
-#if HG_MERGE_SEQ
         // Merge path inside the tile: thread tid owns outputs [tid*EPT, +EPT),
         // finds how many of them come from A by one binary search on its
         // diagonal (A first on equal keys, as merge_split_kernel), then merges
@@ -330,6 +409,8 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         {
             const uint32_t nt = nA + nB;
             const uint32_t d = tid * EPT;
+            MEnt fx[FINAL ? EPT : 1];
+            uint32_t fcnt = 0;
             if (d < nt) {
                 uint32_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
                 while (lo < hi) {
@@ -339,7 +420,10 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                 }
                 uint32_t ai = lo, bj = d - lo;
                 const uint32_t e = min(d + EPT, nt);
-                for (uint32_t q = d; q < e; ++q) {
+#pragma unroll
+                for (uint32_t k = 0; k < EPT; ++k) {  // constant indices: fx stays in VGPRs
+                    const uint32_t q = d + k;
+                    if (q >= e) break;
                     MEnt x;
                     if (bj >= nB || (ai < nA && key_cmp(a, SA[ai], SB[bj]) <= 0)) {
                         x = SA[ai++];
@@ -351,29 +435,54 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                                                : (s.has_prev && key_cmp(a, s.aprev, x) == 0);
                         if (eq) x.tdead |= DEAD;
                     }
-                    dst[q] = x;
+                    if (FINAL) {
+                        fx[FINAL ? k : 0] = x;
+                        fcnt += (x.tdead & DEAD) ? 0u : 1u;
+                    } else {
+                        dst[q] = x;
+                    }
+                }
+            }
+            if (FINAL) {
+                // live entries before this thread's in the tile, the tiles'
+                // before it (look-back), then the pairs at their positions
+                uint32_t ftot;
+                const uint32_t fpre = hgk::block_excl_scan<THREADS / 64>(fcnt, fin_tmp, ftot);
+                if (tid < 64) {
+                    const uint64_t b = final_lookback(f, blockIdx.x, ftot, err);
+                    if (tid == 0) {
+                        fin_base = b;
+                        if (blockIdx.x + 1 == f.ntiles) {
+                            hg_merge_result r;
+                            r.n_out = b + ftot;
+                            r.kind = HG_OK;
+                            r.table = 0;
+                            r.index = 0;
+                            *f.result = r;
+                        }
+                    }
+                }
+                __syncthreads();
+                uint64_t pos = fin_base + fpre;
+                const uint32_t e = d < nt ? min(d + EPT, nt) : d;
+#pragma unroll
+                for (uint32_t k = 0; k < (FINAL ? EPT : 1); ++k) {
+                    if (d + k >= e) break;
+                    const MEnt& x = fx[k];
+                    if (x.tdead & DEAD) continue;
+                    if (pos < f.cap) {
+                        const hg_span sp = a.spans[x.tdead][x.rec];
+                        hg_pair p;
+                        p.key_off = a.table_off[x.tdead] + sp.off + 16;
+                        p.val_off = p.key_off + sp.klen;
+                        p.klen = sp.klen;
+                        p.vlen = sp.vlen;
+                        f.out[pos] = p;
+                    }
+                    ++pos;
                 }
             }
         }
-#else
-        for (uint32_t q = tid; q < nA + nB; q += THREADS) {
-            MEnt x = s.seg[q];
-            uint32_t pos;
-            if (q < nA) {
-                pos = q + lds_bound(a, SB, nB, x, false);
-            } else {
-                const uint32_t jb = q - nA;
-                const uint32_t ub = lds_bound(a, SA, nA, x, true);
-                pos = jb + ub;
-                // newest wins: an equal key in A (inside the tile, or the A
-                // element just before it) kills this lower-priority copy
-                const bool eq_in = ub > 0 && key_cmp(a, SA[ub - 1], x) == 0;
-                const bool eq_prev = ub == 0 && s.has_prev && key_cmp(a, s.aprev, x) == 0;
-                if (eq_in || eq_prev) x.tdead |= DEAD;
-            }
-            dst[pos] = x;
-        }
-#endif
         d0 = d1;
         __syncthreads();
     }
@@ -500,7 +609,7 @@ __global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const 
 // only the loop itself defines the output, so one wave runs it: lane l owns
 // tables l, l + 64, ...; their head entries live in a per-table state array;
 // a butterfly over (key, table) picks the winner in every lane.  Runs only
-// when merge_check_kernel found a table that is not strictly increasing.
+// when merge_prep_kernel found a table that is not strictly increasing.
 struct ExactHead {  // 48 bytes per table
     MEnt e;         // current head entry (valid when idx < cnt)
     uint64_t idx, cnt;
@@ -889,7 +998,7 @@ extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
     using namespace hgm;
     const uint64_t ntiles = (n + TILE - 1) / TILE + 1;
     uint64_t b = 2 * ((n * sizeof(MEnt) + 255) & ~255ull);
-    b += ((ntiles * 4 + 255) & ~255ull) + ((ntiles * 8 + 255) & ~255ull);
+    b += ((ntiles * 4 + 255) & ~255ull) + 2 * ((ntiles * 8 + 255) & ~255ull);
     b += ((4 * (uint64_t)ntables + 64) * 8 + 255) & ~255ull;  // device copy of the staging
     b += 256;                                                  // error word
     b += ((uint64_t)ntables * sizeof(ExactHead) + 255) & ~255ull;  // exact-loop heads
@@ -967,6 +1076,8 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     p += ((ntiles + 1) * 4 + 255) & ~255ull;
     uint64_t* tile_base = reinterpret_cast<uint64_t*>(p);
     p += ((ntiles + 1) * 8 + 255) & ~255ull;
+    unsigned long long* lb_status = reinterpret_cast<unsigned long long*>(p);
+    p += ((ntiles + 1) * 8 + 255) & ~255ull;
     uint64_t* d_stage = reinterpret_cast<uint64_t*>(p);
     p += (stage_words * 8 + 255) & ~255ull;
     unsigned long long* err = reinterpret_cast<unsigned long long*>(p);
@@ -992,9 +1103,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                    : HG_HIP_FAIL;
     }
     const uint32_t g1 = (uint32_t)((n + THREADS - 1) / THREADS);
-    hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, e0);
-    hipLaunchKernelGGL(merge_check_kernel, dim3(g1), dim3(THREADS), 0, stream, a,
-                       (const MEnt*)e0, err);
+    hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, e0, err);
     if (kway) {  // the second entry buffer holds the bucket bounds and the merged order
         KwArgs w;
         w.S = S;
@@ -1027,6 +1136,14 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     MEnt* nxt = e1;
     const uint64_t* roff = a.run_off;
     uint64_t nruns = ntables;
+    FinalArgs fa;
+    fa.st = lb_status;
+    fa.out = d_out;
+    fa.cap = cap;
+    fa.result = d_result;
+    fa.ntiles = (uint32_t)ntiles;
+    if (ntables >= 2 && hipMemsetAsync(lb_status, 0, ntiles * 8, stream) != hipSuccess)
+        return HG_HIP_FAIL;
     while (nruns > 1) {
         LevelArgs l;
         l.roff = roff;
@@ -1035,13 +1152,24 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         const uint32_t gs = (uint32_t)((ntiles + 1 + THREADS - 1) / THREADS);
         hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
                            (const MEnt*)cur, tile_base, ntiles, (const unsigned long long*)err);
-        hipLaunchKernelGGL(merge_level_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
-                           l, (const MEnt*)cur, nxt, (const uint64_t*)tile_base, err);
+        if (nruns == 2)  // the last round emits the pairs
+            hipLaunchKernelGGL(merge_level_kernel<true>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
+                               stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)tile_base,
+                               err, fa);
+        else
+            hipLaunchKernelGGL(merge_level_kernel<false>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
+                               stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)tile_base,
+                               err, fa);
         roff += nruns + 1;
         nruns = (nruns + 1) / 2;
         MEnt* t = cur;
         cur = nxt;
         nxt = t;
+    }
+    if (ntables >= 2) {  // pairs and result written by the last round
+        hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)e0,
+                           (const unsigned long long*)err, heads, d_out, cap, d_result);
+        return HG_LAUNCH_STATUS();
     }
     hipLaunchKernelGGL(merge_count_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
                        (const MEnt*)cur, tile_live);

@@ -544,10 +544,10 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
             if ((rr = ensure(c, c->d_out, arena_len ? arena_len : 1)) != HG_OK ||
                 (rr = ensure(c, c->d_aux, (mr.n_out ? mr.n_out : 1) * sizeof(uint64_t))) != HG_OK)
                 return rr;
-            rr = hg_encode_dev(c, static_cast<const uint8_t*>(c->d_in.p),
+            rr = rt_encode_dev(c, static_cast<const uint8_t*>(c->d_in.p),
                                static_cast<const hg_pair*>(c->mpairs.p), mr.n_out,
                                static_cast<uint8_t*>(c->d_out.p), arena_len,
-                               static_cast<uint64_t*>(c->d_aux.p), 0, nullptr, &enc);
+                               static_cast<uint64_t*>(c->d_aux.p), 0, nullptr, &enc, true);
             if (rr != HG_OK) return rr;
             O[g].bytes = enc;
         }

@@ -153,7 +153,7 @@ int hg_ctx_destroy(hg_ctx* c) {
     if (!c) return HG_ERR_INVALID_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->mws,
+    for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
                       &c->bws, &c->bstage_d, &c->x_res, &c->x_aux})
         if (b->p) hipFree(b->p);
@@ -691,9 +691,10 @@ int hg_encoded_size(hg_ctx* c, const hg_pair* pairs, uint64_t n, uint64_t* bytes
 }
 
 // ---- encode ------------------------------------------------------------------
-int hg_encode_dev_async(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
-                        uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
-                        hg_block* d_blocks, hg_encode_result* d_result) {
+static int encode_dev_async_ex(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs,
+                               uint64_t n, uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
+                               uint32_t block_stride, hg_block* d_blocks,
+                               hg_encode_result* d_result, bool gather) {
     if (!c || !d_result || (n && !d_pairs) || (cap && !d_out)) return HG_ERR_INVALID_ARG;
     if (d_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;  // slice::chunks(0) panics
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
@@ -707,15 +708,28 @@ int hg_encode_dev_async(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pair
         if ((r = ensure(c, c->recoff, n * sizeof(uint64_t))) != HG_OK) return r;
         d_rec_off = static_cast<uint64_t*>(c->recoff.p);
     }
-    return hgk_encode_launch(d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride, d_blocks,
-                             d_result, reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+    return hgk_encode_launch_ex(d_arena, d_pairs, n, nullptr, gather, d_out, cap, d_rec_off, 0,
+                                block_stride, d_blocks, d_result,
+                                reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
 }
 
-int hg_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+int hg_encode_dev_async(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                        uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
+                        hg_block* d_blocks, hg_encode_result* d_result) {
+    return encode_dev_async_ex(c, d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride,
+                               d_blocks, d_result, false);
+}
+
+}  // extern "C"
+
+namespace hgi {
+// hg_encode_dev; gather: the pairs are a merge's output (records of several
+// tables in key order), read with the default cache policy.
+int rt_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
                   uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
-                  hg_block* d_blocks, uint64_t* out_len) {
-    int r = hg_encode_dev_async(c, d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride,
-                                d_blocks, c ? eres(c) : nullptr);
+                  hg_block* d_blocks, uint64_t* out_len, bool gather) {
+    int r = encode_dev_async_ex(c, d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride,
+                                d_blocks, c ? eres(c) : nullptr, gather);
     if (r != HG_OK) return r;
     if (hipMemcpyAsync(c->hres.p, eres(c), sizeof(hg_encode_result), hipMemcpyDeviceToHost,
                        c->stream) != hipSuccess ||
@@ -724,6 +738,16 @@ int hg_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uin
     const hg_encode_result res = *reinterpret_cast<hg_encode_result*>(c->hres.p);
     if (out_len) *out_len = res.out_len;
     return res.kind;
+}
+}  // namespace hgi
+
+extern "C" {
+
+int hg_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                  uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
+                  hg_block* d_blocks, uint64_t* out_len) {
+    return hgi::rt_encode_dev(c, d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride,
+                              d_blocks, out_len, false);
 }
 
 // Host encode with page-locked buffers, in chunks of ~256 MiB of output: the
@@ -924,6 +948,112 @@ int hg_merge_dev(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t a
     return res.n_out > cap ? HG_ERR_CAPACITY : HG_OK;
 }
 
+// Decode -> merge -> encode of tables already in one device arena.  One host
+// sync for the record counts (the merge's launch geometry needs them); the
+// encode reads the merge's output count on the device (grids sized for the
+// input count), so merge and encode run back to back; one sync at the end for
+// the results.  *enc = encoded bytes (0 unless the merge succeeded).
+static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint64_t arena_len,
+                        const uint64_t* toff, const uint64_t* lens, uint8_t* d_out, uint64_t cap,
+                        uint64_t* enc, uint32_t block_stride, hg_block* d_blk,
+                        hg_merge_result* res) {
+    *enc = 0;
+    *res = hg_merge_result{0, HG_OK, 0, 0};
+    uint64_t span_cap = 0;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        if (lens[t] >= kMaxLen) return HG_ERR_TOO_LARGE;
+        if (toff[t] > arena_len || lens[t] > arena_len - toff[t]) return HG_ERR_INVALID_ARG;
+        span_cap += lens[t] / 16;
+    }
+    std::vector<const uint8_t*> dt(ntables);
+    std::vector<hg_span*> ds(ntables);
+    std::vector<const hg_span*> sp(ntables);
+    std::vector<uint64_t> caps(ntables), counts(ntables, 0);
+    std::vector<hg_decode_result> hr(ntables);
+    int r = ensure(c, c->mspans, (span_cap ? span_cap : 1) * sizeof(hg_span));
+    if (r == HG_OK) r = ensure(c, c->d_aux, ntables * sizeof(hg_decode_result) + 64);
+    if (r != HG_OK) return r;
+    hg_span* spans = static_cast<hg_span*>(c->mspans.p);
+    for (uint32_t t = 0; t < ntables; ++t) {
+        dt[t] = arena + toff[t];
+        ds[t] = spans;
+        sp[t] = spans;
+        caps[t] = lens[t] / 16;
+        spans += caps[t];
+    }
+    // 1. one batched decode chain for all tables, one sync for the counts
+    if (ntables) {
+        hg_decode_result* dr = static_cast<hg_decode_result*>(c->d_aux.p);
+        r = hg_decode_batch_dev_async(c, ntables, dt.data(), lens, ds.data(), caps.data(), dr);
+        if (r == HG_OK &&
+            (hipMemcpyAsync(hr.data(), dr, ntables * sizeof(hg_decode_result),
+                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+             hipStreamSynchronize(c->stream) != hipSuccess))
+            r = HG_HIP_FAIL;
+        if (r != HG_OK) return r;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            if (hr[t].kind != HG_OK) {  // the reference's read_all unwrap (storage.rs:64-66)
+                *res = hg_merge_result{0, hr[t].kind, t, hr[t].err_offset};
+                return hr[t].kind;
+            }
+            counts[t] = hr[t].n_records;
+        }
+    }
+    // 2. merge -> pairs; 3. encode (+ blocks) of the merge's device count
+    uint64_t nm = 0;
+    for (uint32_t t = 0; t < ntables; ++t) nm += counts[t];
+    r = ensure(c, c->mpairs, (nm ? nm : 1) * sizeof(hg_pair));
+    if (r == HG_OK) r = ensure(c, c->mres, 128);
+    if (r == HG_OK) r = ensure(c, c->ws, hgk_encode_workspace_bytes(nm ? nm : 1));
+    if (r == HG_OK && d_blk) r = ensure(c, c->recoff, (nm ? nm : 1) * sizeof(uint64_t));
+    if (r != HG_OK) return r;
+    hg_merge_result* dres_m = static_cast<hg_merge_result*>(c->mres.p);
+    hg_encode_result* dres_e =
+        reinterpret_cast<hg_encode_result*>(static_cast<char*>(c->mres.p) + 64);
+    hg_pair* pairs = static_cast<hg_pair*>(c->mpairs.p);
+    r = hg_merge_dev_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm,
+                           dres_m);
+    if (r != HG_OK) return r;
+    if (nm == 0) {
+        if (hipMemsetAsync(dres_e, 0, sizeof(hg_encode_result), c->stream) != hipSuccess)
+            return HG_HIP_FAIL;
+    } else {
+        r = hgk_encode_launch_ex(arena, pairs, nm, &dres_m->n_out, true, d_out, cap,
+                                 d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, 0,
+                                 block_stride, d_blk, dres_e,
+                                 reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+        if (r != HG_OK) return r;
+    }
+    char* h = static_cast<char*>(c->hres.p);
+    if (hipMemcpyAsync(h, c->mres.p, 128, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        return HG_HIP_FAIL;
+    *res = *reinterpret_cast<const hg_merge_result*>(h);
+    const hg_encode_result er = *reinterpret_cast<const hg_encode_result*>(h + 64);
+    if (res->kind != HG_OK) return res->kind;
+    if (res->n_out > nm) return HG_ERR_INTERNAL;  // the merge never grows the record count
+    *enc = er.out_len;
+    return er.kind;
+}
+
+int hg_compact_dev(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
+                   const uint64_t* table_off, const uint64_t* lens, uint8_t* d_out, uint64_t cap,
+                   uint64_t* out_len, uint32_t block_stride, hg_block* d_blocks,
+                   hg_merge_result* result) {
+    if (!c || (ntables && (!d_arena || !table_off || !lens)) || (cap && !d_out))
+        return HG_ERR_INVALID_ARG;
+    if (d_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (out_len) *out_len = 0;
+    uint64_t enc = 0;
+    hg_merge_result res;
+    const int r = compact_core(c, ntables, d_arena, arena_len, table_off, lens, d_out, cap, &enc,
+                               block_stride, d_blocks, &res);
+    if (out_len) *out_len = enc;
+    if (result) *result = res;
+    return r;
+}
+
 int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
                     const uint64_t* lens, uint8_t* h_out, uint64_t cap, uint64_t* out_len,
                     uint32_t block_stride, hg_block* h_blocks, hg_merge_result* result) {
@@ -932,107 +1062,47 @@ int hg_compact_host(hg_ctx* c, uint32_t ntables, const uint8_t* const* h_tables,
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     hg_merge_result res{0, HG_OK, 0, 0};
     if (out_len) *out_len = 0;
-    // 1. all tables into one device arena (8-byte aligned starts), spans per table
-    uint64_t total = 0, span_cap = 0;
-    uint64_t* toff = new (std::nothrow) uint64_t[ntables + 1];
-    uint64_t* sofs = new (std::nothrow) uint64_t[ntables + 1];
-    uint64_t* counts = new (std::nothrow) uint64_t[ntables + 1];
-    const hg_span** sp = new (std::nothrow) const hg_span*[ntables + 1];
-    int r = (toff && sofs && counts && sp) ? HG_OK : HG_ERR_INTERNAL;
+    // 1. all tables into one device arena (8-byte aligned starts)
+    uint64_t total = 0;
+    std::vector<uint64_t> toff(ntables + 1);
+    int r = HG_OK;
     for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
         if (lens[t] && !h_tables[t]) r = HG_ERR_INVALID_ARG;
         if (lens[t] >= kMaxLen) r = HG_ERR_TOO_LARGE;
         toff[t] = total;
         total += (lens[t] + 7) & ~7ull;
-        sofs[t] = span_cap;
-        span_cap += lens[t] / 16;
     }
     if (r == HG_OK) r = ensure(c, c->d_in, total ? total : 1);
-    if (r == HG_OK) r = ensure(c, c->mspans, (span_cap ? span_cap : 1) * sizeof(hg_span));
+    if (r == HG_OK) r = ensure(c, c->d_out, total ? total : 1);  // output <= input bytes
     char* arena = static_cast<char*>(c->d_in.p);
-    hg_span* spans = static_cast<hg_span*>(c->mspans.p);
-    // every table up, then one batched decode chain for all of them and one
-    // sync for the record counts (the merge needs them on the host)
-    for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
-        sp[t] = spans + sofs[t];
-        counts[t] = 0;
+    for (uint32_t t = 0; r == HG_OK && t < ntables; ++t)
         if (lens[t]) r = rt_h2d_pipelined(c, arena + toff[t], h_tables[t], lens[t]);
+    // 2. decode, merge, encode on the device
+    uint64_t enc = 0, nb = 0;
+    hg_block* d_blk = nullptr;
+    if (r == HG_OK && h_blocks) {
+        uint64_t bound = 0;  // block entries: at most one per block_stride input records
+        for (uint32_t t = 0; t < ntables; ++t) bound += lens[t] / 16;
+        r = ensure(c, c->d_blk, (hg_block_count(bound, block_stride) + 1) * sizeof(hg_block));
+        d_blk = static_cast<hg_block*>(c->d_blk.p);
     }
-    if (r == HG_OK && ntables) {
-        const uint8_t** dt = new (std::nothrow) const uint8_t*[ntables];
-        hg_span** ds = new (std::nothrow) hg_span*[ntables];
-        uint64_t* caps = new (std::nothrow) uint64_t[ntables];
-        hg_decode_result* hr = new (std::nothrow) hg_decode_result[ntables];
-        r = (dt && ds && caps && hr) ? HG_OK : HG_ERR_INTERNAL;
-        if (r == HG_OK) r = ensure(c, c->d_aux, ntables * sizeof(hg_decode_result) + 64);
-        for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
-            dt[t] = reinterpret_cast<const uint8_t*>(arena + toff[t]);
-            ds[t] = spans + sofs[t];
-            caps[t] = lens[t] / 16;
-        }
-        hg_decode_result* dr = static_cast<hg_decode_result*>(c->d_aux.p);
-        if (r == HG_OK) r = hg_decode_batch_dev_async(c, ntables, dt, lens, ds, caps, dr);
-        if (r == HG_OK &&
-            (hipMemcpyAsync(hr, dr, ntables * sizeof(hg_decode_result), hipMemcpyDeviceToHost,
-                            c->stream) != hipSuccess ||
-             hipStreamSynchronize(c->stream) != hipSuccess))
-            r = HG_HIP_FAIL;
-        for (uint32_t t = 0; r == HG_OK && t < ntables; ++t) {
-            if (hr[t].kind != HG_OK) {  // the reference's read_all unwrap (storage.rs:64-66)
-                res = hg_merge_result{0, hr[t].kind, t, hr[t].err_offset};
-                r = hr[t].kind;
-                break;
-            }
-            counts[t] = hr[t].n_records;
-        }
-        delete[] dt;
-        delete[] ds;
-        delete[] caps;
-        delete[] hr;
-    }
-    // 2. merge -> pairs into the arena
-    uint64_t nm = 0;
+    if (r == HG_OK)
+        r = compact_core(c, ntables, reinterpret_cast<const uint8_t*>(arena), total, toff.data(),
+                         lens, static_cast<uint8_t*>(c->d_out.p), total, &enc, block_stride, d_blk,
+                         &res);
+    // 3. the compacted table (and its index blocks) back to the host
     if (r == HG_OK) {
-        for (uint32_t t = 0; t < ntables; ++t) nm += counts[t];
-        r = ensure(c, c->mpairs, (nm ? nm : 1) * sizeof(hg_pair));
-    }
-    if (r == HG_OK) {
-        r = hg_merge_dev(c, ntables, reinterpret_cast<const uint8_t*>(arena), total, toff, sp,
-                         counts, static_cast<hg_pair*>(c->mpairs.p), nm, &res);
-    }
-    // 3. encode the merged records (+ index blocks) and copy them out
-    if (r == HG_OK) {
-        const uint64_t n = res.n_out;
-        uint64_t enc = 0;
-        // encoded size = sum of the selected records' sizes (from the pairs)
-        const uint64_t nb = h_blocks ? hg_block_count(n, block_stride) : 0;
-        r = ensure(c, c->d_aux, n * sizeof(uint64_t) + nb * sizeof(hg_block) + 64);
-        hg_block* d_blk = h_blocks ? reinterpret_cast<hg_block*>(static_cast<char*>(c->d_aux.p) +
-                                                                  n * sizeof(uint64_t))
-                                   : nullptr;
-        // out size is only known after the merge: upper bound = input bytes
-        if (r == HG_OK) r = ensure(c, c->d_out, total ? total : 1);
-        if (r == HG_OK)
-            r = hg_encode_dev(c, reinterpret_cast<const uint8_t*>(arena),
-                              static_cast<const hg_pair*>(c->mpairs.p), n,
-                              static_cast<uint8_t*>(c->d_out.p), total,
-                              static_cast<uint64_t*>(c->d_aux.p), block_stride, d_blk, &enc);
-        if (r == HG_OK) {
-            if (out_len) *out_len = enc;
-            if (enc > cap) {
-                r = HG_ERR_CAPACITY;
-            } else {
-                if (enc) r = rt_d2h_pipelined(c, h_out, c->d_out.p, enc);
-                if (r == HG_OK && h_blocks && nb)
-                    r = rt_d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block));
-            }
+        if (out_len) *out_len = enc;
+        nb = h_blocks ? hg_block_count(res.n_out, block_stride) : 0;
+        if (enc > cap) {
+            r = HG_ERR_CAPACITY;
+        } else {
+            if (enc) r = rt_d2h_pipelined(c, h_out, c->d_out.p, enc);
+            if (r == HG_OK && h_blocks && nb)
+                r = rt_d2h_pipelined(c, h_blocks, d_blk, nb * sizeof(hg_block));
         }
     }
     if (result) *result = res;
-    delete[] toff;
-    delete[] sofs;
-    delete[] counts;
-    delete[] sp;
     return r;
 }
 

@@ -395,6 +395,31 @@ class Engine:
         return CompactOut(rc, out[:out_len.value], blocks[:nbo] if blocks is not None else None,
                           res.n_out, res.kind, res.table, res.index)
 
+    def compact_dev(self, arena, table_off, lens, out, block_stride=0, blocks=None):
+        """compact_host on tables already in device tensor `arena` (table t =
+        arena[table_off[t], +lens[t]), priority order: newest first).  Writes
+        the compacted SSTable to device tensor `out` (and, with block_stride,
+        its index blocks to device tensor `blocks`); returns CompactOut whose
+        `data` is the written prefix of `out` (blocks: the written prefix of
+        `blocks`, as hg_block records in a uint8 tensor)."""
+        k = len(lens)
+        toff = (ctypes.c_uint64 * max(k, 1))(*[int(x) for x in table_off])
+        ln = (ctypes.c_uint64 * max(k, 1))(*[int(x) for x in lens])
+        out_len = ctypes.c_uint64()
+        res = HgMergeResult()
+        rc = self.lib.hg_compact_dev(self.ctx, k, _ptr(arena),
+                                     arena.numel() if arena is not None else 0,
+                                     ctypes.cast(toff, ctypes.c_void_p),
+                                     ctypes.cast(ln, ctypes.c_void_p), _ptr(out),
+                                     out.numel() if out is not None else 0, ctypes.byref(out_len),
+                                     int(block_stride), _ptr(blocks), ctypes.byref(res))
+        if rc in (Status.HIP, Status.INVALID_ARG, Status.INTERNAL, Status.TOO_LARGE):
+            raise HorreumGpuError(rc, "hg_compact_dev")
+        nbo = int(self.lib.hg_block_count(res.n_out, block_stride)) if block_stride else 0
+        return CompactOut(rc, out[:out_len.value] if out is not None else None,
+                          blocks[:nbo * 24] if blocks is not None else None,
+                          res.n_out, res.kind, res.table, res.index)
+
 
 _default = None
 

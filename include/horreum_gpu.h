@@ -297,6 +297,18 @@ int hg_compact_host(hg_ctx* ctx, uint32_t ntables, const uint8_t* const* h_table
                     const uint64_t* lens, uint8_t* h_out, uint64_t cap,
                     uint64_t* out_len, uint32_t block_stride, hg_block* h_blocks,
                     hg_merge_result* result);
+/* hg_compact_host on tables already in device memory: table t is
+ * d_arena[table_off[t], +lens[t]) (one allocation, so a key read never leaves
+ * it); the compacted table goes to d_out (cap bytes) and its index blocks,
+ * when d_blocks is given, to d_blocks (hg_block_count(result->n_out,
+ * block_stride) entries).  Synchronous: one host sync for the decoded record
+ * counts (the merge is launched from them), merge and encode back to back
+ * (the encode reads the merge's output count on the device), one sync for the
+ * results. */
+int hg_compact_dev(hg_ctx* ctx, uint32_t ntables, const uint8_t* d_arena,
+                   uint64_t arena_len, const uint64_t* table_off, const uint64_t* lens,
+                   uint8_t* d_out, uint64_t cap, uint64_t* out_len, uint32_t block_stride,
+                   hg_block* d_blocks, hg_merge_result* result);
 
 /* ---- point lookups ----------------------------------------------------
  * Replaces SSTable::get (src/sstable/table.rs:54-70; Index::get,

@@ -110,6 +110,22 @@ def test_cfg5_small_vs_oracle(engine, stride):
     assert c.status == 0 and c.n == wn and np.array_equal(c.data, want)
     if stride:
         assert np.array_equal(c.blocks, wblocks)
+    # hg_compact_dev (the bench leg's entry point) on the same device arena
+    import torch
+    offs, total = [], 0
+    for b in bufs:
+        offs.append(total)
+        total += (b.numel() + 7) & ~7
+    arena = torch.zeros(total, dtype=torch.uint8, device=engine.device)
+    for o, b in zip(offs, bufs):
+        arena[o:o + b.numel()] = b
+    out = engine.empty(total)
+    blocks = engine.empty(24 * (wn // stride + 2)) if stride else None
+    d = engine.compact_dev(arena, offs, [b.numel() for b in bufs], out, stride, blocks)
+    assert d.status == 0 and d.n == wn
+    assert np.array_equal(d.data.cpu().numpy(), want)
+    if stride:
+        assert np.array_equal(d.blocks.cpu().numpy().view(wblocks.dtype), wblocks)
 
 
 @pytest.mark.timeout(600)

@@ -278,3 +278,40 @@ def test_compact_host_decode_error(engine):
     datas = encode_tables(tables)
     out = engine.compact_host([datas[0].tobytes(), datas[1][:-3].tobytes(), datas[2].tobytes()])
     assert out.kind in (1, 2) and out.status == out.kind and out.table == 1
+
+
+@pytest.mark.parametrize("stride", [0, 7])
+@pytest.mark.parametrize("unsorted", [False, True])
+def test_compact_dev(engine, stride, unsorted):
+    """hg_compact_dev (tables already in one device arena; the encode reads the
+    merge's device count) == serialize_flatten of the oracle's compact_inner
+    output, and its index blocks; also through the exact loop (unsorted)."""
+    import torch
+    tables = sorted_tables(5, 5000, 0.4, 31, long_prefix=True)
+    if unsorted:
+        tables[1] = tables[1][::-1]
+    datas = encode_tables(tables)
+    want, wblocks, wn = oracle.compacted_table(datas, block_stride=stride)
+    offs, total = [], 0
+    for d in datas:
+        offs.append(total)
+        total += (d.size + 7) & ~7
+    host = np.zeros(total, np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + d.size] = d
+    arena = torch.from_numpy(host).to(engine.device)
+    out = engine.empty(total)
+    blocks = engine.empty(24 * (wn // stride + 2)) if stride else None
+    c = engine.compact_dev(arena, offs, [d.size for d in datas], out, stride, blocks)
+    assert c.status == 0 and c.kind == 0 and c.n == wn
+    assert c.table == (1 if unsorted else 0)
+    assert np.array_equal(c.data.cpu().numpy(), want)
+    if stride:
+        assert np.array_equal(c.blocks.cpu().numpy().view(wblocks.dtype), wblocks)
+    # too small an output buffer: HG_ERR_CAPACITY, the full size reported
+    small = engine.empty(max(want.size // 2, 1))
+    c2 = engine.compact_dev(arena, offs, [d.size for d in datas], small)
+    assert c2.status == 5 and c2.n == wn
+    # a table that does not decode: its index and the decoder's error
+    c3 = engine.compact_dev(arena, offs, [d.size for d in datas[:-1]] + [datas[-1].size - 3], out)
+    assert c3.kind in (1, 2) and c3.status == c3.kind and c3.table == len(datas) - 1
