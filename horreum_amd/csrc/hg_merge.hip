@@ -201,7 +201,7 @@ __device__ uint64_t merge_path(const MergeArgs& a, const MEnt* A, uint64_t na, c
 }
 
 struct LevelSmem {
-    MEnt seg[TILE + 2];      // A segment then B segment
+    alignas(16) MEnt seg[TILE + 2];  // A segment then B segment (then the merged output)
     MEnt aprev;              // A element just before the tile's A segment
     uint64_t i0, i1;         // A split at the tile's start / end
     uint32_t has_prev;
@@ -404,12 +404,17 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         MEnt* dst = out + d0;
         // Merge path inside the tile: thread tid owns outputs [tid*EPT, +EPT),
         // finds how many of them come from A by one binary search on its
-        // diagonal (A first on equal keys, as merge_split_kernel), then merges
-        // sequentially and stores EPT consecutive entries (coalesced).
+        // diagonal (A first on equal keys, as merge_split_kernel) and merges
+        // them sequentially into registers.  The merged entries (or, in the
+        // FINAL round, the live records' pairs) then go back into LDS in
+        // output order and out with contiguous 16- / 8-byte stores per lane:
+        // per-thread stores of 32-byte entries at a 128-byte lane stride cost
+        // 20 % extra HBM writes, of 24-byte pairs 2x (rocprofv3 WRITE_SIZE).
         {
             const uint32_t nt = nA + nB;
             const uint32_t d = tid * EPT;
-            MEnt fx[FINAL ? EPT : 1];
+            const uint32_t e = d < nt ? min(d + EPT, nt) : d;
+            MEnt fx[EPT];
             uint32_t fcnt = 0;
             if (d < nt) {
                 uint32_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
@@ -419,11 +424,9 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                     else hi = mid;
                 }
                 uint32_t ai = lo, bj = d - lo;
-                const uint32_t e = min(d + EPT, nt);
 #pragma unroll
                 for (uint32_t k = 0; k < EPT; ++k) {  // constant indices: fx stays in VGPRs
-                    const uint32_t q = d + k;
-                    if (q >= e) break;
+                    if (d + k >= e) break;
                     MEnt x;
                     if (bj >= nB || (ai < nA && key_cmp(a, SA[ai], SB[bj]) <= 0)) {
                         x = SA[ai++];
@@ -435,15 +438,20 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                                                : (s.has_prev && key_cmp(a, s.aprev, x) == 0);
                         if (eq) x.tdead |= DEAD;
                     }
-                    if (FINAL) {
-                        fx[FINAL ? k : 0] = x;
-                        fcnt += (x.tdead & DEAD) ? 0u : 1u;
-                    } else {
-                        dst[q] = x;
-                    }
+                    fx[k] = x;
+                    fcnt += (x.tdead & DEAD) ? 0u : 1u;
                 }
             }
-            if (FINAL) {
+            __syncthreads();  // every thread is done reading the segments
+            if (!FINAL) {
+#pragma unroll
+                for (uint32_t k = 0; k < EPT; ++k)
+                    if (d + k < e) s.seg[d + k] = fx[k];
+                __syncthreads();
+                const uint4* src = reinterpret_cast<const uint4*>(s.seg);
+                uint4* o4 = reinterpret_cast<uint4*>(dst);
+                for (uint32_t i = tid; i < 2 * nt; i += THREADS) o4[i] = src[i];
+            } else {
                 // live entries before this thread's in the tile, the tiles'
                 // before it (look-back), then the pairs at their positions
                 uint32_t ftot;
@@ -462,25 +470,28 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                         }
                     }
                 }
-                __syncthreads();
-                uint64_t pos = fin_base + fpre;
-                const uint32_t e = d < nt ? min(d + EPT, nt) : d;
+                hg_pair* lp = reinterpret_cast<hg_pair*>(s.seg);
+                uint32_t r = fpre;
 #pragma unroll
-                for (uint32_t k = 0; k < (FINAL ? EPT : 1); ++k) {
+                for (uint32_t k = 0; k < EPT; ++k) {
                     if (d + k >= e) break;
                     const MEnt& x = fx[k];
                     if (x.tdead & DEAD) continue;
-                    if (pos < f.cap) {
-                        const hg_span sp = a.spans[x.tdead][x.rec];
-                        hg_pair p;
-                        p.key_off = a.table_off[x.tdead] + sp.off + 16;
-                        p.val_off = p.key_off + sp.klen;
-                        p.klen = sp.klen;
-                        p.vlen = sp.vlen;
-                        f.out[pos] = p;
-                    }
-                    ++pos;
+                    const hg_span sp = a.spans[x.tdead][x.rec];
+                    hg_pair p;
+                    p.key_off = a.table_off[x.tdead] + sp.off + 16;
+                    p.val_off = p.key_off + sp.klen;
+                    p.klen = sp.klen;
+                    p.vlen = sp.vlen;
+                    lp[r++] = p;
                 }
+                __syncthreads();  // also publishes fin_base
+                // the tile's pairs are words [3 base, 3 (base + ftot)) of out
+                const uint64_t w0 = 3 * fin_base, wcap = 3 * f.cap;
+                const uint64_t* s8 = reinterpret_cast<const uint64_t*>(s.seg);
+                uint64_t* o8 = reinterpret_cast<uint64_t*>(f.out);
+                for (uint32_t i = tid; i < 3 * ftot; i += THREADS)
+                    if (w0 + i < wcap) o8[w0 + i] = s8[i];
             }
         }
         d0 = d1;
