@@ -18,7 +18,7 @@
 //   2. and in the same pass: each table strictly increasing (else step 5).
 //   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
-//      positions, takes its A/B split from merge_split_kernel (a binary
+//      positions, takes its A/B split from merge_split_kernel (a 16-ary
 //      search per tile boundary, all boundaries at once), stages
 //      both segments in LDS, and each thread finds its 4 outputs' split by one
 //      binary search on its diagonal and merges them sequentially (ties: A
@@ -38,7 +38,10 @@
 namespace hgm {
 
 constexpr uint32_t THREADS = 256;
-constexpr uint32_t TILE = 1024;      // merged positions per workgroup
+#ifndef HG_MERGE_TILE
+#define HG_MERGE_TILE 1024
+#endif
+constexpr uint32_t TILE = HG_MERGE_TILE;  // merged positions per workgroup
 constexpr uint32_t EPT = TILE / THREADS;
 constexpr uint32_t DEAD = 0x80000000u;
 constexpr uint32_t MAX_TABLES = 1u << 16;
@@ -237,18 +240,20 @@ __device__ __forceinline__ void pair_of(const LevelArgs& l, uint64_t d, uint32_t
 }
 
 // A split (A elements among the merged positions before it) for every tile
-// start of a round, one wave per tile boundary, all boundaries at once: the
-// merge-path searches' dependent HBM probes overlap across the grid instead
-// of sitting at the head of every tile of the round.
-// One lane per boundary, a plain binary search (~20 dependent probes of two
-// entries): the 64-ary wave search moved ~12x the bytes for the same answer
-// and, with every boundary searched at once, was bound by those bytes.
+// start of a round, all boundaries at once: the merge-path searches'
+// dependent HBM probes overlap across the grid instead of sitting at the head
+// of every tile of the round.  SPLIT_G lanes per boundary run a SPLIT_G-ary
+// search (~log16(run) dependent rounds of SPLIT_G probes of two entries):
+// one lane per boundary (a binary search, ~20 dependent probes) was bound by
+// the probes' latency, one wave per boundary (64-ary) by the bytes it moved.
+constexpr uint32_t SPLIT_G = 16;
 __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, LevelArgs l,
                                                               const MEnt* in, uint64_t* split,
                                                               uint64_t nb_tiles,
                                                               const unsigned long long* err) {
-    const uint64_t t = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
-    if (t > nb_tiles) return;
+    const uint32_t lane = threadIdx.x & 63u, j = lane % SPLIT_G, gsh = lane - j;
+    const uint64_t t = ((uint64_t)blockIdx.x * THREADS + threadIdx.x) / SPLIT_G;
+    if (t > nb_tiles) return;  // the whole group
     uint64_t i = 0;
     if (*err == ~0ull) {
         const uint64_t d = min(t * TILE, a.n);
@@ -258,19 +263,29 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
         const uint64_t na = amid - o, nb = oend - amid, dd = d - o;
         if (nb == 0) {
             i = dd;
-        } else {  // first c in [lo, hi) with A[c] > B[dd-c-1] (A[c] not among the first dd)
+        } else {  // first c in [lo, hi] with A[c] > B[dd-c-1] (A[c] not among the first dd)
             const MEnt* A = in + o;
             const MEnt* B = in + amid;
             uint64_t lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                if (key_cmp(a, A[mid], B[dd - mid - 1]) <= 0) lo = mid + 1;
-                else hi = mid;
+            while (lo < hi) {  // uniform within the group
+                const uint64_t span = hi - lo;
+                const uint64_t c = lo + span * j / SPLIT_G;  // < hi
+                const bool after = key_cmp(a, A[c], B[dd - c - 1]) > 0;
+                const uint32_t m =
+                    (uint32_t)(__ballot(after) >> gsh) & ((1u << SPLIT_G) - 1u);
+                if (!m) {
+                    lo = lo + span * (SPLIT_G - 1) / SPLIT_G + 1;
+                } else {
+                    const uint32_t f = (uint32_t)__ffs(m) - 1;
+                    const uint64_t cf = lo + span * f / SPLIT_G;
+                    lo = f ? lo + span * (f - 1) / SPLIT_G + 1 : lo;
+                    hi = cf;
+                }
             }
             i = lo;
         }
     }
-    split[t] = i;
+    if (j == 0) split[t] = i;
 }
 
 // The last round (two runs -> one) emits the hg_pairs itself (step 4 fused):
@@ -1160,7 +1175,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         l.roff = roff;
         l.nruns = (uint32_t)nruns;
         // tile_base is free until the final count/scan: the round's splits
-        const uint32_t gs = (uint32_t)((ntiles + 1 + THREADS - 1) / THREADS);
+        const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
         hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
                            (const MEnt*)cur, tile_base, ntiles, (const unsigned long long*)err);
         if (nruns == 2)  // the last round emits the pairs
