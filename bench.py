@@ -646,10 +646,11 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     from horreum_amd import synth
     rng = np.random.default_rng(5 + 1000 * rank)
     shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64))
-    bufs, offs_b, total = [], [], 0
+    bufs, offs_b, total, n_in = [], [], 0, 0
     for t in range(ntab):
         own = rng.integers(0, 1 << 40, size=per_table - shared.size, dtype=np.uint64)
         keys = np.unique(np.concatenate([shared, own]))
+        n_in += int(keys.size)
         buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=50 + t, device=device)
         bufs.append(buf)
     sizes = [b.numel() for b in bufs]
@@ -684,7 +685,22 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     line = {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
             "tables": ntab, "input_bytes_per_gpu": in_bytes, "merged_records": int(m.n),
             "merged_bytes": int(out_len), "ms": round(wall * 1e3, 3),
-            "status": int(m.status), "api": "hg_compact_dev"}
+            "status": int(m.status), "api": "hg_compact_dev", "input_records": n_in}
+    # algorithmic bytes: read the tables, write the compacted table; spans
+    # (16 B per input record) and pairs (24 B per output record) each written
+    # and read once.  PMC traffic of the same leg from the committed profile.
+    alg = in_bytes + int(out_len) + 2 * 16 * n_in + 2 * 24 * int(m.n)
+    line["algorithmic_bytes"] = alg
+    line["achieved_GBps_alg"] = round(world * alg / wall / 1e9, 1)
+    try:
+        with open(os.path.join(ROOT, "profiles", "r2_pmc_compaction.json"), encoding="utf-8") as f:
+            pc = json.load(f)
+        line["traffic"] = pc.get("traffic_bytes_per_call")
+        line["traffic_over_algorithmic"] = (round(line["traffic"] / alg, 3)
+                                            if line["traffic"] else None)
+        line["traffic_source"] = "profiles/r2_pmc_compaction.json"
+    except (OSError, ValueError):
+        line["traffic"] = None
     if hosts is not None:
         hout = np.empty(in_bytes, dtype=np.uint8)  # caller-owned output, reused
         eng.compact_host(hosts, out=hout)  # warm-up (staging buffers, workspaces)

@@ -2056,6 +2056,52 @@ __device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, uint32_t seg0,
     return NO_GUESS;
 }
 
+// lane_walk in 32-bit chunk-relative arithmetic (the lane-walk mode's hot
+// loop): records starting in [x, segend), lim = bytes from the chunk start to
+// the end of the file, clamped to 2^31 (a record reaching past a clamped
+// limit reads as dead, and the chunk then takes the exact serial walk).
+struct LWalk {
+    uint32_t exit;      // chunk-relative
+    uint32_t p01, p23;  // up to four 16-bit positions
+    uint32_t cnt;
+    bool dead;
+};
+
+__device__ __forceinline__ uint32_t walk_pos(const LWalk& w, uint32_t i) {
+    const uint32_t v = i < 2 ? w.p01 : w.p23;
+    return (i & 1) ? (v >> 16) : (v & 0xFFFFu);
+}
+
+__device__ __forceinline__ void lw_walk(const uint8_t* data, uint32_t lim, uint32_t x,
+                                        uint32_t segend, LWalk& w) {
+    w.cnt = 0;
+    w.dead = false;
+    w.p01 = w.p23 = 0;
+    uint32_t cur = x;
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        if (cur >= segend) break;
+        if (cur + 16 > lim) {
+            w.dead = true;
+            break;
+        }
+        uint32_t k0, k1, v0, v1;
+        lds_header32(data, cur, k0, k1, v0, v1);
+        const uint32_t room = lim - cur - 16;
+        if ((k1 | v1) || k0 > room || v0 > room - k0) {
+            w.dead = true;
+            break;
+        }
+        if (it == 0) w.p01 = cur;
+        if (it == 1) w.p01 |= cur << 16;
+        if (it == 2) w.p23 = cur;
+        if (it == 3) w.p23 |= cur << 16;
+        ++w.cnt;
+        cur += 16 + k0 + v0;
+    }
+    w.exit = cur;
+}
+
 // Lane 0 walks the staged chunk exactly from X (the relaxation did not
 // converge: rare, e.g. a wrong guess that links and pushes a long run of
 // lanes past their entries): spans to out (if any).  False if a record on
@@ -2114,20 +2160,17 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     const bool in_chunk = seg0 < clen && lane >= je;
     uint64_t cm0, nb;
     lw_masks(zm, seg0, clen, rem, a.hz, cm0, nb);
+    const uint32_t lim = (uint32_t)min(rem, (uint64_t)1 << 31);
     uint32_t g = NO_GUESS;
-    Walk w;
+    LWalk w;
     w.dead = true;
     w.exit = 0;
     w.cnt = 0;
     w.p01 = w.p23 = 0;
     if (!guess && lane == je) g = (uint32_t)(X - cb);
     else if (in_chunk) g = lw_guess(data, seg0, segend, clen, rem, a.hz, cm0, nb);
-    if (in_chunk && g != NO_GUESS) lane_walk(data, cb, a.len, g, segend, w);
+    if (in_chunk && g != NO_GUESS) lw_walk(data, lim, g, segend, w);
     LW_STAMP(1);
-    auto rel = [&](uint64_t e) -> uint32_t {
-        const uint64_t d = e - cb;
-        return d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
-    };
     // chain marks: which lane guesses some lane's walk exits on
     const bool valid0 = in_chunk && g != NO_GUESS && !w.dead;
     sg[lane] = valid0 ? g : NO_GUESS;
@@ -2135,7 +2178,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     lw_wave_sync();
     bool links = false;
     if (valid0) {
-        const uint32_t u = rel(w.exit);
+        const uint32_t u = w.exit;
         if (u < clen && sg[u / SEG] == u) {
             tg[u / SEG] = 1;
             links = true;
@@ -2158,7 +2201,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     LW_STAMP(2);
     // ---- relaxation from (jl, xw) ----
     const bool act = in_chunk && lane >= jl;
-    uint32_t ev = (act && valid0 && (lane == jl || chain)) ? rel(w.exit) : 0u;
+    uint32_t ev = (act && valid0 && (lane == jl || chain)) ? w.exit : 0u;
     uint32_t st = act ? 0u : 3u;  // 0 walking from g, 1 passed through, 2 waiting, 3 not on the path
     bool conv = false;
     for (uint32_t r = 0; r < LW_WROUNDS; ++r) {
@@ -2177,10 +2220,10 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
             } else {                                 // after it one round each)
                 if (st != 0 || g == NO_GUESS || seed != g) {
                     g = seed;
-                    lane_walk(data, cb, a.len, g, segend, w);
+                    lw_walk(data, lim, g, segend, w);
                 }
                 st = 0;
-                nev = w.dead ? 0u : rel(w.exit);
+                nev = w.dead ? 0u : w.exit;
             }
         }
         const bool changed = nev != ev;
@@ -2199,8 +2242,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     count = __builtin_amdgcn_readlane((int)incl, 63);
     const unsigned long long wm = __ballot(walking);  // the chain's last lane holds the exit
     const uint32_t ll = 63u - (uint32_t)__clzll((long long)wm);
-    exit = ((uint64_t)__builtin_amdgcn_readlane((int)(uint32_t)(w.exit >> 32), ll) << 32) |
-           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)w.exit, ll);
+    exit = cb + (uint32_t)__builtin_amdgcn_readlane((int)w.exit, ll);
     if (out) {
         const uint32_t cmax = __builtin_amdgcn_readlane((int)dpp_max_incl(c), 63);
         const uint32_t pre = incl - c;

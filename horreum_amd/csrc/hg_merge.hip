@@ -101,8 +101,7 @@ __device__ __forceinline__ uint32_t run_of(const MergeArgs& a, uint64_t g) {
     return lo;
 }
 
-__device__ __forceinline__ MEnt make_ent(const MergeArgs& a, uint64_t g) {
-    const uint32_t t = run_of(a, g);
+__device__ __forceinline__ MEnt make_ent(const MergeArgs& a, uint64_t g, uint32_t t) {
     const uint64_t rec = g - a.run_off[t];
     // spans and key bytes are read once: nontemporal 16-byte loads
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -151,15 +150,19 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
     const uint32_t tid = threadIdx.x;
     const uint64_t g = (uint64_t)blockIdx.x * THREADS + tid;
     const bool ok = g < a.n;
+    // the workgroup's first run by a uniform search (scalar loads), then the
+    // rare lane past a run boundary steps forward
+    uint32_t t = run_of(a, (uint64_t)blockIdx.x * THREADS);
+    while (t + 1 < a.ntables && a.run_off[t + 1] <= g) ++t;
     MEnt m;
     if (ok) {
-        m = make_ent(a, g);
+        m = make_ent(a, g, t);
         e[g] = m;
         sh[tid] = m;
     }
     __syncthreads();
     if (!ok || g == 0) return;
-    const MEnt prev = tid ? sh[tid - 1] : make_ent(a, g - 1);
+    const MEnt prev = tid ? sh[tid - 1] : make_ent(a, g - 1, run_of(a, g - 1));
     if (prev.tdead != m.tdead) return;  // first record of a table
     if (key_cmp(a, prev, m) >= 0) atomicMin(err, (unsigned long long)g);
 }
