@@ -1897,6 +1897,9 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
 // a quarter entered off its predecessor's exit is streamed again from it.
 // Any unreadable record on the exact path leaves the batch to decode_kernel's
 // engine, which reports errors exactly.
+#ifndef HG_LW
+#define HG_LW 1  // 0: no lane-walk pre-pass mode (A/B builds)
+#endif
 constexpr uint32_t LW_CHUNK = 64 * SEG;         // bytes per chunk: one wave, 64 x 64 B
 constexpr uint32_t LW_CBUF = LW_CHUNK + 128;    // chunk + halo + read slack
 constexpr uint32_t LW_CPP = PIECE / LW_CHUNK;   // chunks per piece
@@ -2456,7 +2459,9 @@ __device__ __forceinline__ bool stride_geom(const uint8_t* data, uint64_t base, 
 
 __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
     __shared__ SpecSmem s;
+#if HG_LW
     __shared__ uint64_t lw_alt[(PIECE + 512) / 8];  // lane-walk chunk buffers of waves 2 and 3
+#endif
     const uint32_t tid = threadIdx.x;
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     const uint32_t b = blk;
@@ -2521,10 +2526,12 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     if (hop) {
         bad = 0;
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
+#if HG_LW
         if (!ok && s.hcode == SB_HOP_SMALL) {  // small records: lane walks over the staged pieces
             ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total);
             if (tid == 0) s.hcode = ok ? SB_LW : SB_LW_DEAD;
         }
+#endif
     }
     if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
 
