@@ -2457,11 +2457,26 @@ __device__ __forceinline__ bool stride_geom(const uint8_t* data, uint64_t base, 
     return true;
 }
 
+// Thread 0: publish batch b (read by decode_kernel after the kernel boundary),
+// count its records per group, then settle the two links it is part of.
+__device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb, uint32_t b,
+                                             uint64_t X0, uint64_t X, uint64_t total, bool ok,
+                                             uint32_t code) {
+    SpecBatch o;
+    o.x0 = X0;
+    o.exit = X;
+    o.count = (uint32_t)total;
+    o.ok = ok ? 1u : 0u;
+    o.pad = code;
+    sb[b] = o;
+    atomicAdd(&a.gsum[b / SPEC_GROUP], (unsigned long long)total);
+    if (!ok || (b == 0 && X0 != a.entry)) mark_bad(a.ctl, a.nspec, b);
+    if (b > 0) link_arrive(a, b, 0 - X0);
+    if (b + 1 < a.nspec) link_arrive(a, b + 1, X);
+}
+
 __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
     __shared__ SpecSmem s;
-#if HG_LW
-    __shared__ uint64_t lw_alt[(PIECE + 512) / 8];  // lane-walk chunk buffers of waves 2 and 3
-#endif
     const uint32_t tid = threadIdx.x;
     const uint8_t* data = reinterpret_cast<const uint8_t*>(s.data64);
     const uint32_t b = blk;
@@ -2526,35 +2541,50 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     if (hop) {
         bad = 0;
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
-#if HG_LW
-        if (!ok && s.hcode == SB_HOP_SMALL) {  // small records: lane walks over the staged pieces
-            ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total);
-            if (tid == 0) s.hcode = ok ? SB_LW : SB_LW_DEAD;
-        }
-#endif
     }
     if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
 
     if (tid == 0) {
-        // publish (read by decode_kernel after the kernel boundary), count the
-        // records per group, then settle the two links this batch is part of
-        SpecBatch o;
-        o.x0 = X0;
-        o.exit = X;
-        o.count = (uint32_t)total;
-        o.ok = ok ? 1u : 0u;
-        o.pad = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
-        sb[b] = o;
-        atomicAdd(&a.gsum[b / SPEC_GROUP], (unsigned long long)total);
-        if (!ok || (b == 0 && X0 != a.entry)) mark_bad(a.ctl, a.nspec, b);
-        if (b > 0) link_arrive(a, b, 0 - X0);
-        if (b + 1 < a.nspec) link_arrive(a, b + 1, X);
+        const uint32_t code = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
+        if (HG_LW && !ok && code == SB_HOP_SMALL) {
+            // small records: left to decode_lw_kernel, which publishes the
+            // batch (its counts and links) once its lane walks are done
+            SpecBatch o;
+            o.x0 = o.exit = 0;
+            o.count = 0;
+            o.ok = 0;
+            o.pad = SB_HOP_SMALL;
+            sb[b] = o;
+        } else {
+            spec_publish(a, sb, b, X0, X, total, ok, code);
+        }
     }
+}
+
+// The lane-walk mode as its own launch between the pre-pass and decode_kernel:
+// only batches the pre-pass left as SB_HOP_SMALL do work (every other
+// workgroup returns at once), so the stride / hop pre-pass keeps its own
+// register and LDS budget (81 VGPRs, 5 waves/SIMD, 23 KB; the lane walks need
+// 108 and 40 KB, which cost the fixed-stride headline 2 %).
+__device__ void lw_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t b) {
+    __shared__ SpecSmem s;
+    __shared__ uint64_t lw_alt[(PIECE + 512) / 8];  // lane-walk chunk buffers of waves 2 and 3
+    if (__builtin_amdgcn_readfirstlane(sb[b].pad) != SB_HOP_SMALL) return;
+    const uint32_t p0 = b * a.sbp;
+    const uint32_t np = min(a.sbp, a.npieces - p0);
+    uint64_t X0 = 0, X = 0, total = 0;
+    const bool ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total);
+    if (threadIdx.x == 0) spec_publish(a, sb, b, X0, X, total, ok, ok ? SB_LW : SB_LW_DEAD);
 }
 
 __global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
                                                               SpecPiece* sp) {
     spec_body(a, sb, sp, blockIdx.x);
+}
+
+__global__ __launch_bounds__(THREADS, 4) void decode_lw_kernel(DecodeArgs a, SpecBatch* sb,
+                                                            SpecPiece* sp) {
+    lw_body(a, sb, sp, blockIdx.x);
 }
 
 // ---- many tables in one launch ---------------------------------------------------
@@ -2598,6 +2628,14 @@ __global__ __launch_bounds__(THREADS, 4) void decode_spec_multi(const DecodeArgs
     const DecodeArgs a = tabs[t];
     spec_body(a, a.sbatch, const_cast<SpecPiece*>(a.spiece),
               blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
+}
+
+__global__ __launch_bounds__(THREADS, 4) void decode_lw_multi(const DecodeArgs* tabs,
+                                                           const uint32_t* pre, uint32_t ntab) {
+    const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
+    const DecodeArgs a = tabs[t];
+    lw_body(a, a.sbatch, const_cast<SpecPiece*>(a.spiece),
+            blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
 }
 
 // Same register bound as decode_kernel (4 waves/SIMD); the table index is
@@ -2813,6 +2851,9 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
                           : (size_t)env_or("HG_DECODE_SPEC_PAD", 0);
     hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), spec_pad, stream, a,
                        a.sbatch, const_cast<SpecPiece*>(a.spiece));
+    if (HG_LW)
+        hipLaunchKernelGGL(decode_lw_kernel, dim3(a.nspec), dim3(THREADS), 0, stream, a, a.sbatch,
+                           const_cast<SpecPiece*>(a.spiece));
     const uint32_t grid = a.nbatches > a.nspec ? a.nbatches : a.nspec;
     if (d_diag)
         hipLaunchKernelGGL(decode_kernel<true>, dim3(grid), dim3(THREADS), 0, stream, a);
@@ -2921,9 +2962,13 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
     const uint32_t* dpre_s = reinterpret_cast<const uint32_t*>(ds + args_b + zb_b);
     const uint32_t* dpre_d = reinterpret_cast<const uint32_t*>(ds + args_b + zb_b + pre_b);
     hipLaunchKernelGGL(decode_zero_multi, dim3(ntab), dim3(THREADS), 0, stream, dargs, dzb, ntab);
-    if (pre_s[ntab])
+    if (pre_s[ntab]) {
         hipLaunchKernelGGL(decode_spec_multi, dim3(pre_s[ntab]), dim3(THREADS), 0, stream, dargs,
                            dpre_s, ntab);
+        if (HG_LW)
+            hipLaunchKernelGGL(decode_lw_multi, dim3(pre_s[ntab]), dim3(THREADS), 0, stream, dargs,
+                               dpre_s, ntab);
+    }
     if (pre_d[ntab])
         hipLaunchKernelGGL(decode_multi, dim3(pre_d[ntab]), dim3(THREADS), 0, stream, dargs, dpre_d,
                            ntab);
