@@ -10,9 +10,10 @@
 // parallel merge-path rounds below build it.  Any other input (duplicate or
 // unordered keys in a table) runs the reference loop itself (step 5).
 //
-// Design (MI355X): keys are compared through 32-byte merge entries: a 16-byte
+// Design (MI355X): keys are compared through 24-byte merge entries: a 16-byte
 // big-endian key prefix (one 128-bit compare decides almost every pair), the
-// key length and a (table, record) reference; only keys that agree on their
+// key length and the record's global entry index (its table by a search over
+// the run offsets; < 2^31 entries per merge); only keys that agree on their
 // first 16 bytes and are both longer fetch the rest from HBM.
 //   1. merge_prep_kernel: one entry per record (runs laid out table by table),
 //   2. and in the same pass: each table strictly increasing (else step 5).
@@ -46,12 +47,12 @@ constexpr uint32_t EPT = TILE / THREADS;
 constexpr uint32_t DEAD = 0x80000000u;
 constexpr uint32_t MAX_TABLES = 1u << 16;
 
-struct MEnt {          // 32 bytes
+struct MEnt {          // 24 bytes
     uint64_t p0, p1;   // key bytes [0,8) and [8,16), big-endian, zero padded
     uint32_t klen;
-    uint32_t tdead;    // table index | DEAD
-    uint64_t rec;      // record index within its table
+    uint32_t gd;       // global entry index g (runs laid out table by table) | DEAD
 };
+constexpr uint64_t MAX_ENTRIES = DEAD;  // g must fit below the DEAD bit
 
 struct MergeArgs {
     const uint8_t* arena;
@@ -63,16 +64,28 @@ struct MergeArgs {
     uint64_t n;                  // total entries
 };
 
-__device__ __forceinline__ const uint8_t* key_ptr(const MergeArgs& a, uint32_t t, uint64_t rec) {
-    return a.arena + a.table_off[t] + a.spans[t][rec].off + 16;
-}
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
 
+__device__ __forceinline__ uint32_t run_of(const MergeArgs& a, uint64_t g);
+
+// The record behind entry e: its table t and span.
+__device__ __forceinline__ hg_span ent_span(const MergeArgs& a, const MEnt& e, uint32_t& t) {
+    const uint64_t g = e.gd & ~DEAD;
+    t = run_of(a, g);
+    return a.spans[t][g - a.run_off[t]];
+}
+
+__device__ __forceinline__ const uint8_t* key_ptr(const MergeArgs& a, const MEnt& e) {
+    uint32_t t;
+    const hg_span sp = ent_span(a, e, t);
+    return a.arena + a.table_off[t] + sp.off + 16;
+}
+
 // Bytes [from, to) of two keys that agree on their first `from` bytes.
 __device__ int tail_cmp(const MergeArgs& a, const MEnt& x, const MEnt& y) {
-    const uint8_t* kx = key_ptr(a, x.tdead & ~DEAD, x.rec);
-    const uint8_t* ky = key_ptr(a, y.tdead & ~DEAD, y.rec);
+    const uint8_t* kx = key_ptr(a, x);
+    const uint8_t* ky = key_ptr(a, y);
     const uint32_t m = min(x.klen, y.klen);
     for (uint32_t i = 16; i < m; ++i) {
         const uint8_t bx = kx[i], by = ky[i];
@@ -134,8 +147,7 @@ __device__ __forceinline__ MEnt make_ent(const MergeArgs& a, uint64_t g, uint32_
     m.p0 = w0;
     m.p1 = w1;
     m.klen = sp.klen;
-    m.tdead = t;
-    m.rec = rec;
+    m.gd = (uint32_t)g;
     return m;
 }
 
@@ -162,8 +174,8 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
     }
     __syncthreads();
     if (!ok || g == 0) return;
-    const MEnt prev = tid ? sh[tid - 1] : make_ent(a, g - 1, run_of(a, g - 1));
-    if (prev.tdead != m.tdead) return;  // first record of a table
+    if (g == a.run_off[t]) return;  // first record of its table
+    const MEnt prev = tid ? sh[tid - 1] : make_ent(a, g - 1, t);
     if (key_cmp(a, prev, m) >= 0) atomicMin(err, (unsigned long long)g);
 }
 
@@ -172,39 +184,6 @@ struct LevelArgs {
     const uint64_t* roff;  // [nruns + 1] run offsets of this round's input
     uint32_t nruns;
 };
-
-// Number of A elements among the first d merged elements (ties: A first),
-// by a 64-ary search run by one wave.  Returns the same value in every lane.
-__device__ uint64_t merge_path(const MergeArgs& a, const MEnt* A, uint64_t na, const MEnt* B,
-                               uint64_t nb, uint64_t d) {
-    const uint32_t lane = threadIdx.x & 63u;
-    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;  // answer in [lo, hi]
-    while (hi > lo) {
-        // candidate c: "A[c] is among the first d" <=> A[c] <= B[d-c-1]
-        const uint64_t span = hi - lo;
-        const uint64_t c = lo + (span * lane) / 64;  // lanes probe lo .. hi-1
-        bool before = false;
-        if (c < hi) {
-            const MEnt x = A[c];
-            const MEnt y = B[d - c - 1];
-            before = key_cmp(a, x, y) <= 0;
-        }
-        // predicate is monotone (true ... true false ... false) over c
-        const unsigned long long m = __ballot(c < hi && !before);
-        if (!m) {
-            // every probed c is "before": answer > last probe
-            const uint64_t last = lo + (span * 63) / 64;
-            lo = last + 1;
-        } else {
-            const int f = __ffsll((long long)m) - 1;  // first probe that is not before
-            const uint64_t cf = lo + (span * (uint64_t)f) / 64;
-            const uint64_t cp = f > 0 ? lo + (span * (uint64_t)(f - 1)) / 64 + 1 : lo;
-            lo = cp;
-            hi = cf;
-        }
-    }
-    return lo;
-}
 
 struct LevelSmem {
     alignas(16) MEnt seg[TILE + 2];  // A segment then B segment (then the merged output)
@@ -410,8 +389,13 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         }
         const uint64_t j0 = (d0 - o) - i0, j1 = (d1 - o) - i1;
         const uint32_t nA = (uint32_t)(i1 - i0), nB = (uint32_t)(j1 - j0);
-        for (uint32_t q = tid; q < nA; q += THREADS) s.seg[q] = A[i0 + q];
-        for (uint32_t q = tid; q < nB; q += THREADS) s.seg[nA + q] = B[j0 + q];
+        {  // both segments as 8-byte words, contiguous per lane (entries are 24 B)
+            const uint64_t* wa = reinterpret_cast<const uint64_t*>(A + i0);
+            const uint64_t* wb = reinterpret_cast<const uint64_t*>(B + j0);
+            uint64_t* ws = reinterpret_cast<uint64_t*>(s.seg);
+            for (uint32_t q = tid; q < 3 * nA; q += THREADS) ws[q] = wa[q];
+            for (uint32_t q = tid; q < 3 * nB; q += THREADS) ws[3 * nA + q] = wb[q];
+        }
         if (tid == THREADS - 1) {
             s.has_prev = i0 > 0;
             if (i0 > 0 && i0 <= na) s.aprev = A[i0 - 1];
@@ -454,10 +438,10 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                         // the tile, or the one just before the tile) kills an equal key
                         const bool eq = ai > 0 ? key_cmp(a, SA[ai - 1], x) == 0
                                                : (s.has_prev && key_cmp(a, s.aprev, x) == 0);
-                        if (eq) x.tdead |= DEAD;
+                        if (eq) x.gd |= DEAD;
                     }
                     fx[k] = x;
-                    fcnt += (x.tdead & DEAD) ? 0u : 1u;
+                    fcnt += (x.gd & DEAD) ? 0u : 1u;
                 }
             }
             __syncthreads();  // every thread is done reading the segments
@@ -466,9 +450,9 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                 for (uint32_t k = 0; k < EPT; ++k)
                     if (d + k < e) s.seg[d + k] = fx[k];
                 __syncthreads();
-                const uint4* src = reinterpret_cast<const uint4*>(s.seg);
-                uint4* o4 = reinterpret_cast<uint4*>(dst);
-                for (uint32_t i = tid; i < 2 * nt; i += THREADS) o4[i] = src[i];
+                const uint64_t* src = reinterpret_cast<const uint64_t*>(s.seg);
+                uint64_t* o8 = reinterpret_cast<uint64_t*>(dst);
+                for (uint32_t i = tid; i < 3 * nt; i += THREADS) o8[i] = src[i];
             } else {
                 // live entries before this thread's in the tile, the tiles'
                 // before it (look-back), then the pairs at their positions
@@ -494,10 +478,11 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                 for (uint32_t k = 0; k < EPT; ++k) {
                     if (d + k >= e) break;
                     const MEnt& x = fx[k];
-                    if (x.tdead & DEAD) continue;
-                    const hg_span sp = a.spans[x.tdead][x.rec];
+                    if (x.gd & DEAD) continue;
+                    uint32_t t;
+                    const hg_span sp = ent_span(a, x, t);
                     hg_pair p;
-                    p.key_off = a.table_off[x.tdead] + sp.off + 16;
+                    p.key_off = a.table_off[t] + sp.off + 16;
                     p.val_off = p.key_off + sp.klen;
                     p.klen = sp.klen;
                     p.vlen = sp.vlen;
@@ -524,7 +509,7 @@ __global__ __launch_bounds__(THREADS) void merge_count_kernel(MergeArgs a, const
     uint32_t c = 0;
     for (uint32_t q = threadIdx.x; q < TILE; q += THREADS) {
         const uint64_t g = t0 + q;
-        if (g < a.n && !(e[g].tdead & DEAD)) ++c;
+        if (g < a.n && !(e[g].gd & DEAD)) ++c;
     }
     __shared__ uint32_t ws[THREADS / 64];
     c = hgk::wave_sum<uint32_t>(c);
@@ -592,7 +577,7 @@ __global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const 
         lv[k] = false;
         if (g < a.n) {
             x[k] = e[g];
-            lv[k] = !(x[k].tdead & DEAD);
+            lv[k] = !(x[k].gd & DEAD);
         }
     }
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -614,8 +599,8 @@ __global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const 
         }
         const uint64_t pos = run + woff + pre[k];
         if (lv[k] && pos < cap) {
-            const uint32_t t = x[k].tdead;
-            const hg_span sp = a.spans[t][x[k].rec];
+            uint32_t t;
+            const hg_span sp = ent_span(a, x[k], t);
             hg_pair p;
             p.key_off = a.table_off[t] + sp.off + 16;
             p.val_off = p.key_off + sp.klen;
@@ -639,14 +624,15 @@ __global__ __launch_bounds__(THREADS) void merge_emit_kernel(MergeArgs a, const 
 // tables l, l + 64, ...; their head entries live in a per-table state array;
 // a butterfly over (key, table) picks the winner in every lane.  Runs only
 // when merge_prep_kernel found a table that is not strictly increasing.
-struct ExactHead {  // 48 bytes per table
+struct ExactHead {  // 40 bytes per table
     MEnt e;         // current head entry (valid when idx < cnt)
     uint64_t idx, cnt;
 };
 
 __device__ __forceinline__ bool ent_before(const MergeArgs& a, const MEnt& x, const MEnt& y) {
     const int c = key_cmp(a, x, y);
-    return c < 0 || (c == 0 && (x.tdead & ~DEAD) < (y.tdead & ~DEAD));
+    // equal keys: the lower table first -- runs are laid out table by table
+    return c < 0 || (c == 0 && (x.gd & ~DEAD) < (y.gd & ~DEAD));
 }
 
 __device__ __forceinline__ MEnt shfl_ent(const MEnt& m, int src) {
@@ -654,8 +640,7 @@ __device__ __forceinline__ MEnt shfl_ent(const MEnt& m, int src) {
     o.p0 = __shfl(m.p0, src, 64);
     o.p1 = __shfl(m.p1, src, 64);
     o.klen = __shfl(m.klen, src, 64);
-    o.tdead = __shfl(m.tdead, src, 64);
-    o.rec = __shfl(m.rec, src, 64);
+    o.gd = __shfl(m.gd, src, 64);
     return o;
 }
 
@@ -680,8 +665,8 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt
             // :209-216 the first minimum head over the tables in priority order
             bool have = false;
             MEnt best;
-            best.p0 = best.p1 = best.rec = 0;
-            best.klen = best.tdead = 0;
+            best.p0 = best.p1 = 0;
+            best.klen = best.gd = 0;
             for (uint32_t t = lane; t < a.ntables; t += 64) {
                 const ExactHead h = hs[t];
                 if (h.idx < h.cnt && (!have || ent_before(a, h.e, best))) {
@@ -700,8 +685,8 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt
             }
             // :216-217 push the winner
             if (lane == 0 && n < cap) {
-                const uint32_t t = best.tdead & ~DEAD;
-                const hg_span sp = a.spans[t][best.rec];
+                uint32_t t;
+                const hg_span sp = ent_span(a, best, t);
                 hg_pair p;
                 p.key_off = a.table_off[t] + sp.off + 16;
                 p.val_off = p.key_off + sp.klen;
@@ -732,289 +717,6 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt
         r.table = 1;  // on success: 1 = the serial reference loop produced the output
         r.index = 0;
         *result = r;
-    }
-}
-
-// ---- 6. k-way bucket merge (2 <= k <= KW_MAX tables, verified strictly increasing) ------
-// Replaces the log2(k) pairwise rounds through HBM: the entries move once.
-//   a. kw_bounds_kernel: every S-th entry of every run is a sample (S =
-//      KW_BUCKET / k).  Per (sample, run): how many of that run's samples
-//      precede the sample in merged order (key, then run priority) -- summed
-//      over the runs that is the sample's rank, a permutation of the samples --
-//      and the lower bound of its key in that run (a binary search over the
-//      run's samples, then one inside the S entries they bracket).  Row
-//      rank + 1 of `bounds` = the bucket boundary the sample defines.
-//   b. kw_merge_kernel: bucket b = entries between boundary rows b and b+1,
-//      at most S of each run (no sample of a run falls strictly between two
-//      consecutive boundaries), equal keys never split.  Its merged position
-//      is known without a scan (sum of row b).  The bucket is staged in LDS and
-//      merged there by log2(k) merge-path levels (adjacent runs pairwise,
-//      ties: the higher-priority run first; a lower-priority copy of a key the
-//      higher-priority side holds is marked dead -- newest wins); the merged
-//      order goes out as 4-byte entry indices with a dead bit.
-//   c. kw_count / merge_scan / kw_emit: live entries per 1024 merged
-//      positions, their scan, and the hg_pairs in order.
-constexpr uint32_t KW_MAX = 16;
-constexpr uint32_t KW_BUCKET = 1024;              // most entries one bucket can hold (k * S)
-constexpr uint32_t KW_EPT = KW_BUCKET / THREADS;  // merged positions per thread per level
-constexpr uint32_t KW_DEAD = 0x80000000u;
-
-struct KwArgs {
-    uint32_t S;                 // sample stride (entries)
-    uint32_t nsamp;             // samples over all runs
-    const uint64_t* samp_off;   // [k + 1] first sample id of each run
-    MEnt* samp;                 // [nsamp] the samples' entries, dense (L2-resident searches)
-    uint32_t* bounds;           // [(nsamp + 2) * k] bucket b starts at bounds[b * k + r] in run r
-    uint32_t* mid;              // [n] merged order: global entry index | KW_DEAD
-};
-
-struct KwEnt {  // an entry in LDS (24 bytes)
-    uint64_t p0, p1;
-    uint32_t klen, id;  // id: global entry index | KW_DEAD
-};
-
-__device__ __forceinline__ int kw_cmp(const MergeArgs& a, const KwEnt& x, const KwEnt& y) {
-    if (x.p0 != y.p0) return x.p0 < y.p0 ? -1 : 1;
-    if (x.p1 != y.p1) return x.p1 < y.p1 ? -1 : 1;
-    if (x.klen <= 16 || y.klen <= 16) return x.klen < y.klen ? -1 : x.klen > y.klen ? 1 : 0;
-    MEnt mx, my;  // keys equal on 16 bytes and both longer: compare the rest in HBM
-    const uint64_t gx = x.id & ~KW_DEAD, gy = y.id & ~KW_DEAD;
-    const uint32_t tx = run_of(a, gx), ty = run_of(a, gy);
-    mx.klen = x.klen;
-    mx.tdead = tx;
-    mx.rec = gx - a.run_off[tx];
-    my.klen = y.klen;
-    my.tdead = ty;
-    my.rec = gy - a.run_off[ty];
-    return tail_cmp(a, mx, my);
-}
-
-__global__ __launch_bounds__(THREADS) void kw_samples_kernel(MergeArgs a, KwArgs w, const MEnt* e) {
-    const uint32_t sid = blockIdx.x * THREADS + threadIdx.x;
-    if (sid >= w.nsamp) return;
-    uint32_t r = 0;
-    while (r + 1 < a.ntables && w.samp_off[r + 1] <= sid) ++r;
-    w.samp[sid] = e[a.run_off[r] + (sid - w.samp_off[r]) * (uint64_t)w.S];
-}
-
-__global__ __launch_bounds__(THREADS) void kw_bounds_kernel(MergeArgs a, KwArgs w, const MEnt* e) {
-    const uint32_t t = blockIdx.x * THREADS + threadIdx.x;
-    const uint32_t sid = t / KW_MAX, rr = t % KW_MAX;
-    const uint32_t k = a.ntables;
-    const uint64_t S = w.S;
-    uint32_t contrib = 0, lb = 0;
-    const bool act = sid < w.nsamp && rr < k;
-    if (act) {
-        uint32_t r = 0;  // the sample's run and index
-        while (r + 1 < k && w.samp_off[r + 1] <= sid) ++r;
-        const uint64_t i = sid - w.samp_off[r];
-        const MEnt x = w.samp[sid];
-        if (rr == r) {
-            contrib = (uint32_t)i;
-            lb = (uint32_t)(i * S);
-        } else {
-            const uint64_t base = a.run_off[rr], nr = a.run_off[rr + 1] - base;
-            const uint64_t m = w.samp_off[rr + 1] - w.samp_off[rr];
-            const MEnt* sr = w.samp + w.samp_off[rr];
-            uint64_t lo = 0, hi = m;  // samples of rr with key < x
-            while (lo < hi) {
-                const uint64_t md = (lo + hi) >> 1;
-                if (key_cmp(a, sr[md], x) < 0) lo = md + 1;
-                else hi = md;
-            }
-            const bool eq = lo < m && key_cmp(a, sr[lo], x) == 0;
-            contrib = (uint32_t)(lo + ((rr < r && eq) ? 1u : 0u));
-            uint64_t l2 = lo ? (lo - 1) * S + 1 : 0, h2 = lo * S < nr ? lo * S : nr;
-            while (l2 < h2) {  // first entry with key >= x, between the bracketing samples
-                const uint64_t md = (l2 + h2) >> 1;
-                if (key_cmp(a, e[base + md], x) < 0) l2 = md + 1;
-                else h2 = md;
-            }
-            lb = (uint32_t)l2;
-        }
-    }
-    uint32_t rank = contrib;
-#pragma unroll
-    for (int d = KW_MAX / 2; d >= 1; d >>= 1) rank += __shfl_xor(rank, d, KW_MAX);
-    if (act) w.bounds[(size_t)(rank + 1) * k + rr] = lb;
-    if (t < k) {
-        w.bounds[t] = 0;
-        w.bounds[(size_t)(w.nsamp + 1) * k + t] = (uint32_t)(a.run_off[t + 1] - a.run_off[t]);
-    }
-}
-
-struct KwSmem {
-    KwEnt buf[2][KW_BUCKET];
-    uint32_t off[KW_MAX + 1];  // runs' offsets in the bucket
-    uint32_t lo[KW_MAX];       // runs' first entry (run-local index)
-    uint64_t P;                // merged position of the bucket
-    uint32_t size, bad;
-};
-
-__global__ __launch_bounds__(THREADS) void kw_merge_kernel(MergeArgs a, KwArgs w, const MEnt* e,
-                                                           unsigned long long* err) {
-    __shared__ KwSmem s;
-    if (*err != ~0ull) return;  // a table is not strictly increasing: the exact loop takes over
-    const uint32_t k = a.ntables, tid = threadIdx.x;
-    for (uint32_t b = blockIdx.x; b <= w.nsamp; b += gridDim.x) {
-        if (tid < 64) {  // wave 0: lane r reads run r's bounds (independent loads), DPP scans
-            uint32_t lo = 0, len = 0;
-            bool bad = false;
-            if (tid < k) {
-                lo = w.bounds[(size_t)b * k + tid];
-                const uint32_t hi = w.bounds[(size_t)(b + 1) * k + tid];
-                bad = hi < lo;
-                len = bad ? 0u : hi - lo;
-            }
-            const uint32_t incl = hgk::dpp_sum_incl(len);
-            const uint32_t lsum = hgk::dpp_sum_incl(lo);  // P < 2^31 (n < 2^31)
-            if (tid < k) {
-                s.off[tid] = incl - len;
-                s.lo[tid] = lo;
-            }
-            const bool anybad = __ballot(bad) != 0;
-            if (tid == 63) {
-                s.off[k] = incl;
-                s.size = incl;
-                s.P = lsum;
-                s.bad = anybad || incl > KW_BUCKET;
-            }
-        }
-        __syncthreads();
-        const uint32_t size = s.size;
-        if (s.bad) {  // only on input that is not strictly increasing
-            if (tid == 0) atomicMin(err, 0ull);
-            return;
-        }
-        for (uint32_t q = tid; q < size; q += THREADS) {
-            uint32_t r = 0;
-            while (r + 1 < k && s.off[r + 1] <= q) ++r;
-            const uint64_t g = a.run_off[r] + s.lo[r] + (q - s.off[r]);
-            const MEnt m = e[g];
-            KwEnt x;
-            x.p0 = m.p0;
-            x.p1 = m.p1;
-            x.klen = m.klen;
-            x.id = (uint32_t)g;
-            s.buf[0][q] = x;
-        }
-        __syncthreads();
-        uint32_t cur = 0;
-        for (uint32_t wdt = 1; wdt < k; wdt <<= 1) {  // runs [2p*wdt, (2p+1)*wdt) | [.., (2p+2)*wdt)
-            const KwEnt* src = s.buf[cur];
-            KwEnt* dst = s.buf[cur ^ 1];
-            uint32_t q = tid * KW_EPT;
-            const uint32_t qe = min(q + KW_EPT, size);
-            while (q < qe) {
-                uint32_t p = 0;  // the pair holding q
-                while (s.off[min((2 * p + 2) * wdt, k)] <= q) ++p;
-                const uint32_t oA = s.off[min(2 * p * wdt, k)], oB = s.off[min((2 * p + 1) * wdt, k)],
-                               oE = s.off[min((2 * p + 2) * wdt, k)];
-                const KwEnt* A = src + oA;
-                const KwEnt* B = src + oB;
-                const uint32_t nA = oB - oA, nB = oE - oB;
-                const uint32_t d = q - oA;
-                uint32_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
-                while (lo < hi) {  // A elements among the pair's first d outputs (ties: A first)
-                    const uint32_t md = (lo + hi) >> 1;
-                    if (kw_cmp(a, A[md], B[d - 1 - md]) <= 0) lo = md + 1;
-                    else hi = md;
-                }
-                uint32_t ai = lo, bj = d - lo;
-                const uint32_t stop = min(qe, oE);
-                for (; q < stop; ++q) {
-                    KwEnt x;
-                    if (bj >= nB || (ai < nA && kw_cmp(a, A[ai], B[bj]) <= 0)) {
-                        x = A[ai++];
-                    } else {
-                        x = B[bj++];
-                        if (ai > 0 && kw_cmp(a, A[ai - 1], x) == 0) x.id |= KW_DEAD;  // newest wins
-                    }
-                    dst[q] = x;
-                }
-            }
-            __syncthreads();
-            cur ^= 1;
-        }
-        const uint64_t P = s.P;
-        for (uint32_t q = tid; q < size; q += THREADS) w.mid[P + q] = s.buf[cur][q].id;
-        __syncthreads();
-    }
-}
-
-// Live entries per TILE merged positions (kw_emit's tiles).
-__global__ __launch_bounds__(THREADS) void kw_count_kernel(MergeArgs a, KwArgs w, uint32_t* tile_live) {
-    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
-    uint32_t c = 0;
-    for (uint32_t q = threadIdx.x; q < TILE; q += THREADS) {
-        const uint64_t g = t0 + q;
-        if (g < a.n && !(w.mid[g] & KW_DEAD)) ++c;
-    }
-    __shared__ uint32_t ws[THREADS / 64];
-    c = hgk::wave_sum<uint32_t>(c);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t s = 0;
-        for (uint32_t i = 0; i < THREADS / 64; ++i) s += ws[i];
-        tile_live[blockIdx.x] = s;
-    }
-}
-
-// The live entries of each tile, in merged order, as hg_pairs (rank = live
-// entries of the tiles before + of the rows before in the tile + of the
-// lanes before in the row, as merge_emit_kernel).
-__global__ __launch_bounds__(THREADS) void kw_emit_kernel(MergeArgs a, KwArgs w,
-                                                          const uint64_t* tile_base, hg_pair* out,
-                                                          uint64_t cap,
-                                                          const unsigned long long* err) {
-    __shared__ uint32_t wc[EPT][THREADS / 64];
-    if (*err != ~0ull) return;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
-    uint32_t id[EPT];
-    uint32_t pre[EPT];
-    bool lv[EPT];
-#pragma unroll
-    for (uint32_t k = 0; k < EPT; ++k) {
-        const uint64_t g = t0 + (uint64_t)k * THREADS + tid;
-        lv[k] = false;
-        id[k] = 0;
-        if (g < a.n) {
-            id[k] = w.mid[g];
-            lv[k] = !(id[k] & KW_DEAD);
-        }
-    }
-    const unsigned long long below = (1ull << lane) - 1ull;
-#pragma unroll
-    for (uint32_t k = 0; k < EPT; ++k) {
-        const unsigned long long m = __ballot(lv[k]);
-        pre[k] = (uint32_t)__popcll(m & below);
-        if (lane == 0) wc[k][wid] = (uint32_t)__popcll(m);
-    }
-    __syncthreads();
-    uint64_t run = tile_base[blockIdx.x];
-#pragma unroll
-    for (uint32_t k = 0; k < EPT; ++k) {
-        uint32_t row = 0, woff = 0;
-#pragma unroll
-        for (uint32_t v = 0; v < THREADS / 64; ++v) {
-            row += wc[k][v];
-            woff += v < wid ? wc[k][v] : 0u;
-        }
-        const uint64_t pos = run + woff + pre[k];
-        if (lv[k] && pos < cap) {
-            const uint64_t g = id[k];
-            const uint32_t t = run_of(a, g);
-            const hg_span sp = a.spans[t][g - a.run_off[t]];
-            hg_pair p;
-            p.key_off = a.table_off[t] + sp.off + 16;
-            p.val_off = p.key_off + sp.klen;
-            p.klen = sp.klen;
-            p.vlen = sp.vlen;
-            out[pos] = p;
-        }
-        run += row;
     }
 }
 
@@ -1052,6 +754,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
     uint64_t n = 0;
     for (uint32_t t = 0; t < ntables; ++t) n += counts[t];
+    if (n >= MAX_ENTRIES) return HG_ERR_TOO_LARGE;  // entries carry a 31-bit global index
     // host staging: [table_off | span ptrs | run offsets of every round]
     uint64_t* h = static_cast<uint64_t*>(staging);
     uint64_t* h_toff = h;
@@ -1076,25 +779,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
             nr = m;
         }
     }
-    // k-way bucket merge (step 6) for 2..KW_MAX tables: sample stride and the
-    // runs' first sample ids follow the round offsets in the staging
-    // (opt-in, HG_MERGE_KWAY=1: bit-exact, but its buckets average S entries
-    // and the kernel is latency-bound -- 1.3 ms vs 0.58 ms for the three
-    // pairwise rounds on the cfg 5 leg, profiles/r2_kway_v1.log)
-    const char* kw_env = getenv("HG_MERGE_KWAY");
-    const bool kway = ntables >= 2 && ntables <= KW_MAX && n < (1ull << 31) && kw_env &&
-                      kw_env[0] == '1';
-    const uint32_t S = KW_BUCKET / ntables;
-    uint64_t* h_soff = h + 2 * (uint64_t)ntables + total_roff;
-    uint64_t nsamp = 0;
-    if (kway) {
-        for (uint32_t t = 0; t < ntables; ++t) {
-            h_soff[t] = nsamp;
-            nsamp += (counts[t] + S - 1) / S;
-        }
-        h_soff[ntables] = nsamp;
-    }
-    const uint64_t stage_words = 2 * (uint64_t)ntables + total_roff + (kway ? ntables + 1 : 0);
+    const uint64_t stage_words = 2 * (uint64_t)ntables + total_roff;
     if (stage_words * 8 > hgk_merge_staging_bytes(ntables)) return HG_ERR_INTERNAL;
     char* ws = static_cast<char*>(d_ws);
     const uint64_t ntiles = (n + TILE - 1) / TILE;
@@ -1133,34 +818,6 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     }
     const uint32_t g1 = (uint32_t)((n + THREADS - 1) / THREADS);
     hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, e0, err);
-    if (kway) {  // the second entry buffer holds the bucket bounds and the merged order
-        KwArgs w;
-        w.S = S;
-        w.nsamp = (uint32_t)nsamp;
-        w.samp_off = d_stage + 2 * (uint64_t)ntables + total_roff;
-        w.mid = reinterpret_cast<uint32_t*>(e1);
-        w.bounds = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(e1) +
-                                               ((n * sizeof(uint32_t) + 255) & ~255ull));
-        w.samp = reinterpret_cast<MEnt*>(reinterpret_cast<char*>(w.bounds) +
-                                         (((nsamp + 2) * ntables * 4 + 255) & ~255ull));
-        hipLaunchKernelGGL(kw_samples_kernel, dim3((uint32_t)((nsamp + THREADS - 1) / THREADS)),
-                           dim3(THREADS), 0, stream, a, w, (const MEnt*)e0);
-        const uint64_t nthr = nsamp * KW_MAX;
-        hipLaunchKernelGGL(kw_bounds_kernel, dim3((uint32_t)((nthr + THREADS - 1) / THREADS)),
-                           dim3(THREADS), 0, stream, a, w, (const MEnt*)e0);
-        const uint32_t grid = (uint32_t)min(nsamp + 1, (uint64_t)4096);
-        hipLaunchKernelGGL(kw_merge_kernel, dim3(grid), dim3(THREADS), 0, stream, a, w,
-                           (const MEnt*)e0, err);
-        hipLaunchKernelGGL(kw_count_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a, w,
-                           tile_live);
-        hipLaunchKernelGGL(merge_scan_kernel, dim3(1), dim3(1024), 0, stream,
-                           (const uint32_t*)tile_live, (uint32_t)ntiles, tile_base, d_result);
-        hipLaunchKernelGGL(kw_emit_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a, w,
-                           (const uint64_t*)tile_base, d_out, cap, (const unsigned long long*)err);
-        hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)e0,
-                           (const unsigned long long*)err, heads, d_out, cap, d_result);
-        return HG_LAUNCH_STATUS();
-    }
     MEnt* cur = e0;
     MEnt* nxt = e1;
     const uint64_t* roff = a.run_off;

@@ -56,7 +56,8 @@ enum hg_status {
     HG_ERR_CAPACITY = 5,
     HG_ERR_INVALID_ARG = -1,
     HG_ERR_HIP = -2,
-    HG_ERR_TOO_LARGE = -3,  /* input length >= 2^40 bytes (engine limit) */
+    HG_ERR_TOO_LARGE = -3,  /* input length >= 2^40 bytes, or a merge of >= 2^31
+                               records (engine limits) */
     HG_ERR_INTERNAL = -4,   /* e.g. a bounded device spin timed out */
     HG_ERR_EMPTY_MERGE = -5, /* merge of zero records; the reference panics (src/sstable/manager.rs:213) */
     /* Retired (ABI <= 3 returned it for a merge input that was not strictly
