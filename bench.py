@@ -646,11 +646,12 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     from horreum_amd import synth
     rng = np.random.default_rng(5 + 1000 * rank)
     shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64))
-    bufs, offs_b, total, n_in = [], [], 0, 0
+    bufs, offs_b, total, n_in, allkeys = [], [], 0, 0, []
     for t in range(ntab):
         own = rng.integers(0, 1 << 40, size=per_table - shared.size, dtype=np.uint64)
         keys = np.unique(np.concatenate([shared, own]))
         n_in += int(keys.size)
+        allkeys.append(keys)
         buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=50 + t, device=device)
         bufs.append(buf)
     sizes = [b.numel() for b in bufs]
@@ -685,7 +686,9 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     line = {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
             "tables": ntab, "input_bytes_per_gpu": in_bytes, "merged_records": int(m.n),
             "merged_bytes": int(out_len), "ms": round(wall * 1e3, 3),
-            "status": int(m.status), "api": "hg_compact_dev", "input_records": n_in}
+            "status": int(m.status), "api": "hg_compact_dev", "input_records": n_in,
+            # newest wins over sorted unique tables: one record per distinct key
+            "parity_count_ok": int(m.n) == int(np.unique(np.concatenate(allkeys)).size)}
     # algorithmic bytes: read the tables, write the compacted table; spans
     # (16 B per input record) and pairs (24 B per output record) each written
     # and read once.  PMC traffic of the same leg from the committed profile.

@@ -114,6 +114,8 @@ def test_golden_compaction(engine, golden):
     (8, 20000, 0.25, 5, False),
     (8, 3000, 0.9, 6, True),   # heavy overlap
     (13, 6000, 0.2, 7, False),  # odd run counts in every round
+    (16, 30000, 0.3, 8, False),  # four full rounds
+    (17, 9000, 0.3, 9, True),   # a fifth round for one odd run
 ])
 def test_merge_parity(engine, k, n_universe, frac, seed, long_prefix):
     datas = encode_tables(sorted_tables(k, n_universe, frac, seed, long_prefix))
@@ -134,13 +136,21 @@ def test_merge_with_empty_tables(engine):
     assert res.status == 0 and np.array_equal(got, want)
 
 
-def test_merge_large(engine):
-    """~1.2 M records over 8 tables (thousands of tiles per round)."""
-    rng = np.random.default_rng(12)
+@pytest.mark.parametrize("k,sizes", [
+    (8, [150_000] * 8),
+    (5, [400_000, 3, 150_000, 0, 20_000]),  # skewed run sizes, an empty table
+    (3, [200_000, 200_000, 200_000]),       # heavy overlap (universe of 400 k)
+])
+def test_merge_large(engine, k, sizes):
+    """Up to ~1.2 M records (thousands of tiles) vs the oracle."""
+    rng = np.random.default_rng(12 + k)
     universe = np.unique(rng.integers(0, 1 << 40, size=400_000, dtype=np.uint64))
     datas = []
-    for t in range(8):
-        keys = np.sort(rng.choice(universe, size=150_000, replace=False))
+    for t in range(k):
+        if sizes[t] == 0:
+            datas.append(np.zeros(0, np.uint8))
+            continue
+        keys = np.sort(rng.choice(universe, size=sizes[t], replace=False))
         kb = keys.astype(">u8").view(np.uint8).reshape(-1, 8)
         n = keys.size
         pairs = np.zeros(n, dtype=oracle.PAIR_DTYPE)
