@@ -83,18 +83,25 @@ class InternalPair:
 def pack_pairs(pairs):
     """Pairs -> (arena uint8, PAIR_DTYPE descriptors): the contiguous
     key||value arena the engine encodes from (the memtable buffer of
-    SURVEY.md §8 f3).  Host packing only; no record bytes are produced here."""
+    SURVEY.md §8 f3).  Host packing only; no record bytes are produced here.
+    Offsets come from one cumulative sum over the lengths (no per-record
+    descriptor writes)."""
     n = len(pairs)
     desc = np.zeros(n, dtype=PAIR_DTYPE)
-    chunks = []
-    off = 0
-    for i, p in enumerate(pairs):
-        v = p.value if p.value is not None else b""
-        desc[i] = (off, off + len(p.key), len(p.key), len(v))
-        chunks.append(p.key)
-        chunks.append(v)
-        off += len(p.key) + len(v)
-    arena = np.frombuffer(b"".join(chunks), dtype=np.uint8) if off else np.zeros(1, np.uint8)
+    if n == 0:
+        return np.zeros(1, np.uint8), desc
+    keys = [bytes(p.key) for p in pairs]
+    vals = [bytes(p.value) if p.value is not None else b"" for p in pairs]
+    kl = np.fromiter(map(len, keys), dtype=np.uint64, count=n)
+    vl = np.fromiter(map(len, vals), dtype=np.uint64, count=n)
+    starts = np.zeros(n, dtype=np.uint64)
+    np.cumsum((kl + vl)[:-1], out=starts[1:])
+    desc["key_off"] = starts
+    desc["val_off"] = starts + kl
+    desc["klen"] = kl
+    desc["vlen"] = vl
+    blob = b"".join([b for kv in zip(keys, vals) for b in kv])
+    arena = np.frombuffer(blob, dtype=np.uint8) if blob else np.zeros(1, np.uint8)
     return arena, desc
 
 

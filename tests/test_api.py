@@ -80,6 +80,23 @@ def test_persisted_file_no_truncate(tmp_path):
         PersistedFile.open(tmp_path / "missing")
 
 
+def test_pack_pairs_host():
+    """The host packing of InternalPairs into the encode input (arena +
+    descriptors) equals the oracle's, tombstones included (CPU only)."""
+    from horreum_amd.format import pack_pairs
+    rng = np.random.default_rng(3)
+    pairs = [(rng.integers(0, 256, int(rng.integers(0, 20)), dtype=np.uint8).tobytes(),
+              None if rng.random() < 0.2 else
+              rng.integers(0, 256, int(rng.integers(0, 50)), dtype=np.uint8).tobytes())
+             for _ in range(500)]
+    arena, desc = pack_pairs([InternalPair(k, v) for k, v in pairs])
+    warena, wdesc = oracle.pack_pairs(pairs)
+    assert np.array_equal(desc, wdesc)
+    assert arena[:warena.size].tobytes() == warena.tobytes()
+    a0, d0 = pack_pairs([])
+    assert d0.size == 0
+
+
 def test_api_fails_loudly_without_gpu():
     """No CPU codec behind the API: without a HIP device the engine refuses."""
     import torch
