@@ -108,10 +108,22 @@ def mixed_table_vlens(max_bytes, vmin, vmax, tomb_frac, seed):
     return v[: int(np.searchsorted(c, max_bytes, side="right"))]
 
 
-def mixed_sst_host(m, krange, vrange, tomb_frac, seed):
+def span_rows(offs, klens, vlens):
+    """The spans a decode of a generated table must return (record offsets,
+    key and value lengths as generated) as (n, 2) uint64 rows {off, klen |
+    vlen << 32}: the hg_span layout, for checks by generator truth."""
+    offs = np.asarray(offs, dtype=np.uint64)
+    out = np.empty((offs.size, 2), dtype=np.uint64)
+    out[:, 0] = offs
+    out[:, 1] = np.asarray(klens, dtype=np.uint64) | (np.asarray(vlens, dtype=np.uint64) << np.uint64(32))
+    return out
+
+
+def mixed_sst_host(m, krange, vrange, tomb_frac, seed, layout=False):
     """numpy SSTable of m records, key lengths uniform in krange = (lo, hi)
     and value lengths in vrange (hi exclusive), tomb_frac of the values
-    tombstones, random key/value bytes (tools/decode_variants.py shapes)."""
+    tombstones, random key/value bytes (tools/decode_variants.py shapes).
+    layout: also the generated (offsets, klens, vlens)."""
     rng = np.random.default_rng(seed)
     kl = rng.integers(*krange, m)
     vl = rng.integers(*vrange, m)
@@ -121,4 +133,4 @@ def mixed_sst_host(m, krange, vrange, tomb_frac, seed):
     hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
     for i in range(16):
         buf[offs[:-1] + i] = hdr[:, i]
-    return buf
+    return (buf, offs[:-1], kl, vl) if layout else buf
