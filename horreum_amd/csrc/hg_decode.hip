@@ -294,6 +294,24 @@ __device__ __forceinline__ void copy_span(hg_span* dst, const hg_span* src, uint
     *reinterpret_cast<uint4*>(dst) = v;
 }
 
+// store_span for headers whose high words are known zero (the lane walks
+// checked them): two 32-bit halves by byte funnel shifts from dword reads
+// instead of 64-bit shifts.
+#ifndef HG_LW_ST32
+#define HG_LW_ST32 1
+#endif
+__device__ __forceinline__ void lw_store_span(hg_span* out, uint64_t gi, const uint8_t* data,
+                                              uint64_t base, uint32_t p) {
+    if (!HG_LW_ST32) {
+        store_span(out, ~0ull, gi, data, base, p);
+        return;
+    }
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(data + (p & ~3u));
+    const uint32_t sh = p & 3u;
+    write_span(out, gi, base + p, __builtin_amdgcn_alignbyte(w[1], w[0], sh),
+               __builtin_amdgcn_alignbyte(w[3], w[2], sh));
+}
+
 // ---- relaxation ---------------------------------------------------------------
 // Exact per-lane state for piece entry X (absolute).  All threads call it.
 // Each lane caches one walk (from guess g).  A lane is a pass-through when
@@ -1974,7 +1992,8 @@ __device__ __forceinline__ uint32_t lw_fetch_chunk(const DecodeArgs& a, uint64_t
 }
 
 // Granule zero masks of the staged chunk into zm (conflict-free: lane l reads
-// granules l, l+64, l+128, l+192 and the halo's).
+// granules l, l+64, l+128, l+192 and the halo's).  These masks are a large
+// share of the mode's VALU work (zmask4: one multiply gathers the flags).
 __device__ __forceinline__ void lw_chunk_masks(const uint8_t* buf, uint16_t* zm) {
     const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
@@ -2250,7 +2269,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
         const uint32_t cmax = __builtin_amdgcn_readlane((int)dpp_max_incl(c), 63);
         const uint32_t pre = incl - c;
         for (uint32_t i = 0; i < cmax; ++i)  // one store instruction per step
-            if (i < c) store_span(out, ~0ull, pre + i, data, cb, walk_pos(w, i));
+            if (i < c) lw_store_span(out, pre + i, data, cb, walk_pos(w, i));
         nstores = cmax;
     }
     LW_STAMP(4);

@@ -49,14 +49,12 @@ class Index:
         pos = spans["off"][first].astype(np.int64)
         last = spans[-1]
         end = int(last["off"]) + 16 + int(last["klen"]) + int(last["vlen"])
-        nxt = np.append(pos[1:], end)
+        lens = np.diff(np.append(pos, end))
+        kl = spans["klen"][first].astype(np.int64)
         mv = memoryview(data).cast("B")
-        items = []
-        for i, r in enumerate(first.tolist()):
-            k0 = int(spans["off"][r]) + 16
-            items.append(Block(bytes(mv[k0:k0 + int(spans["klen"][r])]), int(pos[i]),
-                               int(nxt[i] - pos[i])))
-        return cls(items)
+        # plain-int lists: no numpy scalar per field in the per-block loop
+        return cls(Block(bytes(mv[p + 16:p + 16 + k]), p, ln)
+                   for p, k, ln in zip(pos.tolist(), kl.tolist(), lens.tolist()))
 
     @classmethod
     def from_encoded(cls, data, blocks):

@@ -5,12 +5,17 @@ The byte work -- encoding on write, decoding on open / get / get_all, the
 block index -- runs in libhorreum_gpu.so; this module does file I/O and the
 reference's host logic (binary searches, size accounting) only.
 
-Host memory: a table file is mmap'd once and the mapping is
-page-locked with hg_host_register, so every later transfer of its bytes
-(open, get_all, compaction) is a direct DMA from the page cache's pages --
-no read() copy and no staging copy.  A directory opens with one batched
-decode of all its tables (SSTableManager).  Batched lookups keep the table,
-its spans and its key index resident in HBM after the first batch.
+Host memory (SURVEY §8 f4): a table file is mmap'd once (no read() copy);
+its transfers go through the engine's pinned staging, the page faults and
+copies split over host threads.  Page-locking the mapping with
+hg_host_register (`PersistedFile.pin`, or `mapped(register=True)`) makes
+every later transfer a direct DMA, but pinning runs at ~4-6 GB/s on the
+MI355X box against ~45 GiB/s for the staged transfer (cold open of 32 x 64
+MiB files: 370-600 ms to register vs ~50 ms to decode through staging), so
+it pays only for a mapping moved many times and is off by default.  A
+directory opens with one batched decode of all its tables (SSTableManager).
+Batched lookups keep the table, its spans and its key index resident in HBM
+after the first batch.
 
 Quirks kept from the reference:
 - `PersistedFile.new` opens with create+write+read and NO truncate
@@ -61,11 +66,14 @@ class PersistedFile:
             raise FileNotFoundError(path)
         return cls(path)
 
-    def mapped(self, engine=None):
-        """The whole file as a uint8 array over a private mmap of it,
-        page-locked with hg_host_register when the engine can (so transfers
-        are direct DMA); the mapping lives until delete() / unmap()."""
+    def mapped(self, engine=None, register=False):
+        """The whole file as a uint8 array over a private mmap of it; with
+        `register`, page-locked with hg_host_register when the engine can (so
+        transfers are direct DMA).  The mapping lives until delete() /
+        unmap()."""
         if self._map is not None:
+            if register and self._map[2] is None and self._map[0] is not None:
+                self._register(engine)
             return self._map[1]
         size = os.path.getsize(self.path)
         if size == 0:
@@ -74,16 +82,24 @@ class PersistedFile:
         with open(self.path, "rb") as fh:
             mm = mmap.mmap(fh.fileno(), size, access=mmap.ACCESS_COPY)
         arr = np.frombuffer(mm, dtype=np.uint8)
-        reg = None
+        self._map = (mm, arr, None)
+        if register:
+            self._register(engine)
+        return arr
+
+    def _register(self, engine=None):
+        mm, arr, _ = self._map
         try:
             from .engine import default_engine
             eng = engine or default_engine()
             eng.host_register(arr)
-            reg = eng
-        except Exception:  # noqa: BLE001 -- pageable fallback (staged copies)
-            reg = None
-        self._map = (mm, arr, reg)
-        return arr
+            self._map = (mm, arr, eng)
+        except Exception:  # noqa: BLE001 -- pageable (staged copies) stays
+            pass
+
+    def pin(self, engine=None):
+        """Map and page-lock the file for repeated direct-DMA transfers."""
+        return self.mapped(engine, register=True)
 
     def unmap(self):
         if self._map is None:

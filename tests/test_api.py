@@ -258,12 +258,16 @@ def test_no_truncate_overwrite_fails_decode(engine, golden, tmp_path):
 
 @pytest.mark.gpu
 def test_mapped_file_is_page_locked(engine, golden, tmp_path):
-    """a table file is mmap'd and registered once; its bytes
-    then go to the device by direct DMA (hg_host_is_pinned)."""
+    """a table file is mmap'd once (pageable: staged
+    transfers); PersistedFile.pin page-locks the same mapping so its bytes go
+    to the device by direct DMA (hg_host_is_pinned); both read the same."""
     c = golden["storage_read"]
     f = PersistedFile.new(tmp_path / "m", _pairs(c), engine)
     arr = f.mapped(engine)
     assert bytes(arr) == bytes.fromhex(c["bytes"])
+    assert not engine.host_is_pinned(arr)
+    assert f.read_all(engine) == _pairs(c)
+    assert f.pin(engine) is arr
     assert engine.host_is_pinned(arr)
     assert f.read_all(engine) == _pairs(c)
     f.delete()
