@@ -2022,11 +2022,18 @@ __device__ __forceinline__ void lw_masks(const uint16_t* zm, uint32_t seg0, uint
         c64 = 1;
     } else {  // 80-bit shifts as 64 + 16 bits
         const uint32_t hi = z1 & 0xFFFFu;
-        uint64_t alo = z0;
-        uint32_t ahi = hi;
-        for (uint32_t k = 1; k < hz; ++k) {  // bit i of A: bytes i .. i+hz-1 are zero
-            alo &= (z0 >> k) | ((uint64_t)hi << (64 - k));
-            ahi &= hi >> k;
+        uint64_t alo = z0;  // bit i of A: bytes i .. i+hz-1 are zero, by doubling:
+        uint32_t ahi = hi;  // A_2p = A_p & (A_p >> p), then one overlapping step
+        uint32_t pw = 1;
+        while (2 * pw <= hz) {
+            alo &= (alo >> pw) | ((uint64_t)ahi << (64 - pw));
+            ahi &= ahi >> pw;
+            pw *= 2;
+        }
+        if (pw < hz) {
+            const uint32_t r = hz - pw;
+            alo &= (alo >> r) | ((uint64_t)ahi << (64 - r));
+            ahi &= ahi >> r;
         }
         const uint32_t s1 = 8 - hz, s2 = 16 - hz;  // s1 in [0, 7], s2 in [8, 15]
         const uint64_t a1 = s1 ? ((alo >> s1) | ((uint64_t)ahi << (64 - s1))) : alo;

@@ -39,12 +39,16 @@ __device__ __forceinline__ void st_agent(unsigned long long* p, unsigned long lo
 // on bits 32..35 of the product and every other partial product on a
 // distinct bit, so nothing carries (lane-walk decode: 5-8 % faster than
 // shift-and-mask gathering, the masks being a large share of its VALU work).
-__device__ __forceinline__ uint32_t zmask4(uint32_t x) {
+// zflags: the 4 flags in bits 0..3, other partial products at bits 8-10, 16,
+// 17 and 24 (left in place by zmask16: shifted by 8 or 12 they land at 16+).
+__device__ __forceinline__ uint32_t zflags(uint32_t x) {
     const uint32_t t = ((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x;  // byte MSB set <=> byte != 0
-    return __umulhi(~t & 0x80808080u, 0x02040810u) & 0xFu;
+    return __umulhi(~t & 0x80808080u, 0x02040810u);
 }
+__device__ __forceinline__ uint32_t zmask4(uint32_t x) { return zflags(x) & 0xFu; }
 __device__ __forceinline__ uint32_t zmask16(uint4 v) {
-    return zmask4(v.x) | (zmask4(v.y) << 4) | (zmask4(v.z) << 8) | (zmask4(v.w) << 12);
+    return (((zflags(v.x) | (zflags(v.y) << 4)) & 0xFFu) | (zflags(v.z) << 8) |
+            (zflags(v.w) << 12)) & 0xFFFFu;
 }
 
 // Unaligned little-endian u64 pair (klen, vlen) at byte offset p of an

@@ -44,6 +44,7 @@ constexpr uint32_t THREADS = 256;
 #endif
 constexpr uint32_t TILE = HG_MERGE_TILE;  // merged positions per workgroup
 constexpr uint32_t EPT = TILE / THREADS;
+constexpr uint32_t WPT = 3 * TILE / THREADS;  // 8-byte words of a tile's entries per thread
 constexpr uint32_t DEAD = 0x80000000u;
 constexpr uint32_t MAX_TABLES = 1u << 16;
 
@@ -389,12 +390,23 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
         }
         const uint64_t j0 = (d0 - o) - i0, j1 = (d1 - o) - i1;
         const uint32_t nA = (uint32_t)(i1 - i0), nB = (uint32_t)(j1 - j0);
-        {  // both segments as 8-byte words, contiguous per lane (entries are 24 B)
+        {  // both segments as 8-byte words, contiguous per lane (entries are 24 B);
+           // every load of a thread is issued before its first LDS write (a
+           // load / wait / write loop paid one HBM round trip per word, 12 per
+           // thread per tile); a word past the segments re-reads the last one
             const uint64_t* wa = reinterpret_cast<const uint64_t*>(A + i0);
             const uint64_t* wb = reinterpret_cast<const uint64_t*>(B + j0);
             uint64_t* ws = reinterpret_cast<uint64_t*>(s.seg);
-            for (uint32_t q = tid; q < 3 * nA; q += THREADS) ws[q] = wa[q];
-            for (uint32_t q = tid; q < 3 * nB; q += THREADS) ws[3 * nA + q] = wb[q];
+            const uint32_t wA = 3 * nA, wT = 3 * (nA + nB);  // wT >= 3: d1 > d0
+            uint64_t v[WPT];
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i) {
+                const uint32_t q = min(tid + i * THREADS, wT - 1);
+                v[i] = *(q < wA ? wa + q : wb + (q - wA));
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < WPT; ++i)
+                if (tid + i * THREADS < wT) ws[tid + i * THREADS] = v[i];
         }
         if (tid == THREADS - 1) {
             s.has_prev = i0 > 0;
@@ -474,15 +486,23 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                 }
                 hg_pair* lp = reinterpret_cast<hg_pair*>(s.seg);
                 uint32_t r = fpre;
+                // the spans of this thread's outputs, every load issued
+                // before the first is used (branch-free: an output past the
+                // tile or dead looks up entry 0 and is dropped below)
+                uint32_t tk[EPT];
+                hg_span spk[EPT];
 #pragma unroll
                 for (uint32_t k = 0; k < EPT; ++k) {
-                    if (d + k >= e) break;
-                    const MEnt& x = fx[k];
-                    if (x.gd & DEAD) continue;
-                    uint32_t t;
-                    const hg_span sp = ent_span(a, x, t);
+                    const uint64_t g = d + k < e ? (uint64_t)(fx[k].gd & ~DEAD) : 0ull;
+                    tk[k] = run_of(a, g);
+                    spk[k] = a.spans[tk[k]][g - a.run_off[tk[k]]];
+                }
+#pragma unroll
+                for (uint32_t k = 0; k < EPT; ++k) {
+                    if (d + k >= e || (fx[k].gd & DEAD)) continue;
+                    const hg_span sp = spk[k];
                     hg_pair p;
-                    p.key_off = a.table_off[t] + sp.off + 16;
+                    p.key_off = a.table_off[tk[k]] + sp.off + 16;
                     p.val_off = p.key_off + sp.klen;
                     p.klen = sp.klen;
                     p.vlen = sp.vlen;

@@ -195,6 +195,17 @@ def _fake_header_table(n, fake_at, fake_k, fake_v, seed):
     return data
 
 
+def test_fake_headers_cfg2_size(engine):
+    """The adversarial table at BASELINE cfg 2 size (8.13 M records, 1 GiB):
+    every record's value carries a self-consistent fake header, so every
+    pre-pass batch's entry guess can lock onto the wrong phase and chains of
+    wrong-guess batches wait on each other's exact redo (the
+    look-back budget must not turn a valid file into an error)."""
+    data = _fake_header_table(8_134_407, 10, 4, 96, seed=12)
+    assert data.size == 1_073_741_724
+    assert_same(engine, data)
+
+
 @pytest.mark.parametrize("fake", [(10, 4, 96), (40, 0, 100), (2, 50, 50), (60, 1, 3)])
 def test_fake_headers_in_values(engine, fake):
     """Adversarial phase: every record carries a self-consistent fake header.

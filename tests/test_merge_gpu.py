@@ -235,6 +235,21 @@ def test_merge_unsorted_multi_tile(engine):
     _exact_case(engine, tables)
 
 
+@pytest.mark.parametrize("j", [1095, 1096, 2119])
+def test_merge_disorder_at_prep_workgroup_edge(engine, j):
+    """A single inversion whose second record is the first (or last) entry of
+    a prep workgroup (256 entries; global index 3000 + j): the order check
+    compares a workgroup's first entry with a predecessor it rebuilds.  The
+    exact loop's output (oracle.compact) must follow."""
+    tables = sorted_tables(2, 9000, 0.6, 23)
+    tables[0] = tables[0][:3000]
+    bad = list(tables[1])
+    assert len(bad) > 2200
+    bad[j - 1], bad[j] = bad[j], bad[j - 1]
+    tables[1] = bad
+    _exact_case(engine, tables)
+
+
 @pytest.mark.parametrize("stride", [0, 3])
 def test_compact_host_unsorted(engine, stride):
     """decode -> exact merge -> encode of tables with duplicate / unordered
