@@ -45,6 +45,7 @@ constexpr uint32_t THREADS = 256;
 constexpr uint32_t TILE = HG_MERGE_TILE;  // merged positions per workgroup
 constexpr uint32_t EPT = TILE / THREADS;
 constexpr uint32_t WPT = 3 * TILE / THREADS;  // 8-byte words of a tile's entries per thread
+constexpr uint32_t FIN_LDS_TABLES = 64;
 constexpr uint32_t DEAD = 0x80000000u;
 constexpr uint32_t MAX_TABLES = 1u << 16;
 
@@ -338,9 +339,22 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
     __shared__ LevelSmem s;
     __shared__ uint32_t fin_tmp[THREADS / 64];
     __shared__ uint64_t fin_base;
+    // FINAL: the tables' run offsets, span arrays and arena offsets in LDS
+    // (up to FIN_LDS_TABLES tables), so a live record's span lookup is one
+    // HBM load after an LDS search instead of a chain of dependent loads
+    __shared__ uint64_t fin_roff[FIN_LDS_TABLES + 1], fin_sp[FIN_LDS_TABLES],
+        fin_toff[FIN_LDS_TABLES];
     const uint32_t tid = threadIdx.x;
     const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
     if (t0 >= a.n) return;
+    const bool fin_lds = FINAL && a.ntables <= FIN_LDS_TABLES;
+    if (fin_lds) {  // read after the segment staging's barrier
+        if (tid <= a.ntables) fin_roff[tid] = a.run_off[tid];
+        if (tid < a.ntables) {
+            fin_sp[tid] = reinterpret_cast<uint64_t>(a.spans[tid]);
+            fin_toff[tid] = a.table_off[tid];
+        }
+    }
     // A FINAL tile that stops early still publishes its status (count 0), so
     // no later tile waits on it; the exact loop then redoes the merge.
     auto fin_abort = [&]() {
@@ -491,18 +505,32 @@ __global__ __launch_bounds__(THREADS) void merge_level_kernel(MergeArgs a, Level
                 // tile or dead looks up entry 0 and is dropped below)
                 uint32_t tk[EPT];
                 hg_span spk[EPT];
+                uint64_t tof[EPT];
 #pragma unroll
                 for (uint32_t k = 0; k < EPT; ++k) {
                     const uint64_t g = d + k < e ? (uint64_t)(fx[k].gd & ~DEAD) : 0ull;
-                    tk[k] = run_of(a, g);
-                    spk[k] = a.spans[tk[k]][g - a.run_off[tk[k]]];
+                    if (fin_lds) {
+                        uint32_t lo = 0, hi = a.ntables;  // last run with fin_roff[r] <= g
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (fin_roff[mid] <= g) lo = mid;
+                            else hi = mid;
+                        }
+                        tk[k] = lo;
+                        tof[k] = fin_toff[lo];
+                        spk[k] = reinterpret_cast<const hg_span*>(fin_sp[lo])[g - fin_roff[lo]];
+                    } else {
+                        tk[k] = run_of(a, g);
+                        tof[k] = a.table_off[tk[k]];
+                        spk[k] = a.spans[tk[k]][g - a.run_off[tk[k]]];
+                    }
                 }
 #pragma unroll
                 for (uint32_t k = 0; k < EPT; ++k) {
                     if (d + k >= e || (fx[k].gd & DEAD)) continue;
                     const hg_span sp = spk[k];
                     hg_pair p;
-                    p.key_off = a.table_off[tk[k]] + sp.off + 16;
+                    p.key_off = tof[k] + sp.off + 16;
                     p.val_off = p.key_off + sp.klen;
                     p.klen = sp.klen;
                     p.vlen = sp.vlen;
