@@ -69,13 +69,18 @@ def aggregate(wall_max_s, steps, world, bytes_per_rank):
     return world * bytes_per_rank / (wall_max_s / steps) / GIB
 
 
+def _backend():
+    return os.environ.get("HG_BENCH_DIST_BACKEND", "nccl")
+
+
 def max_over_ranks(value, world, device=None):
     """Max of a float across ranks (identity when world == 1)."""
     if world == 1:
         return value
     import torch
     import torch.distributed as dist
-    t = torch.tensor([value], dtype=torch.float64, device=device)
+    t = torch.tensor([value], dtype=torch.float64,
+                     device=None if _backend() == "gloo" else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -83,7 +88,7 @@ def max_over_ranks(value, world, device=None):
 def barrier(world, device=None):
     if world > 1:
         import torch.distributed as dist
-        if device is not None and device.type == "cuda":
+        if device is not None and device.type == "cuda" and _backend() != "gloo":
             dist.barrier(device_ids=[device.index])
         else:
             dist.barrier()
@@ -267,10 +272,18 @@ def main(argv=None):
     args = parse(argv)
     rank, world, local = dist_env()
     import torch
+    if os.environ.get("HG_BENCH_SHARE_GPU") == "1":
+        # rehearsal of the N > 1 path on a one-GPU box (ranks share the card,
+        # gloo for the timing collectives); the driver's runs never set it
+        local = local % max(1, torch.cuda.device_count())
+        os.environ["HG_BENCH_DIST_BACKEND"] = "gloo"
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if _backend() == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
