@@ -1171,6 +1171,11 @@ __device__ uint64_t spec_base(const DecodeArgs& a, uint32_t e) {
     return wave_sum<uint64_t>(v);
 }
 
+#ifndef HG_EMIT_U
+#define HG_EMIT_U 4
+#endif
+constexpr uint32_t EMIT_U = HG_EMIT_U;  // scratch spans in flight per thread (emit_spec_range)
+
 // Spans of pieces [q0, q0 + n) (n <= SPEC_BP) from their pre-pass summaries
 // (stride arithmetic, or the hop walk's scratch), record base g0.  All
 // threads; returns the record index after the last piece.
@@ -1184,13 +1189,63 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
     __syncthreads();
     if (tid == 0) {
         uint64_t g = g0;
+        uint32_t hop = 0;
         for (uint32_t i = 0; i < n; ++i) {
             pbase[i] = g;
             g += pc[i].count;
+            hop |= pc[i].pad == SP_HOP;
         }
         pbase[SPEC_BP] = g;
+        pbase[SPEC_BP + 1] = hop;
     }
     __syncthreads();
+    if (uni(pbase[SPEC_BP + 1])) {
+        // Batches with walked pieces (hop / lane-walk spans in scratch): the
+        // copies run over the batch's records flattened, EMIT_U per thread
+        // with every load issued before the first store (per piece, one
+        // load / wait / store round per 256 records had made this a chain
+        // of ~2 HBM round trips per piece).
+        const uint64_t total = uni(pbase[SPEC_BP]) - g0;
+        for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)THREADS * EMIT_U) {
+            uint4 v[EMIT_U];
+            uint32_t pi[EMIT_U];
+            uint64_t tt[EMIT_U];
+    #pragma unroll
+            for (uint32_t u = 0; u < EMIT_U; ++u) {
+                const uint64_t j = min(j0 + u * THREADS + tid, total - 1);
+                const uint64_t gp = g0 + j;
+                uint32_t lo = 0, hi = n;  // the piece holding record gp: last pbase <= gp
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pbase[mid] <= gp) lo = mid;
+                    else hi = mid;
+                }
+                pi[u] = lo;
+                tt[u] = gp - pbase[lo];
+                const hg_span* src = a.scratch + (size_t)(q0 + lo) * MAX_REC_PIECE + tt[u];
+                v[u] = pc[lo].pad == SP_HOP ? *reinterpret_cast<const uint4*>(src)
+                                            : make_uint4(0, 0, 0, 0);
+            }
+    #pragma unroll
+            for (uint32_t u = 0; u < EMIT_U; ++u) {
+                const uint64_t j = j0 + u * THREADS + tid;
+                const uint64_t gp = g0 + j;
+                if (j >= total || gp >= a.cap) continue;
+                const SpecPiece& q = pc[pi[u]];
+                if (q.pad == SP_HOP) {
+                    const uint64_t off = (((uint64_t)v[u].y << 32) | v[u].x) + a.obase;
+                    v[u].x = (uint32_t)off;
+                    v[u].y = (uint32_t)(off >> 32);
+                    *reinterpret_cast<uint4*>(a.spans + gp) = v[u];
+                } else {
+                    write_span(a.spans, gp, a.obase + q.x + tt[u] * q.R, q.kl, q.vl);
+                }
+            }
+        }
+        const uint64_t end = uni(pbase[SPEC_BP]);
+        __syncthreads();
+        return end;
+    }
     for (uint32_t i = 0; i < n; ++i) {
         const uint64_t g = uni(pbase[i]);
         const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
