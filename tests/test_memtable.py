@@ -1,5 +1,7 @@
 """MemTable bookkeeping and flush path (reference src/memtable/mod.rs): the
-reference's own tests, size-accounting parity with the oracle restatement
+reference's own tests, the size accounting pinned by a known-answer trace
+derived by hand from the reference text (mod.rs:75-120; the reference's own
+tests never check actual_size), then parity with the oracle restatement
 over random operation sequences (including the usize wrap of a shorter
 re-put), the arena snapshot, and -- on the GPU -- flush -> encode -> table."""
 import numpy as np
@@ -73,6 +75,44 @@ def test_size_accounting_parity(seed, limit):
                for p in desc]
         # Some(b"") and None are the same record on the wire (src/format.rs:29-33)
         assert got == [(k, v if v else None) for k, v in pairs]
+
+
+# Known answers for the size accounting, derived by hand from the reference
+# text (src/memtable/mod.rs), not from either implementation:
+#   put  :84-87 Some(Some(old)) += new_v - old_v (usize, wrapping)
+#        :88-90 Some(None)      += new_v
+#        :91-94 None            += key + new_v
+#        :99-104 then, if actual_size > size_limit: flush, actual_size = 0
+#   delete :108-118 inserts None; if the old value was Some(v): -= len(v)
+KNOWN_TRACE = [  # (op, key, value, actual_size after, flush sizes so far)
+    ("put", b"abc", b"def", 6, []),            # None: 3 + 3
+    ("put", b"xyz", b"xxx", 12, []),           # None: 3 + 3
+    ("put", b"xyz", b"qwerty", 15, []),        # Some(Some): 15 = 12 + 6 - 3
+    ("del", b"abc", None, 12, []),             # -3, the key stays counted
+    ("del", b"abcdef", None, 12, []),          # absent: None inserted, nothing counted
+    ("put", b"abcdef", b"zz", 14, []),         # Some(None): + 2 only
+    ("put", b"abc", b"", 14, []),              # Some(None): + 0
+    ("put", b"abc", b"1", 15, []),             # Some(Some(b"")): + 1 - 0
+    ("put", b"xyz", b"q", 10, []),             # Some(Some(b"qwerty")): + 1 - 6
+    ("put", b"k", b"vvvvvvvvvvvvvvvvvvvv", 0, [31]),  # None: 10 + 1 + 20 = 31 > 30: flush at 31
+    ("put", b"k", b"v", 2, [31]),              # the map was cleared: None, 1 + 1
+    ("del", b"k", None, 1, [31]),              # -1
+]
+
+
+def test_size_accounting_known_answers():
+    flushed = []
+    t = MemTable(30, on_flush=lambda arena, desc, size: flushed.append(size))
+    for op, k, v, want, want_flushes in KNOWN_TRACE:
+        if op == "put":
+            t.put(k, v)
+        else:
+            t.delete(k)
+        assert (t.actual_size, flushed) == (want, want_flushes), (op, k, v)
+    ref = RefMemTable(30)  # the oracle restatement agrees with the same trace
+    for op, k, v, want, want_flushes in KNOWN_TRACE:
+        ref.put(k, v) if op == "put" else ref.delete(k)
+        assert (ref.actual_size, [sz for _, sz in ref.flushes]) == (want, want_flushes)
 
 
 def test_delete_created_key_never_counts_its_key():
