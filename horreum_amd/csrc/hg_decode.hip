@@ -1979,7 +1979,10 @@ constexpr uint32_t LW_CPP = PIECE / LW_CHUNK;   // chunks per piece
 static_assert(LW_ZM_WORDS == LW_CHUNK / 16 + 8, "lane-walk mask rows");
 static_assert(4 * LW_CBUF <= PIECE + 512, "two waves' chunk buffers per piece buffer");
 constexpr uint32_t LW_WROUNDS = 64;             // relaxation rounds before lane 0 walks it
-constexpr uint32_t LW_TRIES = 2;                // candidates a lane examines for its guess
+#ifndef HG_LW_TRIES
+#define HG_LW_TRIES 1  // 2: small and medium 1.3 % slower (the second try rarely pays for its reads)
+#endif
+constexpr uint32_t LW_TRIES = HG_LW_TRIES;      // candidates a lane examines for its guess
 constexpr uint32_t LW_PROF = 8;
 constexpr uint64_t LW_GUESS = ~0ull;            // "enter at the first linked lane guess"
 // Diagnostics (a.sdiag != null, tools/lw_diag.py): lane 0 of wave 0 charges the
