@@ -41,6 +41,10 @@ constexpr uint32_t ENC_TILE = ENC_THREADS * ENC_RPT;     // records per tile (wo
 #define HG_ENC_U 4
 #endif
 constexpr uint32_t ENC_U = HG_ENC_U;  // 16-byte pieces in flight per lane
+#ifndef HG_ENC_U_GATHER
+#define HG_ENC_U_GATHER 1
+#endif
+constexpr uint32_t ENC_U_GATHER = HG_ENC_U_GATHER;  // the same for gathered pairs
 #ifndef HG_ENC_PRE
 #define HG_ENC_PRE 1
 #endif
@@ -273,6 +277,10 @@ __device__ __forceinline__ void enc_store(const EncodeSmem& s, const EncodeArgs&
 
 template <bool NTL>
 __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
+    // pieces in flight per lane: streaming sources want several; gathered
+    // ones (a compaction's merged order) run faster with one and more
+    // resident waves (cfg 5 leg: 450 -> 424 us; ENC_U 2: 428, 3: 451)
+    constexpr uint32_t U = NTL ? ENC_U : ENC_U_GATHER;
     __shared__ EncodeSmem s;
     const uint32_t tid = threadIdx.x;
     const uint32_t t = blockIdx.x;
@@ -341,7 +349,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
     __syncthreads();
 
     // ---- 2. first pieces in flight, then the look-back ----------------------------
-    // Sources do not depend on the tile's output offset, so the first ENC_U
+    // Sources do not depend on the tile's output offset, so the first U
     // pieces per lane are loaded before the look-back and land while it runs.
     // The copy loop is software-pipelined: the loads of step i+1 are issued
     // before the stores of step i (vmcnt counts loads and stores together, in
@@ -365,7 +373,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
         un.c = un.on ? (uint32_t)((un.R + 15) >> 4) : 1u;
     }
     // a piece without a 16-byte source loads the descriptors' first 16 bytes
-    // (branch-free, so all ENC_U loads are in flight together)
+    // (branch-free, so all U loads are in flight together)
     const uint8_t* safe = reinterpret_cast<const uint8_t*>(a.pairs);
     // ENC_PRE steps of pieces are loaded first; the tile's output offset is
     // read meanwhile: its group's base plus the sums of the tiles before it
@@ -393,12 +401,12 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
     // ---- 3. piece copy ----------------------------------------------------------
     // Unrolled by two with swapped roles, so the in-flight loads are never
     // moved between registers (a move would wait for them).
-    constexpr uint32_t STEP = ENC_THREADS * ENC_U;
+    constexpr uint32_t STEP = ENC_THREADS * U;
     const uint32_t p0 = tid + ENC_PRE * ENC_THREADS;  // first piece of the pipelined loop
-    EncPiece cur[ENC_U], nx[ENC_U];
-    uint4 vc[ENC_U], vn[ENC_U];
+    EncPiece cur[U], nx[U];
+    uint4 vc[U], vn[U];
 #pragma unroll
-    for (uint32_t u = 0; u < ENC_U; ++u) {
+    for (uint32_t u = 0; u < U; ++u) {
         cur[u] = enc_resolve(s, a, p0 + u * ENC_THREADS, ptot, nrec, pscale, un);
         vc[u] = ld_stream16<NTL>(cur[u].kind == 2 ? cur[u].src : safe);
     }
@@ -406,12 +414,12 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
     for (uint32_t k = 0; k < ENC_PRE; ++k) enc_store(s, a, pre[k], vpre[k], tb);
     auto step = [&](EncPiece* c, uint4* vcur, EncPiece* n, uint4* vnext, uint32_t pb) {
 #pragma unroll
-        for (uint32_t u = 0; u < ENC_U; ++u) {
+        for (uint32_t u = 0; u < U; ++u) {
             n[u] = enc_resolve(s, a, pb + STEP + u * ENC_THREADS, ptot, nrec, pscale, un);
             vnext[u] = ld_stream16<NTL>(n[u].kind == 2 ? n[u].src : safe);
         }
 #pragma unroll
-        for (uint32_t u = 0; u < ENC_U; ++u) enc_store(s, a, c[u], vcur[u], tb);
+        for (uint32_t u = 0; u < U; ++u) enc_store(s, a, c[u], vcur[u], tb);
     };
     for (uint32_t pb = p0; pb < ptot; pb += 2 * STEP) {
         step(cur, vc, nx, vn, pb);
