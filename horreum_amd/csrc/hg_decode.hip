@@ -1636,7 +1636,10 @@ __global__ __launch_bounds__(THREADS, 4) void decode_guess_kernel(DecodeArgs a, 
 }
 
 template <bool DIAG>
-__global__ __launch_bounds__(THREADS, 4) void decode_kernel(DecodeArgs a) {
+#ifndef HG_DEC_WAVES
+#define HG_DEC_WAVES 4
+#endif
+__global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_kernel(DecodeArgs a) {
     decode_body<DIAG>(a, blockIdx.x);
 }
 
@@ -2724,7 +2727,7 @@ __global__ __launch_bounds__(THREADS, 4) void decode_lw_multi(const DecodeArgs* 
 
 // Same register bound as decode_kernel (4 waves/SIMD); the table index is
 // block-uniform, so its arguments are fetched with scalar loads into a copy.
-__global__ __launch_bounds__(THREADS, 4) void decode_multi(const DecodeArgs* tabs,
+__global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_multi(const DecodeArgs* tabs,
                                                            const uint32_t* pre, uint32_t ntab) {
     const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
     const DecodeArgs a = tabs[t];

@@ -19,7 +19,7 @@
 //   2. and in the same pass: each table strictly increasing (else step 5).
 //   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
-//      positions, takes its A/B split from merge_split_kernel (a 16-ary
+//      positions, takes its A/B split from merge_split_kernel (an 8-ary
 //      search per tile boundary, all boundaries at once), stages
 //      both segments in LDS, and each thread finds its 4 outputs' split by one
 //      binary search on its diagonal and merges them sequentially (ties: A
@@ -227,10 +227,13 @@ __device__ __forceinline__ void pair_of(const LevelArgs& l, uint64_t d, uint32_t
 // start of a round, all boundaries at once: the merge-path searches'
 // dependent HBM probes overlap across the grid instead of sitting at the head
 // of every tile of the round.  SPLIT_G lanes per boundary run a SPLIT_G-ary
-// search (~log16(run) dependent rounds of SPLIT_G probes of two entries):
+// search (~log8(run) dependent rounds of SPLIT_G probes of two entries):
 // one lane per boundary (a binary search, ~20 dependent probes) was bound by
 // the probes' latency, one wave per boundary (64-ary) by the bytes it moved.
-constexpr uint32_t SPLIT_G = 16;
+#ifndef HG_SPLIT_G
+#define HG_SPLIT_G 8  // cfg5 leg: 8-ary 21 us per round, 4-ary 25, 16-ary 29
+#endif
+constexpr uint32_t SPLIT_G = HG_SPLIT_G;
 __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, LevelArgs l,
                                                               const MEnt* in, uint64_t* split,
                                                               uint64_t nb_tiles,
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
                 const uint64_t c = lo + span * j / SPLIT_G;  // < hi
                 const bool after = key_cmp(a, A[c], B[dd - c - 1]) > 0;
                 const uint32_t m =
-                    (uint32_t)(__ballot(after) >> gsh) & ((1u << SPLIT_G) - 1u);
+                    (uint32_t)((__ballot(after) >> gsh) & ((2ull << (SPLIT_G - 1)) - 1ull));
                 if (!m) {
                     lo = lo + span * (SPLIT_G - 1) / SPLIT_G + 1;
                 } else {
