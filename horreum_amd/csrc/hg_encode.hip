@@ -38,7 +38,7 @@ constexpr uint32_t ENC_THREADS = 256;
 constexpr uint32_t ENC_RPT = HG_ENC_RPT;                 // records per thread
 constexpr uint32_t ENC_TILE = ENC_THREADS * ENC_RPT;     // records per tile (workgroup)
 #ifndef HG_ENC_U
-#define HG_ENC_U 4
+#define HG_ENC_U 6  // cfg 3: 6 -> 1.12 ms, 4 -> 1.145 (a shuffled mixed-size pair order prefers 4: 0.66 vs 0.72 ms)
 #endif
 constexpr uint32_t ENC_U = HG_ENC_U;  // 16-byte pieces in flight per lane
 #ifndef HG_ENC_U_GATHER
