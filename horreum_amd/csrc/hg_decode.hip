@@ -1982,6 +1982,9 @@ constexpr uint32_t LW_CPP = PIECE / LW_CHUNK;   // chunks per piece
 static_assert(LW_ZM_WORDS == LW_CHUNK / 16 + 8, "lane-walk mask rows");
 static_assert(4 * LW_CBUF <= PIECE + 512, "two waves' chunk buffers per piece buffer");
 constexpr uint32_t LW_WROUNDS = 64;             // relaxation rounds before lane 0 walks it
+#ifndef HG_LW_LOOKAHEAD
+#define HG_LW_LOOKAHEAD 0  // 1: a guess must also read a valid next header (small/medium 2.5 % slower; zero-byte values no better)
+#endif
 #ifndef HG_LW_TRIES
 #define HG_LW_TRIES 1  // 2: small and medium 1.3 % slower (the second try rarely pays for its reads)
 #endif
@@ -2134,7 +2137,7 @@ __device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, uint32_t seg0,
             const uint64_t body = (uint64_t)k0 + v0;
             if ((k1 | v1) || body >= HG_FAR_CAND || body > rem - p - 16) continue;
             const uint64_t nx = (uint64_t)p + 16 + body;
-            if (nx < clen) {  // look-ahead: the next header must be a readable record
+            if (HG_LW_LOOKAHEAD && nx < clen) {  // look-ahead: the next header must be a readable record
                 if (nx + 16 > rem) continue;
                 lds_header32(data, (uint32_t)nx, k0, k1, v0, v1);
                 if ((k1 | v1) || (uint64_t)k0 + v0 > rem - nx - 16) continue;
