@@ -120,24 +120,27 @@ def load_traffic(kernels):
 
 
 def time_async(torch, fn, steps, warmup, world, device):
-    """Run fn() warmup+steps times; returns (wall_s_max_over_ranks, per-launch ms list)."""
+    """Run fn() warmup+steps times; returns (wall_s_max_over_ranks, per-launch
+    ms list).  The launch time is the HIP-event time of the whole timed loop
+    on its stream divided by `steps` (one event pair brackets the loop:
+    events between the steps cost ~10 us each on the cfg 2 headline,
+    tools/event_overhead.py), so it includes the gaps between launches."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize(device)
     stream = torch.cuda.current_stream(device)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     barrier(world, device)
     torch.cuda.synchronize(device)
     t0 = time.perf_counter()
-    for s, e in ev:
-        s.record(stream)
+    ev0.record(stream)
+    for _ in range(steps):
         fn()
-        e.record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize(device)
     barrier(world, device)
     wall = time.perf_counter() - t0
-    launch_ms = [s.elapsed_time(e) for s, e in ev]
+    launch_ms = [ev0.elapsed_time(ev1) / steps] * steps
     return max_over_ranks(wall, world, device), launch_ms
 
 
