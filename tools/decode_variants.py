@@ -27,7 +27,8 @@ def workloads(dev):
                              ("small mixed 0..24B/0..64B", 4_000_000, (0, 24), (0, 64)),
                              ("medium 8..64B/64..512B", 1_500_000, (8, 65), (64, 513)),
                              ("large 16B/0..16KiB", 60_000, (16, 17), (0, 16385)),
-                             ("huge 16B/0..64KiB", 15_000, (16, 17), (0, 65537))]:
+                             ("huge 16B/0..64KiB", 15_000, (16, 17), (0, 65537)),
+                             ("midlarge 16B/400..1200B", 1_000_000, (16, 17), (400, 1201))]:
         kl = rng.integers(*kr, m)
         vl = rng.integers(*vr, m)
         vl[rng.random(m) < 0.05] = 0
