@@ -146,7 +146,9 @@ struct SpecBatch {                // one per pre-pass batch
 struct DecodeCtl {
     uint32_t ticket;              // decode_kernel batch tickets
     uint32_t bad_rev;             // max over unresolved pre-pass batches b of nspec - b
-    uint32_t reserved[2];
+    uint32_t progress;            // general batches published (INCL / ERR): the look-back's
+                                  // waits restart their budget whenever it moves
+    uint32_t reserved;
 };
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
@@ -418,8 +420,24 @@ __device__ LookbackOut lookback(const DecodeArgs& a, uint32_t k, uint32_t& spins
     // The budget bounds each wait (a restart waits for a newer batch, so a
     // legitimately long chain of restarts does not add up to a false error);
     // spins_out reports the total.
+    // A wait can legitimately outlast any fixed budget: when every batch
+    // guessed wrong, each INCL is the end of a serial chain of redos below
+    // it.  So the budget counts spins without progress anywhere in the grid
+    // (DecodeCtl::progress unchanged), and only a stalled grid is an error.
     uint32_t spins = 0, spins_done = 0;
     const uint32_t SPIN_LIMIT = 1u << 22;
+    uint32_t seen = __hip_atomic_load(&a.ctl->progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    auto stalled = [&]() -> bool {
+        const uint32_t now =
+            __hip_atomic_load(&a.ctl->progress, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (now != seen) {
+            seen = now;
+            spins_done += spins;
+            spins = 0;
+            return false;
+        }
+        return ++spins > SPIN_LIMIT;
+    };
 restart:
     spins_done += spins;
     spins = 0;
@@ -445,7 +463,7 @@ restart:
             fi = incl ? __ffsll((long long)incl) - 1 : 64;
             unsigned long long relevant = fi >= 63 ? ~0ull : ((1ull << (fi + 1)) - 1ull);
             if (!(notready & relevant)) break;
-            if (++spins > SPIN_LIMIT) {
+            if (stalled()) {
                 r.err = HG_ERR_INTERNAL;
                 spins_out = spins_done + spins;
                 return r;
@@ -480,7 +498,7 @@ restart:
                 unsigned long long v0 = ld_agent(&a.status[2 * jm]);
                 unsigned long long v1 = ld_agent(&a.status[2 * jm + 1]);
                 if (st_flag(v0) == st_flag(v1) && st_flag(v0) >= ST_INCL) break;
-                if (++spins > SPIN_LIMIT) {
+                if (stalled()) {
                     r.err = HG_ERR_INTERNAL;
                     spins_out = spins_done + spins;
                     return r;
@@ -1313,6 +1331,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
                 const uint64_t ex = a.sbatch[e1 - 1].exit;
                 st_agent(&a.status[2 * b0 + 1], pack_status(ST_INCL, 0, gend));
                 st_agent(&a.status[2 * b0], pack_status(ST_INCL, (uint32_t)(gend - g0), ex));
+                __hip_atomic_fetch_add(&a.ctl->progress, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         return;
@@ -1375,6 +1394,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
                 if (tid == 0) {
                     st_agent(&a.status[2 * b + 1], pack_status(ST_INCL, 0, gk0 + ptot));
                     st_agent(&a.status[2 * b], pack_status(ST_INCL, (uint32_t)ptot, pex));
+                    __hip_atomic_fetch_add(&a.ctl->progress, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (b == a.nbatches - 1) {
                         hg_decode_result r;
                         r.n_records = gk0 + ptot;
@@ -1566,6 +1586,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             st_agent(&a.status[2 * b + 1], pack_status(ST_ERR, 0, gk + total));
             st_agent(&a.status[2 * b], pack_status(ST_ERR, (uint32_t)(kind + 16), errpos));
         }
+        __hip_atomic_fetch_add(&a.ctl->progress, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (kind == HG_OK && spec_ok) {
         uint64_t go = gres;

@@ -76,6 +76,12 @@ CORPORA = {
     "mixed_4k": (mixed, dict(n=3000, kmax=32, vmax=4096, seed=15, kmin=8, vmin=8)),
     "large_values": (mixed, dict(n=120, kmax=64, vmax=70000, seed=16, tomb_frac=0.1)),
     "zero_large": (mixed, dict(n=60, kmax=8, vmax=50000, seed=17, zero_values=True)),
+    # 400-1200 B records: the shape where the hop and lane-walk pre-passes
+    # trade places; the zero-valued variant makes every value a
+    # run of header candidates.
+    "midlarge": (mixed, dict(n=4000, kmin=16, kmax=16, vmin=400, vmax=1200, seed=18)),
+    "midlarge_zero": (mixed, dict(n=3000, kmin=16, kmax=16, vmin=400, vmax=1200, seed=19,
+                                  zero_values=True)),
 }
 
 

@@ -206,6 +206,18 @@ def test_fake_headers_cfg2_size(engine):
     assert_same(engine, data)
 
 
+@pytest.mark.parametrize("zero", [False, True])
+def test_midlarge_bench_size(engine, zero):
+    """400-1200 B records at the size tools/decode_variants.py times (1 M
+    records, ~816 MB): the pre-pass picks hop or lane-walk per batch here
+    (DESIGN §3.1); zero-filled values add a header candidate every 16 bytes."""
+    arena, pairs = corpus.mixed(1_000_000, 16, 1200, seed=81, kmin=16, vmin=400,
+                                zero_values=zero)
+    data = oracle.encode(arena, pairs)[0]
+    del arena, pairs
+    assert_same(engine, data)
+
+
 @pytest.mark.parametrize("fake", [(10, 4, 96), (40, 0, 100), (2, 50, 50), (60, 1, 3)])
 def test_fake_headers_in_values(engine, fake):
     """Adversarial phase: every record carries a self-consistent fake header.
