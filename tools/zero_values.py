@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Decode time of small records whose values are zero bytes (the lane-walk
 guesses' worst case: every 16 bytes of a value read as a header candidate),
-checked against the oracle; A/B tool for the guess rules."""
+checked against the oracle; A/B tool for the guess rules.  `--midlarge`:
+400-1200 B zero values instead."""
 import json
 import os
 import sys
@@ -18,9 +19,14 @@ from oracle import oracle  # noqa: E402
 
 def main():
     rng = np.random.default_rng(9)
-    m = 3_000_000
-    kl = rng.integers(1, 24, m)
-    vl = rng.integers(0, 64, m)
+    if "--midlarge" in sys.argv:  # 16 B keys, 400-1200 B zero values (~816 MB)
+        m = 1_000_000
+        kl = np.full(m, 16)
+        vl = rng.integers(400, 1201, m)
+    else:
+        m = 3_000_000
+        kl = rng.integers(1, 24, m)
+        vl = rng.integers(0, 64, m)
     offs = np.concatenate([[0], np.cumsum(16 + kl + vl)])
     buf = np.zeros(int(offs[-1]), np.uint8)
     hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
@@ -48,7 +54,7 @@ def main():
     n = int(res[:8].cpu().numpy().view("<u8")[0])
     want = oracle.decode(buf)[0]
     ok = n == m and np.array_equal(spans[: n * 16].cpu().numpy().view(oracle.SPAN_DTYPE), want)
-    print(json.dumps({"workload": "small records, zero-byte values", "bytes": int(buf.size),
+    print(json.dumps({"workload": ("midlarge" if "--midlarge" in sys.argv else "small") + " records, zero-byte values", "bytes": int(buf.size),
                       "records": m, "ms": round(float(np.median(ts)), 4), "parity": bool(ok)}))
 
 
