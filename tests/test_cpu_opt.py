@@ -9,7 +9,8 @@ from tests import corpus
 
 
 @pytest.mark.parametrize("name", ["fixed_16_100", "mixed_small", "tiny", "empty_keys_tombs",
-                                  "zero_values", "mixed_4k", "large_values"])
+                                  "zero_values", "mixed_4k", "large_values", "midlarge",
+                                  "midlarge_zero"])
 @pytest.mark.parametrize("threads", [1, 3, 8])
 def test_mt_decode_matches_oracle(name, threads):
     _, _, data, _ = corpus.make(name)
