@@ -84,6 +84,9 @@ constexpr uint32_t NONE_REL = 0x3FFFFFu;          // "no record starts here"
 #define HG_LEADIN 1  // general batches guess their entry from a walked lead-in piece
 #endif
 constexpr uint32_t NO_GUESS = 0xFFFFFFFFu;
+#ifndef HG_SPLICE
+#define HG_SPLICE 1  // 0: a pre-pass batch entered off its predecessor's exit is decoded again (A/B)
+#endif
 #ifndef HG_LEAN
 #define HG_LEAN 1  // lean lane guesses for pieces entered at a known position (0: candidate
                    // evaluation + backing everywhere; 2: lean entry guesses too)
@@ -116,6 +119,7 @@ struct DecodeArgs {
     // pieces [0, first_bad) are resolved; decode_kernel writes their spans.
     struct SpecBatch* sbatch;
     const struct SpecPiece* spiece;
+    struct SpecPiece* spiece_rw;     // the same records (splice_repair rewrites its batch's)
     struct DecodeCtl* ctl;
     unsigned long long* gsum;    // records per group of SPEC_GROUP pre-pass batches
     unsigned long long* link;    // per adjacent pre-pass batch pair: arrivals | exit - x0
@@ -148,7 +152,7 @@ struct DecodeCtl {
     uint32_t bad_rev;             // max over unresolved pre-pass batches b of nspec - b
     uint32_t progress;            // general batches published (INCL / ERR): the look-back's
                                   // waits restart their budget whenever it moves
-    uint32_t reserved;
+    uint32_t repairs;             // pre-pass batches spliced onto their predecessor's exit
 };
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
@@ -1282,6 +1286,165 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
     return end;
 }
 
+__device__ __forceinline__ bool rec_ok(uint64_t q, uint64_t len, uint64_t kl, uint64_t vl) {
+    return kl <= ~0ull - vl && kl + vl <= len - q - 16 && !((kl >> 32) | (vl >> 32));
+}
+
+// Header at absolute q (q + 16 <= len) straight from HBM.
+__device__ __forceinline__ void hbm_header(const DecodeArgs& a, uint64_t q, uint64_t& kl,
+                                           uint64_t& vl) {
+    const uint64_t* p = reinterpret_cast<const uint64_t*>(a.sst + q);
+    kl = p[0];
+    vl = p[1];
+}
+
+// ---- splice repair of a pre-pass batch entered off its predecessor's exit -------
+// Pre-pass batch e (pieces [q0, q0 + n)) was resolved from a guessed entry x0
+// that is not the exit X of batch e - 1 (both resolved).  Exits are usually
+// right even then: a wrong guess follows a self-consistent path (inside a
+// zero-byte value every position reads as an empty record; a shifted header
+// read can decode as one long record) that joins the true path at some true
+// header, after which the two paths are the same walk.  So instead of
+// decoding the batch again, wave 0 walks the exact path from X through HBM
+// headers (one dependent 16-byte read per record) until it lands on a start of
+// the speculative path -- found by a two-pointer sweep over the speculative
+// starts, 64 per step (stride pieces arithmetically, walked pieces from their
+// scratch spans) -- or on the batch exit.  The exact records before that point
+// replace the speculative ones: they go in front of the speculative spans of
+// the piece holding the join point (its scratch slot shifted in place; a
+// stride piece is written out as spans), the pieces before it are emptied.
+// Only this general batch reads these pieces' records (the resolved prefix
+// stops before e), so rewriting them needs no cross-workgroup ordering.
+// Returns (wave 0) the batch's exact record count; ~0u if the path cannot be
+// read, does not join within SPLICE_MAX records, or the joined piece would
+// overflow its slot -- the look-back and the general engine then take the
+// batch as before.
+constexpr uint32_t SPLICE_MAX = 512;  // exact records before the join (LDS: 8 KiB)
+struct SpliceArgs {  // what splice_repair needs of DecodeArgs (by value: it is not inlined)
+    const uint8_t* sst;
+    uint64_t len, stop;
+    hg_span* scratch;
+    SpecPiece* spiece;
+    DecodeCtl* ctl;
+    uint32_t sbp, npieces;
+};
+__device__ __noinline__ uint32_t splice_repair(SpliceArgs a, uint4* ebuf, uint32_t e, uint64_t X,
+                                               uint64_t exit_e, uint32_t count_e) {
+    // ebuf: SPLICE_MAX exact spans in LDS; returns the new count, or ~0u
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t q0 = e * a.sbp;
+    const uint32_t n = min(a.sbp, a.npieces - q0);
+    const uint64_t bend = min((uint64_t)(q0 + n) * PIECE, a.stop);
+    // piece records: lane i holds piece i's
+    SpecPiece pr{};
+    if (lane < n) pr = a.spiece[q0 + lane];
+    const uint32_t pcnt = lane < n ? pr.count : 0u;
+    auto piece_pos = [&](uint32_t pi, uint32_t j) -> uint64_t {  // start of record j of piece pi
+        const uint64_t x = __shfl(pr.x, (int)pi, 64), R = __shfl(pr.R, (int)pi, 64);
+        const uint32_t kind = __shfl(pr.pad, (int)pi, 64);
+        if (kind == SP_HOP) return a.scratch[(size_t)(q0 + pi) * MAX_REC_PIECE + j].off;
+        return x + (uint64_t)j * R;
+    };
+    // speculative sweep: chunk = records [lo, lo + 64) of piece pi
+    uint32_t pi = 0, lo = 0;
+    auto next_nonempty = [&](uint32_t from) -> uint32_t {
+        const unsigned long long m = __ballot(lane >= from && lane < n && pcnt > 0);
+        return m ? (uint32_t)(__ffsll((long long)m) - 1) : n;
+    };
+    pi = next_nonempty(0);
+    uint64_t pos = ~0ull, cmax = ~0ull;
+    auto load_chunk = [&]() {
+        if (pi >= n) {
+            pos = ~0ull;
+            cmax = ~0ull;
+            return;
+        }
+        const uint32_t c = __shfl(pcnt, (int)pi, 64);
+        pos = lo + lane < c ? piece_pos(pi, lo + lane) : ~0ull;
+        const uint32_t last = min(lo + 63u, c - 1u);
+        cmax = __shfl(pos, (int)(last - lo), 64);
+    };
+    load_chunk();
+    uint64_t p = X;
+    uint32_t E = 0, jpi = n, jlo = 0;  // join: piece jpi, record jlo (jpi == n: at the exit)
+    for (;;) {
+        if (p >= bend) {
+            if (p != exit_e) return ~0u;
+            jpi = n;
+            break;
+        }
+        while (pi < n && cmax < p) {  // every start in the chunk is before p
+            lo += 64;
+            if (lo >= __shfl(pcnt, (int)pi, 64)) {
+                pi = next_nonempty(pi + 1);
+                lo = 0;
+            }
+            load_chunk();
+        }
+        const unsigned long long m = __ballot(pos == p);
+        if (m) {
+            jpi = pi;
+            jlo = lo + (uint32_t)(__ffsll((long long)m) - 1);
+            break;
+        }
+        if (E == SPLICE_MAX || p + 16 > a.len) return ~0u;
+        uint64_t kl = 0, vl = 0;
+        if (lane == 0) {
+            const uint64_t* hp = reinterpret_cast<const uint64_t*>(a.sst + p);
+            kl = hp[0];
+            vl = hp[1];
+        }
+        kl = __shfl(kl, 0, 64);
+        vl = __shfl(vl, 0, 64);
+        if (kl > ~0ull - vl || kl + vl > a.len - p - 16 || ((kl >> 32) | (vl >> 32))) return ~0u;
+        if (lane == 0) ebuf[E] = make_uint4((uint32_t)p, (uint32_t)(p >> 32), (uint32_t)kl, (uint32_t)vl);
+        ++E;
+        p += 16 + kl + vl;
+    }
+    // the join piece: exact spans, then its speculative spans from jlo on
+    const uint32_t tp = jpi < n ? jpi : n - 1;           // piece that takes the exact spans
+    const uint32_t tc = __shfl(pcnt, (int)tp, 64);
+    const uint32_t keep0 = jpi < n ? jlo : tc;           // its speculative spans kept: [keep0, tc)
+    const uint32_t keep = tc - keep0;
+    if (E + keep > MAX_REC_PIECE) return ~0u;
+    uint32_t before = 0;                                 // speculative records dropped
+    {
+        const uint32_t c = lane < tp ? pcnt : 0u;
+        before = wave_sum<uint32_t>(c) + keep0;
+    }
+    hg_span* slot = a.scratch + (size_t)(q0 + tp) * MAX_REC_PIECE;
+    const uint32_t tkind = __shfl(pr.pad, (int)tp, 64);
+    if (keep && tkind != SP_HOP) {  // a stride piece: write its kept records out as spans
+        const uint64_t x = __shfl(pr.x, (int)tp, 64), R = __shfl(pr.R, (int)tp, 64);
+        const uint32_t kl = __shfl(pr.kl, (int)tp, 64), vl = __shfl(pr.vl, (int)tp, 64);
+        for (uint32_t j = lane; j < keep; j += 64)
+            write_span(slot, E + j, x + (uint64_t)(keep0 + j) * R, kl, vl);
+    } else if (keep && E < keep0) {  // shift down, ascending (no chunk reads what an earlier one wrote)
+        for (uint32_t j0 = 0; j0 < keep; j0 += 64) {
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (j0 + lane < keep) v = *reinterpret_cast<const uint4*>(slot + keep0 + j0 + lane);
+            if (j0 + lane < keep) *reinterpret_cast<uint4*>(slot + E + j0 + lane) = v;
+        }
+    } else if (keep && E > keep0) {  // shift up, descending
+        for (uint32_t j1 = keep; j1 > 0;) {
+            const uint32_t j0 = j1 > 64 ? j1 - 64 : 0;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (j0 + lane < j1) v = *reinterpret_cast<const uint4*>(slot + keep0 + j0 + lane);
+            if (j0 + lane < j1) *reinterpret_cast<uint4*>(slot + E + j0 + lane) = v;
+            j1 = j0;
+        }
+    }
+    for (uint32_t j = lane; j < E; j += 64) *reinterpret_cast<uint4*>(slot + j) = ebuf[j];
+    if (lane <= tp) {  // pieces before the join piece hold nothing now
+        SpecPiece o = pr;
+        o.count = lane == tp ? E + keep : 0u;
+        o.pad = SP_HOP;
+        a.spiece[q0 + lane] = o;
+    }
+    if (lane == 0) atomicAdd(&a.ctl->repairs, 1u);
+    return count_e - before + E;
+}
+
 template <bool DIAG>
 __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
     __shared__ DecodeSmem s;
@@ -1353,19 +1516,41 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
     {
         const uint32_t e0 = b * a.q, e1 = min((b + 1) * a.q, a.nspec);
         if (tid < 64) {
+            // Each pre-pass batch must be resolved and entered at its
+            // predecessor's exit; one entered elsewhere is spliced onto that
+            // exit (splice_repair).  The first one's predecessor belongs to the
+            // previous general batch: its exit is only a better guess of our
+            // entry (the look-back below checks it).
             bool good = true;
-            uint64_t cnt = 0;
-            if (tid < e1 - e0) {
-                const SpecBatch sbe = a.sbatch[e0 + tid];
-                good = sbe.ok && (tid == 0 || sbe.x0 == a.sbatch[e0 + tid - 1].exit);
-                cnt = sbe.count;
+            uint64_t cnt = 0, P0 = a.sbatch[e0].x0;
+            for (uint32_t e = e0; e < e1 && good; ++e) {
+                const SpecBatch sbe = a.sbatch[e];
+                uint32_t c = sbe.count;
+                good = sbe.ok != 0;
+                if (good && e > 0) {
+                    const SpecBatch sbp = a.sbatch[e - 1];
+                    if (sbe.x0 != sbp.exit && (sbp.ok || e > e0)) {
+                        const SpliceArgs sa{a.sst, a.len, a.stop, a.scratch, a.spiece_rw, a.ctl, a.sbp,
+                                            a.npieces};
+                        const uint32_t cr =
+                            HG_SPLICE && sbp.ok
+                                ? splice_repair(sa, reinterpret_cast<uint4*>(s.data64), e, sbp.exit,
+                                                sbe.exit, c)
+                                : ~0u;
+                        if (cr != ~0u) {
+                            c = cr;
+                            if (e == e0) P0 = sbp.exit;
+                        } else if (e > e0) {
+                            good = false;
+                        }
+                    }
+                }
+                cnt += c;
             }
-            good = __all(good);
-            cnt = wave_sum<uint64_t>(cnt);
             if (tid == 0) {
                 s.pred_ok = good;
                 s.gk = cnt;
-                s.xk = a.sbatch[e0].x0;
+                s.xk = P0;
                 s.exitk = a.sbatch[e1 - 1].exit;
             }
         }
@@ -1728,18 +1913,6 @@ struct SpecSmem {
     uint64_t lw_last;
 };
 
-__device__ __forceinline__ bool rec_ok(uint64_t q, uint64_t len, uint64_t kl, uint64_t vl) {
-    return kl <= ~0ull - vl && kl + vl <= len - q - 16 && !((kl >> 32) | (vl >> 32));
-}
-
-// Header at absolute q (q + 16 <= len) straight from HBM.
-__device__ __forceinline__ void hbm_header(const DecodeArgs& a, uint64_t q, uint64_t& kl,
-                                           uint64_t& vl) {
-    const uint64_t* p = reinterpret_cast<const uint64_t*>(a.sst + q);
-    kl = p[0];
-    vl = p[1];
-}
-
 // Span of the HOP_CHECK records after the (valid) record at p, or 0 if one
 // of them cannot be read.  Reaching the end of the file exactly passes.
 __device__ uint64_t hop_check(const DecodeArgs& a, uint64_t p, uint64_t kl, uint64_t vl) {
@@ -1787,7 +1960,13 @@ __device__ void hop_walk(const DecodeArgs& a, uint64_t x, uint64_t end, hg_span*
 }
 
 // Phase A for segment starting at S (absolute), by one wave, window staged in
-// w (HOP_WIN + 16 bytes).  Returns (guess, span) in every lane.
+// w (HOP_WIN + 16 bytes).  Returns (guess, span) in every lane.  Each lane
+// tries the candidates of its 64 bytes that END a run of candidates first (a
+// genuine header with short lengths also passes the filter 1-3 bytes to its
+// left; a record read from such a shifted position can still chain into a
+// true header far ahead and pass the check, which made a batch's entry
+// wrong), then the others; all-zero headers are skipped (inside zero-byte
+// values every position reads as an empty record and chains on).
 __device__ void hop_guess(const DecodeArgs& a, const uint8_t* w, uint64_t S, uint64_t& guess,
                           uint64_t& span) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -1797,19 +1976,24 @@ __device__ void hop_guess(const DecodeArgs& a, const uint8_t* w, uint64_t S, uin
     const uint32_t plim = plim64 < 0xFFFFFFFFull ? (uint32_t)plim64 : 0xFFFFFFFFu;
     const uint32_t clen = rem < HOP_WIN ? (uint32_t)rem : HOP_WIN;
     unsigned long long best = ~0ull;  // (position << 40) | span
+    uint64_t cm = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; ++j)
+        cm |= (uint64_t)filter_bits(w, lane * 4 + j, a.hz, clen, plim, any_valid) << (16 * j);
+    const uint64_t nb = filter_bits(w, lane * 4 + 4, a.hz, clen, plim, any_valid) & 1u;
+    const uint64_t runend = cm & ~((cm >> 1) | (nb << 63));
+    uint64_t c = runend;
     uint32_t tries = 0;
 #pragma unroll 1
-    for (uint32_t j = 0; j < 4 && best == ~0ull && tries < HOP_TRIES; ++j) {
-        const uint32_t gi = lane * 4 + j;
-        uint32_t c = filter_bits(w, gi, a.hz, clen, plim, any_valid);
+    for (uint32_t pass = 0; pass < 2 && best == ~0ull; ++pass) {
+        if (pass) c = cm & ~runend;
         while (c && tries < HOP_TRIES) {
-            const uint32_t bpos = __ffs(c) - 1;
+            const uint32_t p = lane * 64 + (uint32_t)(__ffsll((long long)c) - 1);
             c &= c - 1;
             ++tries;
-            const uint32_t p = gi * 16 + bpos;
             uint64_t kl, vl;
             lds_header(w, p, kl, vl);
-            if (!rec_ok(S + p, a.len, kl, vl)) continue;
+            if ((kl | vl) == 0 || !rec_ok(S + p, a.len, kl, vl)) continue;
             const uint64_t d = hop_check(a, S + p, kl, vl);
             if (d) {
                 best = ((unsigned long long)p << 40) | (d < V40 ? d : V40);
@@ -1897,7 +2081,7 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
     }
     __syncthreads();
     if (s.hg[0] == NO_HOP) {  // no entry for the batch: the general engine takes it
-        s.hcode = SB_HOP_DEAD;
+        s.hcode = SB_HOP_DEAD | (1u << 8);
         return false;
     }
     // B: one lane per segment walks it into scratch
@@ -1914,12 +2098,13 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
     __syncthreads();
     // C: stitch in segment order (re-walk a segment entered off its guess)
     if (tid == 0) {
-        uint32_t ok = s.hdead[0] == 0, redo = 0;
+        uint32_t ok = s.hdead[0] == 0, redo = 0, why = ok ? 0u : 3u;
         uint64_t x = s.hexit[0], t = s.hcnt[0];
         for (uint32_t k = 1; k < nseg && ok; ++k) {
             if (s.hg[k] != x) {
                 if (++redo > HOP_MAX_REDO) {
                     ok = 0;
+                    why = 2;
                     break;
                 }
                 const uint64_t S1 = (uint64_t)(p0 + (k + 1) * HOP_SEG_PIECES) * PIECE;
@@ -1933,13 +2118,16 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
                 s.hdead[k] = dd;
             }
             ok = s.hdead[k] == 0;
+            if (!ok) why = 3;
             x = s.hexit[k];
             t += s.hcnt[k];
         }
         s.hok = ok;
         s.hx = x;
         s.ht = t;
-        s.hcode = ok ? SB_HOP : SB_HOP_DEAD;
+        // SpecBatch.pad bits 8..15: why a hop batch failed (1 no entry guess, 2 too
+        // many re-walks, 3 a walk hit an unreadable record or HOP_MAX_RECS)
+        s.hcode = ok ? SB_HOP : (SB_HOP_DEAD | (why << 8));
     }
     __syncthreads();
     if (!s.hok) return false;
@@ -2003,8 +2191,12 @@ constexpr uint32_t LW_CPP = PIECE / LW_CHUNK;   // chunks per piece
 static_assert(LW_ZM_WORDS == LW_CHUNK / 16 + 8, "lane-walk mask rows");
 static_assert(4 * LW_CBUF <= PIECE + 512, "two waves' chunk buffers per piece buffer");
 constexpr uint32_t LW_WROUNDS = 64;             // relaxation rounds before lane 0 walks it
+constexpr uint32_t LW_ENTRY_RETRIES = 4;        // guessed entries tried after one whose path dies
 #ifndef HG_LW_LOOKAHEAD
 #define HG_LW_LOOKAHEAD 0  // 1: a guess must also read a valid next header (small/medium 2.5 % slower; zero-byte values no better)
+#endif
+#ifndef HG_LW_ZERO
+#define HG_LW_ZERO 1  // 0: lane guesses may take all-zero headers (A/B builds; see lw_guess_nz)
 #endif
 #ifndef HG_LW_TRIES
 #define HG_LW_TRIES 1  // 2: small and medium 1.3 % slower (the second try rarely pays for its reads)
@@ -2139,11 +2331,63 @@ __device__ __forceinline__ void lw_masks(const uint16_t* zm, uint32_t seg0, uint
     cm0 = c;
 }
 
+// lw_guess when the lane's guess reads as an all-zero header followed by 16
+// more zero bytes (a genuine empty record -- InternalPair::default, 16 zero
+// bytes -- is followed by a header, not by zeros): the lane is inside a run
+// of zero bytes (a zero-byte value), where every
+// position reads as an empty 16-byte record and a walk chains on through the
+// zeros -- a guess there is self-consistent but usually off the true path, so
+// the chunk's entry and the lanes after it would follow it.  The candidates
+// at which 16 zero bytes start are dropped (doubling over the zero-byte
+// masks), run ends recomputed, and up to LW_ZTRIES candidates tried with a
+// look-ahead (a shifted read of a header next to a zero run decodes as a
+// short record that lands inside a key).  Only lanes that meet a zero header
+// pay for this.
+constexpr uint32_t LW_ZTRIES = 4;
+constexpr uint32_t LW_ZERO_HDR = 1u << 30;  // lw_guess: the guess reads as an all-zero header
+__device__ __noinline__ uint32_t lw_guess_nz(const uint8_t* data, const uint16_t* zm,
+                                             uint32_t seg0, uint32_t clen, uint64_t rem,
+                                             uint64_t cm0, uint64_t nextbit) {
+    const uint32_t gi = seg0 / 16;
+    uint64_t alo = *reinterpret_cast<const uint64_t*>(&zm[gi]);
+    uint32_t ahi = zm[gi + 4] & 0xFFFFu;
+#pragma unroll
+    for (uint32_t pw = 1; pw < 16; pw *= 2) {  // bit j <=> bytes j .. j+15 are zero
+        alo &= (alo >> pw) | ((uint64_t)ahi << (64 - pw));
+        ahi &= ahi >> pw;
+    }
+    const uint64_t cm = cm0 & ~alo;
+    const uint64_t nb = nextbit & ~(uint64_t)(ahi & 1u);
+    const uint64_t runend = cm & ~((cm >> 1) | (nb << 63));
+    uint64_t c = runend;
+    uint32_t tries = 0;
+    for (uint32_t pass = 0; pass < 2; ++pass) {
+        if (pass) c = cm & ~runend;
+        while (c && tries++ < LW_ZTRIES) {
+            const uint32_t p = seg0 + (uint32_t)(__ffsll((long long)c) - 1);
+            c &= c - 1;
+            uint32_t k0, k1, v0, v1;
+            lds_header32(data, p, k0, k1, v0, v1);
+            const uint64_t body = (uint64_t)k0 + v0;
+            if ((k1 | v1) || body == 0 || body >= HG_FAR_CAND || body > rem - p - 16) continue;
+            const uint64_t nx = (uint64_t)p + 16 + body;
+            if (nx < clen) {
+                if (nx + 16 > rem) continue;
+                lds_header32(data, (uint32_t)nx, k0, k1, v0, v1);
+                if ((k1 | v1) || (uint64_t)k0 + v0 > rem - nx - 16) continue;
+            }
+            return p;
+        }
+    }
+    return NO_GUESS;
+}
+
 // This lane's guess in [seg0, segend) (piece-relative) or NO_GUESS; cm0 / the
 // next lane's first candidate bit as in lean_prepare.
-__device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, uint32_t seg0, uint32_t segend,
-                                             uint32_t clen, uint64_t rem, uint32_t hz,
-                                             uint64_t cm0, uint64_t nextbit) {
+__device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, const uint16_t* zm,
+                                             uint32_t seg0, uint32_t segend, uint32_t clen,
+                                             uint64_t rem, uint32_t hz, uint64_t cm0,
+                                             uint64_t nextbit) {
     const uint64_t runend = cm0 & ~((cm0 >> 1) | (nextbit << 63));
     uint64_t cm = runend;
     uint32_t tries = 0;  // a lane left without a guess is entered by the relaxation
@@ -2162,6 +2406,10 @@ __device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, uint32_t seg0,
                 if (nx + 16 > rem) continue;
                 lds_header32(data, (uint32_t)nx, k0, k1, v0, v1);
                 if ((k1 | v1) || (uint64_t)k0 + v0 > rem - nx - 16) continue;
+            }
+            if (HG_LW_ZERO && body == 0) {  // (0, 0): inside a run of >= 32 zero bytes?
+                lds_header32(data, p + 16, k0, k1, v0, v1);  // (in the chunk buffer's halo)
+                if ((k0 | k1 | v0 | v1) == 0) return p | LW_ZERO_HDR;  // see lw_guess_nz
             }
             return p;
         }
@@ -2282,7 +2530,9 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     w.cnt = 0;
     w.p01 = w.p23 = 0;
     if (!guess && lane == je) g = (uint32_t)(X - cb);
-    else if (in_chunk) g = lw_guess(data, seg0, segend, clen, rem, a.hz, cm0, nb);
+    else if (in_chunk) g = lw_guess(data, zm, seg0, segend, clen, rem, a.hz, cm0, nb);
+    if (HG_LW_ZERO && g != NO_GUESS && (g & LW_ZERO_HDR))  // rare: a lane inside zero bytes
+        g = lw_guess_nz(data, zm, seg0, clen, rem, cm0, nb);
     if (in_chunk && g != NO_GUESS) lw_walk(data, lim, g, segend, w);
     LW_STAMP(1);
     // chain marks: which lane guesses some lane's walk exits on
@@ -2301,9 +2551,10 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     lw_wave_sync();
     const bool chain = tg[lane] != 0;
     uint32_t jl = je, xw = 0;
+    unsigned long long vm = 0;
     if (guess) {
         const unsigned long long lm = __ballot(valid0 && links);
-        const unsigned long long vm = __ballot(valid0);
+        vm = __ballot(valid0);
         if (!vm) return false;  // nothing that reads as a record: no entry
         jl = (uint32_t)__ffsll((long long)(lm ? lm : vm)) - 1;
         xw = __shfl(g, (int)jl, 64);
@@ -2349,8 +2600,25 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     }
     LW_STAMP(3);
     const bool walking = act && st == 0;
-    if (!conv || __ballot(act && (st == 2 || (st == 0 && w.dead))))
-        return lw_chunk_serial(a, data, cb, clen, X, out, count, exit, nstores);
+    if (!conv || __ballot(act && (st == 2 || (st == 0 && w.dead)))) {
+        const bool sok = lw_chunk_serial(a, data, cb, clen, X, out, count, exit, nstores);
+        if (sok || !guess) return sok;
+        // A guessed entry whose path cannot be read (e.g. a shifted read next to
+        // a run of zero bytes that still looked like a record): walk from the
+        // next lanes' original guesses (sg) in order until one path reaches
+        // the chunk end.  Guess mode writes no spans (lead-in chunks).
+        unsigned long long cand = vm & ~((2ull << jl) - 1ull);
+        for (uint32_t t = 0; t < LW_ENTRY_RETRIES && cand; ++t) {
+            const uint32_t l2 = (uint32_t)(__ffsll((long long)cand) - 1);
+            cand &= cand - 1;
+            const uint64_t X2 = cb + sg[l2];
+            if (lw_chunk_serial(a, data, cb, clen, X2, out, count, exit, nstores)) {
+                entry = X2;
+                return true;
+            }
+        }
+        return false;
+    }
     const uint32_t c = walking ? w.cnt : 0u;
     const uint32_t incl = dpp_sum_incl(c);
     count = __builtin_amdgcn_readlane((int)incl, 63);
@@ -2376,14 +2644,16 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
 __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint8_t* bufs,
                                           uint16_t* zm, uint32_t* sg, uint8_t* tg, uint32_t pb,
                                           uint32_t pe, uint64_t X, SpecPiece* sp, uint64_t& entry,
-                                          uint64_t& exit, uint64_t& total) {
+                                          uint64_t& exit, uint64_t& total, uint32_t nlead) {
     const uint32_t lane = threadIdx.x & 63u;
     // piece records of the quarter, kept in LDS until the stream ends so the
     // chunk loop issues no vector memory operations besides its span stores
     uint64_t* const px = s.lw_px[threadIdx.x >> 6];
     uint32_t* const pc = s.lw_pc[threadIdx.x >> 6];
     const bool lead = X == LW_GUESS;
-    const uint64_t k0 = (uint64_t)pb * LW_CPP - (lead ? 1u : 0u);
+    // nlead lead-in chunks: the first entered at a guess, the others exactly
+    const uint64_t nl = lead ? min((uint64_t)nlead, (uint64_t)pb * LW_CPP) : 0u;
+    const uint64_t k0 = (uint64_t)pb * LW_CPP - nl;
     const uint64_t k1 = (uint64_t)pe * LW_CPP;
     lw_fetch_chunk(a, k0 * LW_CHUNK, bufs);
     lw_wait_vm(0);
@@ -2400,7 +2670,7 @@ __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint
         LW_STAMP(0);
         const uint64_t cb = k * LW_CHUNK;
         const uint32_t clen = a.stop > cb ? (uint32_t)min((uint64_t)LW_CHUNK, a.stop - cb) : 0u;
-        const bool is_lead = lead && k == k0;
+        const bool is_lead = k < k0 + nl;
         const uint64_t piece = k / LW_CPP;
         hg_span* out = is_lead ? nullptr : a.scratch + (size_t)piece * MAX_REC_PIECE + pcount;
         uint64_t en = 0, ex = 0;
@@ -2465,8 +2735,9 @@ __device__ __forceinline__ void spec_stage(SpecSmem& s, const uint4 (&v)[GPT], u
 // caller are not used: every chunk is fetched again, L2-warm).
 __device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const DecodeArgs& a,
                                          uint32_t p0, uint32_t np, SpecPiece* sp, uint64_t& X0,
-                                         uint64_t& X, uint64_t& total) {
+                                         uint64_t& X, uint64_t& total, uint32_t& why) {
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    why = 0;
     uint8_t* const bufs = wid < 2 ? reinterpret_cast<uint8_t*>(s.data64) + wid * 2 * LW_CBUF
                                   : reinterpret_cast<uint8_t*>(alt) + (wid - 2) * 2 * LW_CBUF;
     uint16_t* const zm = s.lw_zm[wid];
@@ -2483,11 +2754,12 @@ __device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const Decod
     bool exact = xin != LW_GUESS;
     uint64_t en = 0, ex = 0, tot = 0;
     bool okw = true, run = pb < pe;
-    bool ok = true;
+    bool ok = true, long_lead = false;
+    uint32_t nlead = 1;
     uint64_t x = 0;
     uint32_t flast = 0;
     for (uint32_t att = 0;; ++att) {  // one call site of lw_stream (first pass and re-streams)
-        if (run) okw = lw_stream(s, a, bufs, zm, sg, tg, pb, pe, xin, sp, en, ex, tot);
+        if (run) okw = lw_stream(s, a, bufs, zm, sg, tg, pb, pe, xin, sp, en, ex, tot, nlead);
         run = false;
         const uint32_t f = att & 1u;
         flast = f;
@@ -2506,20 +2778,34 @@ __device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const Decod
             if (!(fl & 4u)) continue;  // no pieces
             const bool entered = v == 0 || s.lw_wx[f][v] == x;
             if ((fl & 1u) || !entered) {  // unresolved, or entered off the exact exit
-                if (v == 0 || (fl & 2u)) ok = false;  // exact entry and still unresolved
-                else fix = v;
+                if (v == 0 && !(fl & 2u) && !long_lead) {
+                    // the first quarter's guessed entry led nowhere (a path that
+                    // survived the 4 KiB lead-in inside zero-byte values): stream
+                    // it again behind a whole piece of lead-in chunks
+                    fix = 0;
+                    long_lead = true;
+                } else if (v == 0 || (fl & 2u)) {  // exact entry and still unresolved
+                    ok = false;
+                    why = (fl & 2u) ? 2u : 1u;
+                } else {
+                    fix = v;
+                }
                 break;
             }
             x = s.lw_wexit[f][v];
             total += s.lw_wcnt[f][v];
         }
         if (!ok || fix == NW || att == NW) {
-            if (fix != NW) ok = false;
+            if (fix != NW) {
+                ok = false;
+                why = 3;
+            }
             break;
         }
         if (wid == fix) {  // stream the quarter again from the exact entry
-            exact = true;
-            xin = x;
+            exact = fix != 0 || (p0 == 0);
+            xin = fix == 0 ? (p0 == 0 ? a.entry : LW_GUESS) : x;
+            nlead = fix == 0 ? LW_CPP : 1u;
             run = true;
         }
         x = 0;
@@ -2684,8 +2970,11 @@ __device__ void lw_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint3
     const uint32_t p0 = b * a.sbp;
     const uint32_t np = min(a.sbp, a.npieces - p0);
     uint64_t X0 = 0, X = 0, total = 0;
-    const bool ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total);
-    if (threadIdx.x == 0) spec_publish(a, sb, b, X0, X, total, ok, ok ? SB_LW : SB_LW_DEAD);
+    uint32_t why = 0;
+    const bool ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total, why);
+    // SpecBatch.pad bits 8..15 of a failed batch: 1 the first quarter's guessed
+    // entry, 2 a quarter entered exactly, 3 too many re-streams
+    if (threadIdx.x == 0) spec_publish(a, sb, b, X0, X, total, ok, ok ? SB_LW : (SB_LW_DEAD | (why << 8)));
 }
 
 __global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
@@ -2911,6 +3200,7 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     a.sdiag = d_diag ? d_diag + (size_t)l.nbatches * DIAG_WORDS : nullptr;
     a.sbatch = reinterpret_cast<SpecBatch*>(ws + l.sbatch_off);
     a.spiece = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
+    a.spiece_rw = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
     a.q = a.bp / a.sbp;
     zero_bytes = (l.status_off + 2 * (uint64_t)a.nbatches * 8 + 7) & ~7ull;

@@ -1,16 +1,21 @@
 // hg_lookup.hip — batched point lookups on a decoded SSTable (gfx950).
 //
 // Replaces SSTable::get (reference src/sstable/table.rs:54-70): Index::get
-// (src/sstable/index.rs:72-78) picks a block, the block is read and decoded,
-// and binary_search_by_key finds the key.  For the strictly increasing tables
-// horreum writes that is the record whose key equals the query, if any --
-// which a batch of queries finds on the device in one launch:
+// (src/sstable/index.rs:72-78) binary-searches the block first keys, the
+// block is read and decoded, and binary_search_by_key finds the key in it.
+// Both searches are Rust's slice::binary_search_by (std 1.52-1.81: probe
+// mid = left + (right - left) / 2, return the first probe that compares
+// Equal), so on tables with duplicate or unordered keys (legal,
+// table.rs:93-108) the record found is the one the reference finds, not
+// merely some record with the key.  A batch of queries runs on the device in
+// one launch:
 //   keyindex_kernel: one 32-byte entry per record (16-byte big-endian key
 //     prefix, key length, record index), built once per decoded table;
-//   lookup_kernel: one thread per query, lower-bound binary search over the
-//     entries (one 32-byte load per probe; the top levels are shared by all
-//     queries and stay in L2), keys that agree on 16 bytes and are both
-//     longer finish the compare on the table bytes.
+//   lookup_kernel: one thread per query; the block search probes entries
+//     b * stride (block first keys), the in-block search the block's entries
+//     (one 32-byte load per probe; the top levels are shared by all queries
+//     and stay in L2); keys that agree on 16 bytes and are both longer finish
+//     the compare on the table bytes.
 #include "hg_device.hpp"
 
 namespace hgl {
@@ -73,33 +78,59 @@ __device__ __forceinline__ int cmp_entry(const uint8_t* table, const hg_span* sp
     return e.klen < ql ? -1 : e.klen > ql ? 1 : 0;
 }
 
+// Rust's binary_search_by over entries base + i * step, i in [0, size):
+// Ok(i) -> (true, i); Err(i) -> (false, i).
+__device__ __forceinline__ bool rust_search(const uint8_t* table, const hg_span* spans,
+                                            const KEnt* ents, uint64_t base, uint64_t step,
+                                            uint64_t size, const uint8_t* q, uint64_t qp0,
+                                            uint64_t qp1, uint32_t ql, uint64_t& pos) {
+    uint64_t left = 0, right = size;
+    while (left < right) {
+        const uint64_t mid = left + (right - left) / 2;
+        const int c = cmp_entry(table, spans, ents[base + mid * step], q, qp0, qp1, ql);
+        if (c == 0) {
+            pos = mid;
+            return true;
+        }
+        if (c < 0) left = mid + 1;
+        else right = mid;
+    }
+    pos = left;
+    return false;
+}
+
 __global__ __launch_bounds__(THREADS) void lookup_kernel(const uint8_t* table, const hg_span* spans,
                                                          const KEnt* ents, uint64_t n,
-                                                         const uint8_t* keys, const hg_key* queries,
-                                                         uint64_t nq, hg_lookup_result* out) {
+                                                         uint64_t stride, const uint8_t* keys,
+                                                         const hg_key* queries, uint64_t nq,
+                                                         hg_lookup_result* out) {
     const uint64_t i = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
     if (i >= nq) return;
     const hg_key qk = queries[i];
     const uint8_t* q = keys + qk.off;
     uint64_t qp0, qp1;
     prefix16(q, qk.len, qk.len, qp0, qp1);
-    uint64_t lo = 0, hi = n;  // first entry >= query
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (cmp_entry(table, spans, ents[mid], q, qp0, qp1, qk.len) < 0) lo = mid + 1;
-        else hi = mid;
-    }
     hg_lookup_result r;
     r.rec = ~0ull;
     r.val_off = 0;
     r.vlen = 0;
     r.found = 0;
-    if (lo < n && cmp_entry(table, spans, ents[lo], q, qp0, qp1, qk.len) == 0) {
-        const hg_span s = spans[lo];
-        r.rec = lo;
-        r.val_off = s.off + 16 + s.klen;
-        r.vlen = s.vlen;
-        r.found = 1;
+    // Index::get (index.rs:72-78): Ok(b) -> block b; Err(b) -> block b - 1, none if b == 0
+    const uint64_t nb = n ? (n - 1) / stride + 1 : 0;
+    uint64_t b = 0;
+    bool hit = rust_search(table, spans, ents, 0, stride, nb, q, qp0, qp1, qk.len, b);
+    if (hit || b > 0) {
+        if (!hit) --b;
+        const uint64_t r0 = b * stride;
+        const uint64_t cnt = n - r0 < stride ? n - r0 : stride;
+        uint64_t j = 0;
+        if (rust_search(table, spans, ents, r0, 1, cnt, q, qp0, qp1, qk.len, j)) {  // table.rs:65-68
+            const hg_span s = spans[r0 + j];
+            r.rec = r0 + j;
+            r.val_off = s.off + 16 + s.klen;
+            r.vlen = s.vlen;
+            r.found = 1;
+        }
     }
     out[i] = r;
 }
@@ -118,14 +149,17 @@ extern "C" int hgk_keyindex_launch(const uint8_t* d_table, uint64_t len, const h
     return HG_LAUNCH_STATUS();
 }
 
+// block_stride 0: the whole table is one block.
 extern "C" int hgk_lookup_launch(const uint8_t* d_table, const hg_span* d_spans,
-                                 const void* d_index, uint64_t n, const uint8_t* d_keys,
-                                 const hg_key* d_queries, uint64_t nq,
+                                 const void* d_index, uint64_t n, uint32_t block_stride,
+                                 const uint8_t* d_keys, const hg_key* d_queries, uint64_t nq,
                                  hg_lookup_result* d_results, hipStream_t stream) {
     using namespace hgl;
     if (nq == 0) return HG_OK;
+    const uint64_t stride = block_stride ? block_stride : (n ? n : 1);
     hipLaunchKernelGGL(lookup_kernel, dim3((uint32_t)((nq + THREADS - 1) / THREADS)),
                        dim3(THREADS), 0, stream, d_table, d_spans,
-                       static_cast<const KEnt*>(d_index), n, d_keys, d_queries, nq, d_results);
+                       static_cast<const KEnt*>(d_index), n, stride, d_keys, d_queries, nq,
+                       d_results);
     return HG_LAUNCH_STATUS();
 }

@@ -107,6 +107,40 @@ int decode_share(hg_ctx* c, Share& sh, const uint8_t* const* h_tables, const uin
     return sync_d2h(c, sh.res.data(), dr, k * sizeof(hg_decode_result));
 }
 
+// Device bytes one decode_share of these tables takes: the arena (256-byte
+// aligned starts) and the spans (capacity len / 16 each).
+uint64_t share_bytes(uint64_t len) { return ((len + 255) & ~255ull) + (len / 16) * sizeof(hg_span); }
+
+// Byte budget of one batched decode of many tables (SSTableManager's cold open
+// of a whole directory): HG_DECODE_GROUP_BYTES, else 40 % of the device memory
+// free now.  A share larger than this is decoded in groups of tables, one
+// group after another; a table larger than the budget is a group of its own.
+uint64_t group_budget() {
+    if (const char* e = getenv("HG_DECODE_GROUP_BYTES")) {
+        const long long v = atoll(e);
+        if (v > 0) return (uint64_t)v;
+    }
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr == 0) return 4ull << 30;
+    return (uint64_t)(fr / 10 * 4);
+}
+
+std::vector<std::vector<uint32_t>> groups_of(const std::vector<uint32_t>& ids, const uint64_t* lens,
+                                              uint64_t budget) {
+    std::vector<std::vector<uint32_t>> g;
+    uint64_t acc = 0;
+    for (uint32_t t : ids) {
+        const uint64_t b = share_bytes(lens[t]);
+        if (g.empty() || (acc + b > budget && !g.back().empty())) {
+            g.emplace_back();
+            acc = 0;
+        }
+        g.back().push_back(t);
+        acc += b;
+    }
+    return g;
+}
+
 std::vector<Share> round_robin(uint32_t nctx, uint32_t ntables) {
     std::vector<Share> sh(nctx);
     for (uint32_t t = 0; t < ntables; ++t) sh[t % nctx].ids.push_back(t);
@@ -205,23 +239,28 @@ int hg_multi_decode_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
     std::vector<Share> sh = round_robin(nctx, ntables);
     return fan_out(nctx, [&](uint32_t ci) {
         hg_ctx* c = ctxs[ci];
-        Share& s = sh[ci];
-        int r = decode_share(c, s, h_tables, lens);
-        if (r != HG_OK) return r;
-        const hg_span* spans = static_cast<const hg_span*>(c->mspans.p);
-        for (size_t j = 0; j < s.ids.size(); ++j) {
-            const uint32_t t = s.ids[j];
-            const hg_decode_result& res = s.res[j];
-            n_out[t] = res.n_records;
-            if (errs) {
-                errs[t].kind = res.kind;
-                errs[t].reserved = 0;
-                errs[t].offset = res.kind != HG_OK ? res.err_offset : 0;
+        if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
+        // groups under the byte budget (a directory larger than HBM opens too)
+        for (const std::vector<uint32_t>& grp : groups_of(sh[ci].ids, lens, group_budget())) {
+            Share s;
+            s.ids = grp;
+            int r = decode_share(c, s, h_tables, lens);
+            if (r != HG_OK) return r;
+            const hg_span* spans = static_cast<const hg_span*>(c->mspans.p);
+            for (size_t j = 0; j < s.ids.size(); ++j) {
+                const uint32_t t = s.ids[j];
+                const hg_decode_result& res = s.res[j];
+                n_out[t] = res.n_records;
+                if (errs) {
+                    errs[t].kind = res.kind;
+                    errs[t].reserved = 0;
+                    errs[t].offset = res.kind != HG_OK ? res.err_offset : 0;
+                }
+                const uint64_t nc = std::min(std::min(res.n_records, caps[t]), lens[t] / 16);
+                if (nc && (r = d2h_pipelined(c, h_spans[t], spans + s.soff[j],
+                                             nc * sizeof(hg_span))) != HG_OK)
+                    return r;
             }
-            const uint64_t nc = std::min(std::min(res.n_records, caps[t]), lens[t] / 16);
-            if (nc && (r = d2h_pipelined(c, h_spans[t], spans + s.soff[j],
-                                         nc * sizeof(hg_span))) != HG_OK)
-                return r;
         }
         return (int)HG_OK;
     });

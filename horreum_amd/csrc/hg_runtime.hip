@@ -172,6 +172,26 @@ int hg_ctx_destroy(hg_ctx* c) {
     return HG_OK;
 }
 
+int hg_ctx_trim(hg_ctx* c) {
+    if (!c) return HG_ERR_INVALID_ARG;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return HG_HIP_FAIL;
+    for (DevBuf* b : {&c->ws, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
+                      &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res, &c->bws,
+                      &c->x_aux}) {
+        if (b->p) hipFree(b->p);
+        b->p = nullptr;
+        b->bytes = 0;
+    }
+    for (int i = 0; i < c->naux; ++i) {
+        if (c->aux[i] && hipStreamSynchronize(c->aux[i]) != hipSuccess) return HG_HIP_FAIL;
+        if (c->aux_ws[i].p) hipFree(c->aux_ws[i].p);
+        c->aux_ws[i].p = nullptr;
+        c->aux_ws[i].bytes = 0;
+    }
+    return HG_OK;
+}
+
 int hg_ctx_set_stream(hg_ctx* c, void* s) {
     if (!c) return HG_ERR_INVALID_ARG;
     c->stream = reinterpret_cast<hipStream_t>(s);
@@ -1117,17 +1137,18 @@ int hg_keyindex_build_dev_async(hg_ctx* c, const uint8_t* d_table, uint64_t len,
 }
 
 int hg_lookup_dev_async(hg_ctx* c, const uint8_t* d_table, const hg_span* d_spans,
-                        const void* d_index, uint64_t n, const uint8_t* d_keys,
-                        const hg_key* d_queries, uint64_t nq, hg_lookup_result* d_results) {
+                        const void* d_index, uint64_t n, uint32_t block_stride,
+                        const uint8_t* d_keys, const hg_key* d_queries, uint64_t nq,
+                        hg_lookup_result* d_results) {
     if (!c || (nq && (!d_queries || !d_results)) || (n && nq && (!d_table || !d_spans || !d_index)))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
-    return hgk_lookup_launch(d_table, d_spans, d_index, n, d_keys, d_queries, nq, d_results,
-                             c->stream);
+    return hgk_lookup_launch(d_table, d_spans, d_index, n, block_stride, d_keys, d_queries, nq,
+                             d_results, c->stream);
 }
 
-int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, const uint8_t* h_keys,
-                   uint64_t keys_len, const hg_key* h_queries, uint64_t nq,
+int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, uint32_t block_stride,
+                   const uint8_t* h_keys, uint64_t keys_len, const hg_key* h_queries, uint64_t nq,
                    hg_lookup_result* h_results) {
     if (!c || (len && !h_table) || (nq && (!h_queries || !h_results)) || (keys_len && !h_keys))
         return HG_ERR_INVALID_ARG;
@@ -1159,7 +1180,7 @@ int hg_lookup_host(hg_ctx* c, const uint8_t* h_table, uint64_t len, const uint8_
     if (r == HG_OK)
         r = hg_lookup_dev_async(c, static_cast<const uint8_t*>(c->d_in.p),
                                 static_cast<const hg_span*>(c->d_out.p), c->lk_index.p, n,
-                                reinterpret_cast<const uint8_t*>(kd),
+                                block_stride, reinterpret_cast<const uint8_t*>(kd),
                                 reinterpret_cast<const hg_key*>(kd + qat), nq,
                                 static_cast<hg_lookup_result*>(c->lk_res.p));
     if (r != HG_OK) return r;

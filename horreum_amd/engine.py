@@ -179,6 +179,11 @@ class Engine:
         check(self.lib.hg_encoded_size(self.ctx, ptr, n, ctypes.byref(out)), "hg_encoded_size")
         return out.value
 
+    def trim(self):
+        """Free this context's device work buffers (hg_ctx_trim): they grow
+        again on demand."""
+        check(self.lib.hg_ctx_trim(self.ctx), "hg_ctx_trim")
+
     def decode_many_host(self, tables):
         """Many host tables (bytes-like) decoded by ONE batched launch chain on
         this context (hg_multi_decode_host with one context; the cold open of
@@ -287,14 +292,15 @@ class Engine:
         arena = np.frombuffer(b"".join(keys), dtype=np.uint8) if off else np.zeros(1, np.uint8)
         return arena, desc
 
-    def lookup_host(self, table, keys):
+    def lookup_host(self, table, keys, block_stride=0):
         """SSTable::get for many keys (src/sstable/table.rs:54-70) on host
-        table bytes -> LOOKUP_DTYPE results (found, rec, val_off, vlen)."""
+        table bytes with blocks of `block_stride` records (0: one block) ->
+        LOOKUP_DTYPE results (found, rec, val_off, vlen)."""
         buf = np.ascontiguousarray(np.frombuffer(memoryview(table).cast("B"), dtype=np.uint8))
         arena, desc = self.pack_keys(keys)
         out = np.zeros(max(len(desc), 1), dtype=LOOKUP_DTYPE)
         check(self.lib.hg_lookup_host(self.ctx, buf.ctypes.data_as(ctypes.c_void_p), buf.size,
-                                      arena.ctypes.data_as(ctypes.c_void_p),
+                                      int(block_stride), arena.ctypes.data_as(ctypes.c_void_p),
                                       int(desc["len"].sum()) if desc.size else 0,
                                       desc.ctypes.data_as(ctypes.c_void_p), desc.size,
                                       out.ctypes.data_as(ctypes.c_void_p)), "hg_lookup_host")
@@ -311,9 +317,10 @@ class Engine:
         idx = self.keyindex_build(dev, out.spans, out.n) if out.kind == 0 else None
         return ResidentTable(dev, out.spans, idx, out.n, out.kind, out.offset)
 
-    def lookup_resident(self, rt, keys):
-        """Batched point lookups against a ResidentTable: only the query keys
-        go up and the results come back (LOOKUP_DTYPE)."""
+    def lookup_resident(self, rt, keys, block_stride=0):
+        """Batched point lookups against a ResidentTable (blocks of
+        `block_stride` records, 0: one block): only the query keys go up and
+        the results come back (LOOKUP_DTYPE)."""
         torch = _torch()
         arena, desc = self.pack_keys(keys)
         nq = desc.size
@@ -322,7 +329,8 @@ class Engine:
         if nq:
             kd = self.to_device(arena)
             qd = self.to_device(desc.view(np.uint8))
-            self.lookup_dev_async(rt.table, rt.spans, rt.index, rt.n, kd, qd, nq, res)
+            self.lookup_dev_async(rt.table, rt.spans, rt.index, rt.n, kd, qd, nq, res,
+                                  block_stride)
         out = res[: nq * LOOKUP_DTYPE.itemsize].cpu().numpy().view(LOOKUP_DTYPE)
         return out
 
@@ -334,9 +342,10 @@ class Engine:
               "hg_keyindex_build_dev_async")
         return idx
 
-    def lookup_dev_async(self, table, spans, index, n, keys, queries, nq, results):
+    def lookup_dev_async(self, table, spans, index, n, keys, queries, nq, results, block_stride=0):
         check(self.lib.hg_lookup_dev_async(self.ctx, _ptr(table), _ptr(spans), _ptr(index), int(n),
-                                           _ptr(keys), _ptr(queries), int(nq), _ptr(results)),
+                                           int(block_stride), _ptr(keys), _ptr(queries), int(nq),
+                                           _ptr(results)),
               "hg_lookup_dev_async")
 
     # ---- merge / compaction -----------------------------------------------------------

@@ -7,12 +7,32 @@ replacing the reference's second full `serialize_flatten` per block
 from a decode's spans (cold open, src/sstable/table.rs:46) without encoding
 anything.  `get` is the reference's binary search (:72-78).
 """
-import bisect
 from collections import namedtuple
 
 import numpy as np
 
 Block = namedtuple("Block", "key position length")  # src/sstable/index.rs:6-29
+
+
+def rust_binary_search(keys, key):
+    """Rust's slice::binary_search_by_key as the reference calls it
+    (index.rs:74, table.rs:65), std 1.52-1.81: probe mid = left + (right -
+    left) // 2 and return the first probe that compares Equal.  On keys that
+    are not strictly increasing (legal, table.rs:93-108) this picks the same
+    record the reference does, not just any record with the key.  Returns
+    (True, i) for Ok(i), (False, i) for Err(i).  hg_lookup.hip runs the same
+    search on the device."""
+    left, right = 0, len(keys)
+    while left < right:
+        mid = left + (right - left) // 2
+        k = keys[mid]
+        if k == key:
+            return True, mid
+        if k < key:
+            left = mid + 1
+        else:
+            right = mid
+    return False, left
 
 
 class Index:
@@ -69,16 +89,13 @@ class Index:
         return cls(items)
 
     def get(self, key):
-        """src/sstable/index.rs:72-78: exact first-key match -> that block;
-        otherwise the block before the insertion point; None before the
-        first block.  Returns (position, length)."""
-        key = bytes(key)
-        i = bisect.bisect_left(self._keys, key)
-        if i < len(self._keys) and self._keys[i] == key:
-            pos = i
-        elif i > 0:
-            pos = i - 1
-        else:
-            return None
+        """src/sstable/index.rs:72-78: Ok(pos) of the binary search over the
+        first keys -> that block; Err(pos) -> the block before it; None
+        before the first block.  Returns (position, length)."""
+        hit, pos = rust_binary_search(self._keys, bytes(key))
+        if not hit:
+            if pos == 0:
+                return None
+            pos -= 1
         b = self.items[pos]
         return (b.position, b.length)

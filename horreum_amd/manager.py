@@ -44,15 +44,18 @@ class SSTableManager:
         self.compaction_trigger_ratio = compaction_trigger_ratio / 100.0
 
     def _open_all(self, paths):
-        """manager.rs:47-55 as ONE batched decode of every table (the files
-        mmap'd and page-locked, one launch chain for all of them); a table
-        that does not decode raises DecodeError like SSTable.open."""
+        """manager.rs:47-55 as batched decodes of the tables (the files
+        mmap'd pageable -- staged through pinned buffers, see table.py --
+        and decoded by one launch chain per group of tables under the
+        engine's byte budget); a table that does not decode raises
+        DecodeError like SSTable.open."""
         if not paths:
             return []
         eng = self.engine or default_engine()
         files = [PersistedFile.open(p) for p in paths]
         datas = [f.read_bytes(eng) for f in files]
         outs = eng.decode_many_host(datas)
+        eng.trim()  # the batched decode sized the context's buffers for the whole directory
         tables = []
         for f, d, o in zip(files, datas, outs):
             if o.kind != 0:
@@ -126,7 +129,7 @@ class SSTableManager:
             t.delete()
         f = PersistedFile(self._new_table_path())  # table_0 (:77-81 on the emptied list)
         f.write_bytes(data)
-        self.tables.append(SSTable(f, Index.from_encoded(data, out.blocks), size))
+        self.tables.append(SSTable(f, Index.from_encoded(data, out.blocks), size, self.block_stride))
         return True
 
     def flush_arena(self, arena, desc, size):
@@ -138,7 +141,7 @@ class SSTableManager:
         data = out.data.tobytes()
         f = PersistedFile(self._new_table_path())
         f.write_bytes(data)
-        self.tables.append(SSTable(f, Index.from_encoded(data, out.blocks), size))
+        self.tables.append(SSTable(f, Index.from_encoded(data, out.blocks), size, self.block_stride))
         self.compact()
 
     def flush(self, pairs, size):

@@ -24,14 +24,13 @@ Quirks kept from the reference:
 - `SSTable.size` is the payload Σ(klen + vlen), not the file size
   (table.rs:36-45); for a decoded table that is L - 16·n.
 """
-import bisect
 import mmap
 import os
 
 import numpy as np
 
 from .format import DecodeError, decode_spans, pairs_from_spans, serialize_flatten
-from .index import Index
+from .index import Index, rust_binary_search
 
 
 class PersistedFile:
@@ -152,10 +151,11 @@ class PersistedFile:
 class SSTable:
     """src/sstable/table.rs:7-90."""
 
-    def __init__(self, file, index, size):
+    def __init__(self, file, index, size, block_stride=0):
         self.file = file
         self.index = index
         self.size = size
+        self.block_stride = block_stride  # records per index block (batched lookups)
         self._resident = None  # (engine, ResidentTable): lookups stay in HBM
 
     @classmethod
@@ -167,12 +167,12 @@ class SSTable:
         data, blocks = serialize_flatten(pairs, engine, block_stride=block_stride)
         f = PersistedFile(path)
         f.write_bytes(data)
-        return cls(f, Index.from_blocks(pairs, blocks), size)
+        return cls(f, Index.from_blocks(pairs, blocks), size, block_stride)
 
     @classmethod
     def new(cls, file, pairs, size, block_stride, engine=None):
         """table.rs:22-31: a table over an already written file."""
-        return cls(file, Index.new(pairs, block_stride, engine), size)
+        return cls(file, Index.new(pairs, block_stride, engine), size, block_stride)
 
     @classmethod
     def open(cls, path, block_stride, engine=None):
@@ -188,7 +188,7 @@ class SSTable:
         if block_stride <= 0:
             raise ValueError("block_stride must be positive (reference: chunks(0) panics)")
         size = len(data) - 16 * int(spans.size)
-        return cls(f, Index.from_spans(data, spans, block_stride), size)
+        return cls(f, Index.from_spans(data, spans, block_stride), size, block_stride)
 
     def get(self, key, engine=None):
         """table.rs:54-70: index -> one block read -> decode -> binary search."""
@@ -198,10 +198,8 @@ class SSTable:
         position, length = hit
         block = self.file.read_at(position, length)
         pairs = pairs_from_spans(block, decode_spans(block, engine))
-        keys = [p.key for p in pairs]
-        key = bytes(key)
-        i = bisect.bisect_left(keys, key)
-        return pairs[i] if i < len(keys) and keys[i] == key else None
+        hit, i = rust_binary_search([p.key for p in pairs], bytes(key))
+        return pairs[i] if hit else None
 
     def resident(self, engine=None):
         """The table in HBM for batched lookups: uploaded, decoded and
@@ -217,13 +215,15 @@ class SSTable:
 
     def get_many(self, keys, engine=None):
         """SSTable::get for a batch of keys in one device launch against the
-        resident table (only the keys go up).  Returns one InternalPair
-        (tombstones included) or None per key."""
+        resident table (only the keys go up): the same block search and
+        in-block search as `get`, so `get_many(ks)[i] == get(ks[i])` on any
+        table, duplicate or unordered keys included.  Returns one
+        InternalPair (tombstones included) or None per key."""
         from .engine import default_engine
         from .format import InternalPair
         eng = engine or default_engine()
         rt = self.resident(eng)
-        res = eng.lookup_resident(rt, keys)
+        res = eng.lookup_resident(rt, keys, self.block_stride)
         data = self.file.read_bytes(eng)
         mv = memoryview(data).cast("B")
         out = []

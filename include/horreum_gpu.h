@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 4
+#define HG_ABI_VERSION 5
 
 /* Status codes: return values, and the `kind` field of hg_err / results. */
 enum hg_status {
@@ -158,6 +158,11 @@ int hg_ctx_create(int device, hg_ctx** out);
 int hg_ctx_destroy(hg_ctx* ctx);
 /* Launch on a caller stream (a hipStream_t; NULL = the null stream). */
 int hg_ctx_set_stream(hg_ctx* ctx, void* hip_stream);
+/* Free the context's device work buffers (decode/encode/merge arenas and
+ * workspaces; they grow again on demand): e.g. after SSTableManager's cold
+ * open (src/sstable/manager.rs:47-55), whose batched decode sized them for a
+ * whole directory.  Synchronizes the context's stream first. */
+int hg_ctx_trim(hg_ctx* ctx);
 /* Go back to the stream the context created for itself. */
 int hg_ctx_use_own_stream(hg_ctx* ctx);
 void* hg_ctx_stream(hg_ctx* ctx);
@@ -312,22 +317,25 @@ int hg_compact_dev(hg_ctx* ctx, uint32_t ntables, const uint8_t* d_arena,
                    hg_block* d_blocks, hg_merge_result* result);
 
 /* ---- point lookups ----------------------------------------------------
- * Replaces SSTable::get (src/sstable/table.rs:54-70; Index::get,
- * src/sstable/index.rs:72-78) for a batch of keys.  The table is decoded
- * (d_spans, n records) and must be strictly increasing by key, as every
- * table horreum writes is; then the record whose key equals each query is
- * what the reference's block-index path returns.  First build the key index
- * once per table (32 * n bytes of device memory at d_index), then look up
- * any number of batches. */
+ * Replaces SSTable::get (src/sstable/table.rs:54-70) for a batch of keys:
+ * Index::get (src/sstable/index.rs:72-78) binary-searches the first keys of
+ * the blocks of `block_stride` records (0: the whole table is one block),
+ * then binary_search_by_key searches that block.  Both follow Rust's
+ * slice::binary_search_by (std 1.52-1.81: mid = left + (right - left) / 2,
+ * the first probe that compares Equal wins), so on any table -- duplicate or
+ * unordered keys included (legal, table.rs:93-108) -- the record found is
+ * the reference's.  First build the key index once per decoded table (d_spans,
+ * n records; 32 * n bytes of device memory at d_index), then look up any
+ * number of batches. */
 uint64_t hg_keyindex_bytes(uint64_t n);
 int hg_keyindex_build_dev_async(hg_ctx* ctx, const uint8_t* d_table, uint64_t len,
                                 const hg_span* d_spans, uint64_t n, void* d_index);
 int hg_lookup_dev_async(hg_ctx* ctx, const uint8_t* d_table, const hg_span* d_spans,
-                        const void* d_index, uint64_t n, const uint8_t* d_keys,
-                        const hg_key* d_queries, uint64_t nq,
+                        const void* d_index, uint64_t n, uint32_t block_stride,
+                        const uint8_t* d_keys, const hg_key* d_queries, uint64_t nq,
                         hg_lookup_result* d_results);
 /* Host table bytes and host keys: decode, index, look up, copy back. */
-int hg_lookup_host(hg_ctx* ctx, const uint8_t* h_table, uint64_t len,
+int hg_lookup_host(hg_ctx* ctx, const uint8_t* h_table, uint64_t len, uint32_t block_stride,
                    const uint8_t* h_keys, uint64_t keys_len, const hg_key* h_queries,
                    uint64_t nq, hg_lookup_result* h_results);
 
@@ -350,7 +358,10 @@ int hg_host_is_pinned(const void* h_ptr);
  *
  * Many tables (SSTableManager::new opening a directory, manager.rs:47-55;
  * BASELINE config 4): table i goes to context i % nctx; each context uploads
- * its tables and decodes them in one batched launch chain.  spans of table i
+ * its tables and decodes them in one batched launch chain per group of tables
+ * under a device byte budget (HG_DECODE_GROUP_BYTES, default 40 % of the free
+ * device memory; tables plus span capacity), so a directory larger than HBM
+ * opens group by group.  spans of table i
  * to h_spans[i] (capacity caps[i]), n_out[i] records, errs[i] its format
  * error (kind HG_OK if none; errs may be NULL).  Returns HG_OK unless a
  * runtime error occurred. */

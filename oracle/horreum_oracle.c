@@ -141,40 +141,47 @@ found:
     return 1;
 }
 
+/* Rust's slice::binary_search_by_key over records base + i * step, i in
+ * [0, size), as the reference calls it (index.rs:74, table.rs:65).  Rust std
+ * 1.52-1.81 (the reference pins no toolchain; this is the implementation
+ * current from its tokio-1.0 era on): mid = left + size / 2 with size =
+ * right - left, the first probe that compares Equal returns Ok(mid), else
+ * Err(left).  The reference's own tests search unique keys only, so which
+ * duplicate a search returns is this restatement's choice ("parity unpinned"
+ * for duplicate keys).  Returns 1 (Ok) or 0 (Err) and the index in *pos. */
+static int rust_search(const uint8_t* data, const hg_span* spans, uint64_t base, uint64_t step,
+                       uint64_t size, const uint8_t* key, uint64_t klen, uint64_t* pos) {
+    uint64_t left = 0, right = size;
+    while (left < right) {
+        const uint64_t mid = left + (right - left) / 2;
+        const hg_span* s = &spans[base + mid * step];
+        const int c = key_cmp(data + s->off + 16, s->klen, key, klen);
+        if (c == 0) { *pos = mid; return 1; }
+        if (c < 0) left = mid + 1;
+        else right = mid;
+    }
+    *pos = left;
+    return 0;
+}
+
 /* src/sstable/table.rs:54-70 (SSTable::get) on a decoded table: the block
  * index of Index::new (index.rs:55-67, blocks of `stride` records), its get
- * (index.rs:72-78: exact first key -> that block, else the block before the
- * insertion point, none before the first block), then binary_search_by_key
+ * (index.rs:72-78: Ok(b) of the binary search over the blocks' first keys ->
+ * block b, Err(b) -> block b - 1, none if b == 0), then binary_search_by_key
  * over the block's records.  Returns 1 and the record index if found. */
 int hgo_table_get(const uint8_t* data, const hg_span* spans, uint64_t n, uint32_t stride,
                   const uint8_t* key, uint64_t klen, uint64_t* rec) {
     if (n == 0 || stride == 0) return 0;
     const uint64_t nb = (n + stride - 1) / stride;
-    uint64_t lo = 0, hi = nb; /* first block whose first key >= key */
-    while (lo < hi) {
-        uint64_t mid = lo + (hi - lo) / 2;
-        const hg_span* s = &spans[mid * stride];
-        if (key_cmp(data + s->off + 16, s->klen, key, klen) < 0) lo = mid + 1;
-        else hi = mid;
+    uint64_t b = 0, j = 0;
+    if (!rust_search(data, spans, 0, stride, nb, key, klen, &b)) {
+        if (b == 0) return 0;
+        --b;
     }
-    uint64_t b;
-    if (lo < nb && key_cmp(data + spans[lo * stride].off + 16, spans[lo * stride].klen, key, klen) == 0)
-        b = lo;
-    else if (lo == 0)
-        return 0;
-    else
-        b = lo - 1;
-    /* binary_search_by_key within the block's records */
-    uint64_t r0 = b * stride, r1 = r0 + stride < n ? r0 + stride : n;
-    uint64_t l = r0, h = r1;
-    while (l < h) {
-        uint64_t mid = l + (h - l) / 2;
-        int c = key_cmp(data + spans[mid].off + 16, spans[mid].klen, key, klen);
-        if (c == 0) { if (rec) *rec = mid; return 1; }
-        if (c < 0) l = mid + 1;
-        else h = mid;
-    }
-    return 0;
+    const uint64_t r0 = b * stride, cnt = n - r0 < stride ? n - r0 : stride;
+    if (!rust_search(data, spans, r0, 1, cnt, key, klen, &j)) return 0;
+    if (rec) *rec = r0 + j;
+    return 1;
 }
 
 /* src/sstable/manager.rs:199-234. */

@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_status_strings():
     lib = abi.load_library()
-    assert lib.hg_abi_version() == 4
+    assert lib.hg_abi_version() == 5
     for st in abi.Status:
         s = lib.hg_status_string(int(st)).decode()
         assert s and s != "unknown status", st

@@ -289,3 +289,32 @@ def test_resident_lookups(engine, golden, tmp_path):
     assert t.resident(engine) is rt
     assert first == [t.get(k, engine) for k in keys]
     assert second == list(reversed(first))
+
+
+def test_rust_binary_search_two_level_matches_oracle():
+    """index.rust_binary_search used as SSTable::get uses it (Index::get over
+    block first keys, then the block; index.rs:72-78, table.rs:65-68) picks
+    the oracle's record on tables with duplicate and unordered keys."""
+    from horreum_amd.index import rust_binary_search
+    rng = np.random.default_rng(5)
+    for trial in range(40):
+        n = int(rng.integers(1, 60))
+        keys = [bytes(rng.choice(list(b"ab"), size=int(rng.integers(0, 3))).tolist()) for _ in range(n)]
+        pairs = [(k, b"v") for k in keys]
+        arena, recs = oracle.pack_pairs(pairs)
+        data = oracle.encode(arena, recs)[0]
+        spans = oracle.decode(data)[0]
+        for stride in (1, 2, 3, 7):
+            firsts = keys[::stride]
+            for q in [b"", b"a", b"b", b"aa", b"ab", b"ba", b"bb", b"c", b"aaa"]:
+                hit, b = rust_binary_search(firsts, q)
+                got = None
+                if hit or b > 0:
+                    b = b if hit else b - 1
+                    blk = keys[b * stride:(b + 1) * stride]
+                    h2, j = rust_binary_search(blk, q)
+                    got = b * stride + j if h2 else None
+                assert got == oracle.table_get(data, spans, stride, q), (trial, stride, q)
+    # Ok on the first probe that compares Equal, as Rust's std (1.52-1.81) does
+    assert rust_binary_search([b"a", b"a", b"a", b"a"], b"a") == (True, 2)
+    assert rust_binary_search([b"a", b"b"], b"c") == (False, 2)

@@ -478,3 +478,99 @@ def test_lane_walk_mode_at_scale(engine, shape):
     assert np.mean(codes == 6) >= 0.99, np.unique(codes, return_counts=True)
     assert_same(engine, data[: data.size - 5])
     assert_same(engine, data[: (data.size // CHUNK - 5) * CHUNK + 3])
+
+
+def _zero_valued(m, kr, vr, seed):
+    """Random non-zero key bytes, all-zero value bytes (tools/decode_variants.py
+    zero shapes): every 16 value bytes read as an empty record."""
+    rng = np.random.default_rng(seed)
+    kl = np.full(m, kr[0]) if kr[1] - kr[0] == 1 else rng.integers(*kr, m)
+    vl = rng.integers(*vr, m)
+    offs = np.concatenate([[0], np.cumsum(16 + kl + vl)])
+    buf = np.zeros(int(offs[-1]), np.uint8)
+    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
+    for i in range(16):
+        buf[offs[:-1] + i] = hdr[:, i]
+    nk = int(kl.sum())
+    kpos = np.repeat(offs[:-1] + 16, kl) + (np.arange(nk) - np.repeat(np.cumsum(kl) - kl, kl))
+    buf[kpos] = rng.integers(1, 256, nk, dtype=np.uint8)
+    return buf
+
+
+def _decode_ms(engine, data, reps=3):
+    import time
+    import torch
+    d = engine.to_device(data)
+    spans = engine.empty(data.size // 16 * 16)
+    res = engine.empty(64)
+    engine.decode_dev_async(d, data.size, spans, data.size // 16, res)
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        engine.decode_dev_async(d, data.size, spans, data.size // 16, res)
+        torch.cuda.synchronize()
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return sorted(ts)[len(ts) // 2]
+
+
+@pytest.mark.parametrize("shape", [("small", 1_500_000, (1, 24), (0, 64)),
+                                   ("midlarge", 400_000, (16, 17), (400, 1201))])
+def test_zero_valued_records_resolved_fast(engine, shape):
+    """Zero-byte values (every position inside a value reads as an empty
+    record): bit-exact vs the oracle, every pre-pass batch resolved by the
+    lane walks (lw_guess_nz, the long lead-in), and no serial redo chain --
+    round 2 took 984 ms on 832 MB of the midlarge shape; the bound here is
+    loose (box noise) but three orders of magnitude below that."""
+    _, m, kr, vr = shape
+    data = _zero_valued(m, kr, vr, seed=9)
+    assert_same(engine, data)
+    codes = _prepass_codes(engine) & 0xFF
+    assert np.mean(codes == 6) >= 0.99, np.unique(codes, return_counts=True)
+    assert _decode_ms(engine, data) < 25.0
+    assert_same(engine, data[: data.size - 3])
+
+
+def _ctl_repairs(engine):
+    import ctypes
+    lib = engine.lib
+    ctl = np.zeros(4, np.uint32)
+    ws = lib.hgk_ctx_workspace(engine.ctx)
+    lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws), 16)
+    return int(ctl[3])
+
+
+@pytest.mark.parametrize("fake_every", [1, 3])
+def test_splice_repair_of_wrong_batch_entries(engine, fake_every):
+    """A pre-pass batch whose guessed entry is wrong but whose path joins the
+    true one (a fake header planted inside the value that spans the batch's
+    first byte, decoding as one record that lands on a later true header) is
+    spliced onto its predecessor's exit (splice_repair) instead of decoded
+    again: spans bit-exact vs the oracle, repairs counted."""
+    arena, pairs = _large_mixed(30000, seed=71, vmin=1024, vmax=4096, tomb=0.0)
+    data, rec_off, _, _ = oracle.encode(arena, pairs)
+    starts = rec_off.astype(np.int64)
+    assert_same(engine, data)  # learn the pre-pass geometry of this size
+    import ctypes
+    lay = (ctypes.c_uint64 * 8)()
+    engine.lib.hgk_decode_last_layout(lay)
+    sbp = int(lay[3])
+    bsz = sbp * CHUNK
+    planted = 0
+    for b in range(1, data.size // bsz, fake_every):
+        B = b * bsz
+        i = int(np.searchsorted(starts, B, side="right")) - 1  # record spanning B
+        if i + 3 >= starts.size:
+            break
+        vstart = int(starts[i]) + 16 + int(pairs["klen"][i])
+        f = max(B + 5, vstart)
+        if f + 16 > int(starts[i + 1]) - 16:
+            continue  # no room inside this value before the next header
+        h2 = int(starts[i + 2])  # the fake record jumps over starts[i + 1]
+        body = h2 - f - 16
+        hdr = (40).to_bytes(8, "little") + int(body - 40).to_bytes(8, "little")
+        data[f:f + 16] = np.frombuffer(hdr, np.uint8)
+        planted += 1
+    assert planted > 10
+    assert_same(engine, data)
+    assert _ctl_repairs(engine) > 0

@@ -96,3 +96,66 @@ def test_manager_get_many(engine, golden, tmp_path):
                   for k, v in kvs], size)
     keys = [b"abc00", b"abc01", b"abc02", b"xxx", b"zzz", b""]
     assert m.get_many(keys) == [m.get(k) for k in keys]
+
+
+# ---- tables that are not strictly increasing (legal: src/sstable/table.rs:93-108) ------
+def _unordered_pairs(seed, n):
+    """Keys from a small alphabet: runs of duplicates, disorder, tombstones."""
+    rng = np.random.default_rng(seed)
+    pairs = []
+    for _ in range(n):
+        k = bytes(rng.choice(list(b"abc"), size=int(rng.integers(0, 4))).tolist())
+        if rng.random() < 0.5 and pairs:
+            k = pairs[-1][0]  # a duplicate of the previous key
+        v = None if rng.random() < 0.3 else rng.integers(0, 256, int(rng.integers(1, 6)),
+                                                          dtype=np.uint8).tobytes()
+        pairs.append((k, v))
+    return pairs
+
+
+def _all_keys(depth=3):
+    out = [b""]
+    for d in range(1, depth + 2):
+        out += [bytes(t) for t in np.array(np.meshgrid(*[list(b"abcd")] * d)).T.reshape(-1, d).tolist()]
+    return out
+
+
+@pytest.mark.parametrize("stride", [0, 1, 2, 3, 10])
+def test_lookup_duplicate_and_unordered_keys(engine, golden, stride):
+    """The record found is the reference's (Rust binary searches over the
+    block first keys and in the block), on the table.rs:93-108 pairs and on
+    random tables with duplicate runs and disorder."""
+    tables = [[(b"abc", b"defg"), (b"abc", None), ("日本語💖".encode(), "ржавчина".encode())]]
+    tables += [_unordered_pairs(seed, n) for seed, n in [(31, 50), (32, 300), (33, 2000)]]
+    for pairs in tables:
+        arena, recs = oracle.pack_pairs(pairs)
+        data = oracle.encode(arena, recs)[0]
+        spans = oracle.decode(data)[0]
+        queries = sorted({k for k, _ in pairs}) + _all_keys() + ["日本語💖".encode()]
+        res = engine.lookup_host(data.tobytes(), queries, stride)
+        for q, r in zip(queries, res):
+            want = oracle.table_get(data, spans, stride or max(len(pairs), 1), q)
+            assert (r["found"] == 1) == (want is not None), (stride, q)
+            if want is not None:
+                assert r["rec"] == want, (stride, q)
+
+
+@pytest.mark.parametrize("stride", [1, 3])
+def test_get_many_equals_get_on_duplicates(engine, tmp_path, stride):
+    """SSTable.get_many == SSTable.get key by key on the table.rs:93-108
+    pairs (a live value and a tombstone under the same key), both equal to
+    the oracle's record."""
+    pairs = [InternalPair(b"abc", b"defg"), InternalPair(b"abc", None),
+             InternalPair("日本語💖".encode(), "ржавчина".encode())]
+    path = tmp_path / f"dup{stride}"
+    table = SSTable.new(PersistedFile.new(path, pairs, engine), pairs, 39, stride, engine)
+    keys = [b"abc", "日本語💖".encode(), b"ab", b"abd", b""]
+    got = table.get_many(keys, engine)
+    data = np.fromfile(path, dtype=np.uint8)
+    spans = oracle.decode(data)[0]
+    for k, g in zip(keys, got):
+        assert g == table.get(k, engine), k
+        want = oracle.table_get(data, spans, stride, k)
+        assert (g is None) == (want is None), k
+        if want is not None:
+            assert g == pairs[want], k

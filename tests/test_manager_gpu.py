@@ -148,3 +148,33 @@ def test_compaction_of_duplicate_key_table(engine, golden, tmp_path):
     merged = [InternalPair(*oracle.pairs_from_spans(dec[t][0], dec[t][1][r:r + 1])[0])
               for t, r in refs]
     assert m.tables[0].get_all(engine) == merged
+
+
+def test_cold_open_over_the_byte_budget(engine, tmp_path, monkeypatch):
+    """A directory larger than the batched decode's device byte budget opens
+    group by group (HG_DECODE_GROUP_BYTES set below one table's share, so
+    every table is a group), spans identical to the oracle's; the context's
+    work buffers are released afterwards (hg_ctx_trim)."""
+    import numpy as np
+    rng = np.random.default_rng(41)
+    want = []
+    for i in range(6):
+        pairs = [(b"k%06d" % j + bytes([i]), rng.integers(0, 256, int(rng.integers(0, 200)),
+                                                           dtype=np.uint8).tobytes())
+                 for j in range(int(rng.integers(1000, 4000)))]
+        arena, rec = oracle.pack_pairs(pairs)
+        data = oracle.encode(arena, rec)[0]
+        (tmp_path / f"table_{i}").write_bytes(data.tobytes())
+        want.append(oracle.decode(data)[0])
+    monkeypatch.setenv("HG_DECODE_GROUP_BYTES", str(64 << 10))
+    m = SSTableManager(tmp_path, 10, 1000, engine)
+    assert len(m.tables) == 6
+    for t, w in zip(m.tables, want):
+        got = [p.key for p in t.get_all(engine)]
+        assert len(got) == w.size
+        data = np.fromfile(t.file.path, dtype=np.uint8)
+        assert got == [data[int(s["off"]) + 16:int(s["off"]) + 16 + int(s["klen"])].tobytes()
+                       for s in w]
+    monkeypatch.setenv("HG_DECODE_GROUP_BYTES", str(1 << 40))
+    m2 = SSTableManager(tmp_path, 10, 1000, engine)  # one group: same tables
+    assert [t.get_size() for t in m2.tables] == [t.get_size() for t in m.tables]

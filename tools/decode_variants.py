@@ -38,6 +38,27 @@ def workloads(dev):
         for i in range(16):
             buf[offs[:-1] + i] = hdr[:, i]
         yield label, torch.from_numpy(buf).to(dev)
+    # zero-byte values (keys non-zero): every 16 value bytes read as a header candidate
+    for label, m, kr, vr, seed in [("zero small 1..23B/0..63B", 3_000_000, (1, 24), (0, 64), 9),
+                                   ("zero midlarge 16B/400..1200B", 1_000_000, (16, 17), (400, 1201), 9)]:
+        yield label, torch.from_numpy(zero_valued(m, kr, vr, seed)).to(dev)
+
+
+def zero_valued(m, kr, vr, seed):
+    """Records with random non-zero key bytes and all-zero value bytes
+    (tools/zero_values.py's shapes)."""
+    rng = np.random.default_rng(seed)
+    kl = np.full(m, kr[0]) if kr[1] - kr[0] == 1 else rng.integers(*kr, m)
+    vl = rng.integers(*vr, m)
+    offs = np.concatenate([[0], np.cumsum(16 + kl + vl)])
+    buf = np.zeros(int(offs[-1]), np.uint8)
+    hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
+    for i in range(16):
+        buf[offs[:-1] + i] = hdr[:, i]
+    nk = int(kl.sum())
+    kpos = np.repeat(offs[:-1] + 16, kl) + (np.arange(nk) - np.repeat(np.cumsum(kl) - kl, kl))
+    buf[kpos] = rng.integers(1, 256, nk, dtype=np.uint8)
+    return buf
 
 
 def main():

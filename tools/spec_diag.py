@@ -31,7 +31,8 @@ SB = np.dtype([("x0", "<u8"), ("exit", "<u8"), ("count", "<u4"), ("ok", "<u4"), 
 
 
 def main():
-    only = sys.argv[1] if len(sys.argv) > 1 else None
+    args = [x for x in sys.argv[1:] if not x.startswith("--")]
+    only = args[0] if args else None
     eng = Engine(0)
     lib = eng.lib
     lib.hgk_ctx_workspace.restype = ctypes.c_void_p
@@ -52,11 +53,19 @@ def main():
         ctl = np.zeros(4, np.uint32)
         lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws), 16)
         fb = nspec - int(ctl[1])
-        codes = Counter(int(c) & 0xFFFFFFFF for c in sb["pad"])
+        codes = Counter(int(c) & 0xFF for c in sb["pad"])
+        why = Counter((int(c) >> 8) & 0xFF for c in sb["pad"] if (int(c) >> 8) & 0xFF)
         links = int(np.sum(sb["x0"][1:] != sb["exit"][:-1]))
         print(f"{label}: n={out.n} kind={out.kind} nspec={nspec} sbp={sbp} bp={bp} "
-              f"first_bad={fb} codes={dict(sorted(codes.items()))} link_mismatch={links} "
-              f"ok={int(sb['ok'].sum())} lw_serial={int((sb['pad'] >> 32).sum())}", flush=True)
+              f"first_bad={fb} codes={dict(sorted(codes.items()))} dead_why={dict(why)} link_mismatch={links} "
+              f"ok={int(sb['ok'].sum())} lw_serial={int((sb['pad'] >> 32).sum())} repairs={int(ctl[3])}", flush=True)
+        if "--truth" in sys.argv:  # are the guessed entries / exits true record starts?
+            from oracle import oracle
+            starts = oracle.decode(sst.cpu().numpy())[0]["off"]
+            okm = sb["ok"] != 0
+            x_in = np.isin(sb["x0"][okm], starts) | (sb["x0"][okm] == L)
+            e_in = np.isin(sb["exit"][okm], starts) | (sb["exit"][okm] == L)
+            print(f"   ok batches {int(okm.sum())}: entry true {int(x_in.sum())}, exit true {int(e_in.sum())}")
         bad = np.nonzero(sb["x0"][1:] != sb["exit"][:-1])[0][:5]
         for j in bad:
             print(f"   link {j}->{j+1}: exit {sb['exit'][j]} x0 {sb['x0'][j+1]} "
