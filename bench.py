@@ -333,6 +333,9 @@ def main(argv=None):
                                                            host=not args.no_host and world == 1)
         extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank,
                                                          host=not args.no_host and world == 1)
+        extra["compaction_cfg5_share"] = compaction_leg(torch, eng, device, world, rank,
+                                                        per_table=8_134_407, exact=True,
+                                                        pmc_name="r3_pmc_compaction_share.json")
 
     if not args.no_extra:
         extra["decode_general"] = general_legs(torch, eng, device, world)
@@ -382,29 +385,55 @@ def main(argv=None):
     return 0 if ok else 1
 
 
-GENERAL_SHAPES = [  # (label, records, key range, value range, tombstones, seed)
-    ("small mixed 0..24B/0..64B", 4_000_000, (0, 24), (0, 64), 0.05, 4),
-    ("medium 8..64B/64..512B", 1_500_000, (8, 65), (64, 513), 0.05, 4),
+GENERAL_SHAPES = [  # (key, label, records, key range, value range, tombstones, seed, zero values)
+    ("small", "small mixed 0..24B/0..64B", 4_000_000, (0, 24), (0, 64), 0.05, 4, False),
+    ("medium", "medium 8..64B/64..512B", 1_500_000, (8, 65), (64, 513), 0.05, 4, False),
+    ("midlarge", "midlarge 16B/400..1200B", 1_000_000, (16, 17), (400, 1201), 0.05, 4, False),
+    ("zmidlarge", "zero-valued midlarge 16B/400..1200B", 1_000_000, (16, 17), (400, 1201), 0.0, 9,
+     True),
+    ("zsmall", "zero-valued small 1..23B/0..63B", 3_000_000, (1, 24), (0, 64), 0.0, 9, True),
 ]
 
 
+def load_leg_pmc(name, sources):
+    """A bench leg's PMC summary (tools/summarize_pmc.py): per-kernel HBM
+    bytes and the sha256 of the sources it was taken at; current_source says
+    whether those are the sources being run now."""
+    import hashlib
+    path = os.path.join(ROOT, "profiles", name)
+    try:
+        with open(path, encoding="utf-8") as f:
+            pmc = json.load(f)
+    except (OSError, ValueError):
+        return {}, {"file": None}
+    src = dict(pmc.get("_source", {}))
+    cur = {}
+    for s in sources:
+        try:
+            cur[s] = hashlib.sha256(open(os.path.join(ROOT, "horreum_amd", "csrc", s), "rb").read()).hexdigest()
+        except OSError:
+            cur[s] = None
+    src["file"] = f"profiles/{name}"
+    src["current_source"] = all(src.get("sha256", {}).get(s) == h for s, h in cur.items())
+    src.pop("sha256", None)
+    return pmc.get("kernels", {}), src
+
+
 def general_legs(torch, eng, device, world, reps=8):
-    """The general decode engine (no stride run, no hop) on variable-size
-    records: small (0-24 B keys / 0-64 B values) and medium (8-64 B / 64-512 B)
-    tables, device resident; roofline against the same algorithmic bytes as
-    the headline (L + 16 n), HIP-event time of the decode call; every span
-    checked against the generator's own record layout (offsets, lengths)."""
+    """Decode of variable-size records (no stride run): small (0-24 B keys /
+    0-64 B values) and medium (8-64 B / 64-512 B) records -- the lane-walk
+    pre-pass --, 400-1200 B records (hop mode), and the same mid-size and
+    small shapes with all-zero value bytes (every 16 value bytes read as an
+    empty record: the guesses' worst case).  Device resident; roofline
+    against the headline's algorithmic bytes (L + 16 n), HIP-event time of
+    the decode call; every span checked against the generator's own record
+    layout; PMC traffic from the committed, source-hashed profile of the
+    shape (profiles/r3_pmc_<shape>.json)."""
     from horreum_amd import synth
     out = {}
-    pmc = {}
-    try:
-        for s in ("small", "medium"):
-            with open(os.path.join(ROOT, "profiles", f"r2_pmc_{s}.json"), encoding="utf-8") as f:
-                pmc[s] = json.load(f)
-    except (OSError, ValueError):
-        pass
-    for label, m, kr, vr, tomb, seed in GENERAL_SHAPES:
-        host, g_off, g_kl, g_vl = synth.mixed_sst_host(m, kr, vr, tomb, seed, layout=True)
+    for key, label, m, kr, vr, tomb, seed, zero in GENERAL_SHAPES:
+        host, g_off, g_kl, g_vl = synth.mixed_sst_host(m, kr, vr, tomb, seed, layout=True,
+                                                       zero_values=zero)
         sst = torch.from_numpy(host).to(device)
         L = host.size
         cap = L // 16
@@ -424,18 +453,15 @@ def general_legs(torch, eng, device, world, reps=8):
         ok = nn == wn and kind == 0 and bool(np.array_equal(
             spans[: nn * 16].cpu().numpy().view("<u8").reshape(-1, 2), want))
         alg = L + 16 * wn
-        key = "small" if label.startswith("small") else "medium"
-        kern = pmc.get(key, {}).get("kernels", {})
-        traffic = sum(kern.get(k, {}).get("hbm_read_bytes", 0) + kern.get(k, {}).get(
-            "hbm_write_bytes", 0) for k in ("hgk::decode_spec_kernel",
-                                            "hgk::decode_kernel<false>")) or None
+        kern, src = load_leg_pmc(f"r3_pmc_{key}.json", ("hg_decode.hip",))
+        traffic = sum(v.get("hbm_read_bytes", 0) + v.get("hbm_write_bytes", 0)
+                      for k, v in kern.items() if "decode" in k) or None
         out[key] = {"workload": label, "bytes": L, "records": wn,
                     "ms": round(mean_ms, 4), "value_GiB_s": round(L / (mean_ms * 1e-3) / GIB, 2),
                     "roofline": {"bound": "hbm", "achieved": round(alg / (mean_ms * 1e-3) / 1e9, 1),
                                  "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                  "frac": round(alg / (mean_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                 "traffic": traffic,
-                                 "traffic_source": f"profiles/r2_pmc_{key}.json"},
+                                 "traffic": traffic, "traffic_source": src},
                     "parity_ok": ok}
         del sst, spans
         torch.cuda.empty_cache()
@@ -704,26 +730,38 @@ def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32, ho
                                               "the generated record layout"}
 
 
-def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000, host=False):
-    """BASELINE config 5 scaled to one GPU's share: 8 sorted tables of 1 M
-    records (16 B keys / 100 B values, 132 MB each), 25 % of each table's keys
-    shared by all tables.  Decode all, device merge (newest wins), encode the
-    merged table: one hg_compact_dev call, timed end to end (its host sync
-    for the record counts -- the merge is launched from them -- and the final
-    one for the results included).  With `host`, also the
-    end-to-end rate from host memory (cfg 5 asks for H2D/D2H included):
-    hg_compact_host on pageable copies of the same tables (H2D of every
+def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000, host=False,
+                   pmc_name="r3_pmc_compaction.json", exact=False):
+    """BASELINE config 5 on this GPU's key range: 8 sorted tables of
+    `per_table` records each (16 B keys / 100 B values, 132 B records), 25 %
+    of each table's keys shared by all tables.  The global dataset is 8
+    tables over the key space [0, world * 2^40); rank r holds key range
+    [r * 2^40, (r + 1) * 2^40) of every table -- the split by key range of
+    SURVEY §8e, its splitters the range boundaries (the first keys of the
+    blocks at the cuts) -- so each GPU compacts its slices with no data
+    movement and the compacted table is the ranks' outputs in rank order.
+    per_table = 8,134,407 (1 GiB of records per table) is one GPU's share of
+    cfg 5's 8 x 8 GiB over 8 GPUs.  Decode all, device merge (newest wins),
+    encode: one hg_compact_dev call, timed end to end (its host sync for the
+    record counts -- the merge is launched from them -- and the final one
+    included), median of 3.  Parity: the record count equals the distinct
+    keys; with `exact`, the output equals, byte for byte, the rows of the
+    key union each taken from the newest table holding it (a stable sort of
+    (key, table), gathered on the device).  With `host`, also the end-to-end
+    rate from host memory (hg_compact_host on pageable copies: H2D of every
     table, decode, merge, encode, D2H of the compacted table), median of 3."""
     from horreum_amd import synth
     rng = np.random.default_rng(5 + 1000 * rank)
-    shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64))
+    lo = np.uint64(rank) << np.uint64(40)
+    shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64)) + lo
     bufs, offs_b, total, n_in, allkeys = [], [], 0, 0, []
     for t in range(ntab):
-        own = rng.integers(0, 1 << 40, size=per_table - shared.size, dtype=np.uint64)
+        own = rng.integers(0, 1 << 40, size=per_table - shared.size, dtype=np.uint64) + lo
         keys = np.unique(np.concatenate([shared, own]))
         n_in += int(keys.size)
         allkeys.append(keys)
-        buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=50 + t, device=device)
+        buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=50 + t + 1000 * rank,
+                                   device=device)
         bufs.append(buf)
     sizes = [b.numel() for b in bufs]
     hosts = [b.cpu().numpy() for b in bufs] if host else None
@@ -733,7 +771,19 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     arena = torch.zeros(total, dtype=torch.uint8, device=device)
     for o, b in zip(offs_b, bufs):
         arena[o:o + b.numel()] = b
-    del bufs
+    want_rows = None
+    if exact:  # newest-wins union: stable sort of (key, table)
+        allk = np.concatenate(allkeys)
+        row = np.concatenate([np.arange(k.size, dtype=np.int64) + base for k, base in
+                              zip(allkeys, np.cumsum([0] + [k.size for k in allkeys[:-1]]))])
+        order = np.argsort(allk, kind="stable")
+        ks = allk[order]
+        first = np.ones(ks.size, bool)
+        first[1:] = ks[1:] != ks[:-1]
+        want_rows = torch.from_numpy(row[order][first]).to(device)
+        del allk, row, order, ks, first
+    else:
+        del bufs
     out = eng.empty(total)
 
     def run():
@@ -752,29 +802,37 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
         times.append(time.perf_counter() - t0)
     wall = max_over_ranks(sorted(times)[1], world, device)
     in_bytes = sum(sizes)
+    n_distinct = int(np.unique(np.concatenate(allkeys)).size)
+    exact_ok = None
+    if want_rows is not None:
+        rows = torch.cat(bufs).view(-1, 132)
+        exact_ok = bool(out_len == want_rows.numel() * 132 and torch.equal(
+            out[:out_len], rows.index_select(0, want_rows).view(-1)))
+        del rows, bufs, want_rows
     del arena, out
     torch.cuda.empty_cache()
     line = {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
-            "tables": ntab, "input_bytes_per_gpu": in_bytes, "merged_records": int(m.n),
-            "merged_bytes": int(out_len), "ms": round(wall * 1e3, 3),
+            "tables": ntab, "records_per_table": per_table, "input_bytes_per_gpu": in_bytes,
+            "merged_records": int(m.n), "merged_bytes": int(out_len),
+            "ms": round(wall * 1e3, 3), "times_ms": [round(t * 1e3, 3) for t in times],
             "status": int(m.status), "api": "hg_compact_dev", "input_records": n_in,
+            "split": f"key range {rank} of {world} (no data movement between GPUs)",
             # newest wins over sorted unique tables: one record per distinct key
-            "parity_count_ok": int(m.n) == int(np.unique(np.concatenate(allkeys)).size)}
+            "parity_count_ok": int(m.n) == n_distinct, "parity_bytes_ok": exact_ok}
     # algorithmic bytes: read the tables, write the compacted table; spans
     # (16 B per input record) and pairs (24 B per output record) each written
-    # and read once.  PMC traffic of the same leg from the committed profile.
+    # and read once.  PMC traffic of the same leg from the committed,
+    # source-hashed profile.
     alg = in_bytes + int(out_len) + 2 * 16 * n_in + 2 * 24 * int(m.n)
     line["algorithmic_bytes"] = alg
     line["achieved_GBps_alg"] = round(world * alg / wall / 1e9, 1)
-    try:
-        with open(os.path.join(ROOT, "profiles", "r2_pmc_compaction.json"), encoding="utf-8") as f:
-            pc = json.load(f)
-        line["traffic"] = pc.get("traffic_bytes_per_call")
-        line["traffic_over_algorithmic"] = (round(line["traffic"] / alg, 3)
-                                            if line["traffic"] else None)
-        line["traffic_source"] = "profiles/r2_pmc_compaction.json"
-    except (OSError, ValueError):
-        line["traffic"] = None
+    line["roofline_frac"] = round(alg / wall / 1e9 / HBM_PEAK_GBS, 4)
+    kern, src = load_leg_pmc(pmc_name, ("hg_decode.hip", "hg_merge.hip", "hg_encode.hip"))
+    traffic = sum(v.get("hbm_read_bytes", 0) + v.get("hbm_write_bytes", 0)
+                  for v in kern.values()) or None
+    line["traffic"] = traffic
+    line["traffic_over_algorithmic"] = round(traffic / alg, 3) if traffic else None
+    line["traffic_source"] = src
     if hosts is not None:
         hout = np.empty(in_bytes, dtype=np.uint8)  # caller-owned output, reused
         eng.compact_host(hosts, out=hout)  # warm-up (staging buffers, workspaces)

@@ -138,6 +138,8 @@ _PROTOS = {
     "hg_multi_compact_host": (ctypes.c_int, [_vp, _u32, _u32, _vp, _vp, _u8p, _u64,
                                              ctypes.POINTER(_u64), _u32, _vp,
                                              ctypes.POINTER(HgMergeResult)]),
+    "hg_multi_compact_dev": (ctypes.c_int, [_vp, _u32, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                            ctypes.POINTER(HgMergeResult)]),
 }
 
 _lib = None

@@ -95,6 +95,7 @@ struct hg_ctx {
     bool bstage_busy = false;
     // multi-context driver (hg_multi.hip): decode results, gathered offsets
     hgi::DevBuf x_res, x_aux;
+    hgi::DevBuf x_arena, x_spans;  // split compaction: this context's key-range slices
 };
 
 namespace hgi {

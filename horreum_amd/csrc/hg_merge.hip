@@ -784,7 +784,7 @@ extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
     const uint64_t ntiles = (n + TILE - 1) / TILE + 1;
     uint64_t b = 2 * ((n * sizeof(MEnt) + 255) & ~255ull);
     b += ((ntiles * 4 + 255) & ~255ull) + 2 * ((ntiles * 8 + 255) & ~255ull);
-    b += ((4 * (uint64_t)ntables + 64) * 8 + 255) & ~255ull;  // device copy of the staging
+    b += ((5 * (uint64_t)ntables + 72) * 8 + 255) & ~255ull;  // device copy of the staging
     b += 256;                                                  // error word
     b += ((uint64_t)ntables * sizeof(ExactHead) + 255) & ~255ull;  // exact-loop heads
     return b;
@@ -796,7 +796,7 @@ extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
 // [table_off | span ptrs | run offsets of every round]: the rounds' offset
 // lists total at most 2 * ntables + 2 * ceil(log2 ntables) + 2 words.
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t ntables) {
-    return (4 * (uint64_t)ntables + 64) * 8;
+    return (5 * (uint64_t)ntables + 72) * 8;
 }
 
 extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint32_t ntables,
@@ -813,17 +813,27 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     uint64_t* h = static_cast<uint64_t*>(staging);
     uint64_t* h_toff = h;
     uint64_t* h_sp = h + ntables;
-    uint64_t* h_roff = h + 2 * (uint64_t)ntables;  // round 0 offsets; later rounds follow
-    uint64_t nr = ntables, total_roff = 0;
+    uint64_t* h_roff = h + 2 * (uint64_t)ntables;  // table run offsets, then every round's
+    uint64_t nr = 0, total_roff = 0, nruns0 = 0;
     for (uint32_t t = 0; t < ntables; ++t) {
         h_toff[t] = table_off[t];
         h_sp[t] = reinterpret_cast<uint64_t>(spans[t]);
     }
-    {  // run offsets per round: round r has nr runs (nr + 1 offsets)
+    {  // [ntables + 1] run offsets of the tables (entry layout; empty runs
+       // included), then per round r its nr runs (nr + 1 offsets).  Round 0
+       // merges the NON-EMPTY runs only: an empty run as the last round's B
+       // side would have sent that round down the odd-run copy path, which
+       // emits no pairs (and publishes no look-back status).
         uint64_t* r = h_roff;
         r[0] = 0;
         for (uint32_t t = 0; t < ntables; ++t) r[t + 1] = r[t] + counts[t];
-        total_roff = nr + 1;
+        uint64_t* r0 = r + ntables + 1;
+        r0[0] = 0;
+        for (uint32_t t = 0; t < ntables; ++t)
+            if (counts[t]) r0[++nr] = r[t + 1];
+        total_roff = (uint64_t)ntables + 1 + nr + 1;
+        nruns0 = nr;  // non-empty runs (round 0)
+        r = r0;
         while (nr > 1) {
             uint64_t* nxt = r + (nr + 1);
             const uint64_t m = (nr + 1) / 2;
@@ -874,15 +884,15 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, e0, err);
     MEnt* cur = e0;
     MEnt* nxt = e1;
-    const uint64_t* roff = a.run_off;
-    uint64_t nruns = ntables;
+    const uint64_t* roff = a.run_off + ntables + 1;  // round 0: the non-empty runs
+    uint64_t nruns = nruns0;
     FinalArgs fa;
     fa.st = lb_status;
     fa.out = d_out;
     fa.cap = cap;
     fa.result = d_result;
     fa.ntiles = (uint32_t)ntiles;
-    if (ntables >= 2 && hipMemsetAsync(lb_status, 0, ntiles * 8, stream) != hipSuccess)
+    if (nruns0 >= 2 && hipMemsetAsync(lb_status, 0, ntiles * 8, stream) != hipSuccess)
         return HG_HIP_FAIL;
     while (nruns > 1) {
         LevelArgs l;
@@ -906,7 +916,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         cur = nxt;
         nxt = t;
     }
-    if (ntables >= 2) {  // pairs and result written by the last round
+    if (nruns0 >= 2) {  // pairs and result written by the last round
         hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)e0,
                            (const unsigned long long*)err, heads, d_out, cap, d_result);
         return HG_LAUNCH_STATUS();

@@ -67,6 +67,39 @@ struct Share {
     std::vector<hg_decode_result> res;
 };
 
+// Tables already on c's device (d_tables[ids[j]]): one batched decode, spans
+// into c->mspans at soff[j], results to the host.
+int decode_share_dev(hg_ctx* c, Share& sh, const uint8_t* const* d_tables, const uint64_t* lens) {
+    const uint32_t k = (uint32_t)sh.ids.size();
+    sh.soff.resize(k);
+    sh.res.assign(k, hg_decode_result{0, HG_OK, 0, 0});
+    if (!k) return HG_OK;
+    if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    uint64_t sb = 0;
+    for (uint32_t j = 0; j < k; ++j) {
+        sh.soff[j] = sb;
+        sb += lens[sh.ids[j]] / 16;
+    }
+    int r = ensure(c, c->mspans, (sb ? sb : 1) * sizeof(hg_span));
+    if (r == HG_OK) r = ensure(c, c->x_res, k * sizeof(hg_decode_result) + 64);
+    if (r != HG_OK) return r;
+    hg_span* spans = static_cast<hg_span*>(c->mspans.p);
+    std::vector<const uint8_t*> dt(k);
+    std::vector<hg_span*> ds(k);
+    std::vector<uint64_t> ln(k), caps(k);
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint32_t t = sh.ids[j];
+        dt[j] = d_tables[t];
+        ds[j] = spans + sh.soff[j];
+        ln[j] = lens[t];
+        caps[j] = lens[t] / 16;
+    }
+    hg_decode_result* dr = static_cast<hg_decode_result*>(c->x_res.p);
+    r = hg_decode_batch_dev_async(c, k, dt.data(), ln.data(), ds.data(), caps.data(), dr);
+    if (r != HG_OK) return r;
+    return sync_d2h(c, sh.res.data(), dr, k * sizeof(hg_decode_result));
+}
+
 int decode_share(hg_ctx* c, Share& sh, const uint8_t* const* h_tables, const uint64_t* lens) {
     const uint32_t k = (uint32_t)sh.ids.size();
     sh.aoff.resize(k);
@@ -377,6 +410,263 @@ int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx, const uint8_t*
 }
 
 // ---- compaction split by key range -----------------------------------------------------
+}  // extern "C"
+
+namespace {
+
+// n bytes from device memory of device src_dev to c's device, on c's stream
+// (a device-to-device copy, or a peer copy over xGMI: a copy, not a collective).
+int copy_dev(hg_ctx* c, void* dst, int src_dev, const void* src, size_t n) {
+    if (!n) return HG_OK;
+    const hipError_t e = src_dev == c->device
+                             ? hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream)
+                             : hipMemcpyPeerAsync(dst, c->device, src, src_dev, n, c->stream);
+    return e == hipSuccess ? HG_OK : HG_HIP_FAIL;
+}
+
+// Direct peer access between every pair of the contexts' devices where the
+// hardware allows it (xGMI); copies work without it too (staged by the runtime).
+void enable_peers(hg_ctx* const* ctxs, uint32_t nctx) {
+    for (uint32_t i = 0; i < nctx; ++i)
+        for (uint32_t j = 0; j < nctx; ++j) {
+            const int a = ctxs[i]->device, b = ctxs[j]->device;
+            if (a == b) continue;
+            int can = 0;
+            if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+            if (hipSetDevice(a) == hipSuccess) (void)hipDeviceEnablePeerAccess(b, 0);  // may already be on
+        }
+    (void)hipGetLastError();
+}
+
+// Decoded tables of every context (owner[t]: the context holding table t at
+// dptr[t]; sh[owner[t]].soff[slot[t]]: its spans in that context's mspans).
+struct Owned {
+    std::vector<Share> sh;
+    std::vector<uint32_t> owner, slot;
+    std::vector<const uint8_t*> dptr;
+};
+
+struct RangeOut {
+    uint64_t n = 0, bytes = 0;
+    uint32_t exact = 0;
+};
+
+// Steps 2-5 of a split compaction over decoded tables: samples -> splitters ->
+// cut points -> every range on its context (slices gathered by device copies,
+// merged, encoded into dsts[g] or, when dsts is null, c->d_out).  separable =
+// false: the input is not range-separable (keys not strictly increasing at a
+// cut or inside a slice); nothing usable was produced.
+int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const uint64_t* lens,
+                  Owned& ow, uint8_t* const* dsts, const uint64_t* caps, std::vector<RangeOut>& O,
+                  bool& separable) {
+    separable = true;
+    // 2. samples of every table's keys (on its owner), then nctx - 1 splitters
+    std::vector<std::vector<KeyRef>> samples(nctx);
+    constexpr uint64_t kSamples = 256;  // per table
+    int r = fan_out(nctx, [&](uint32_t ci) {
+        hg_ctx* c = ctxs[ci];
+        Share& s = ow.sh[ci];
+        if (s.ids.empty()) return (int)HG_OK;
+        if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
+        uint64_t m_tot = 0;
+        for (size_t j = 0; j < s.ids.size(); ++j)
+            if (s.res[j].n_records) m_tot += std::min<uint64_t>(kSamples, s.res[j].n_records);
+        if (!m_tot) return (int)HG_OK;
+        int rr = ensure(c, c->x_aux, m_tot * sizeof(KeyRef));
+        if (rr != HG_OK) return rr;
+        KeyRef* d = static_cast<KeyRef*>(c->x_aux.p);
+        uint64_t at = 0;
+        for (size_t j = 0; j < s.ids.size(); ++j) {
+            const uint64_t n = s.res[j].n_records;
+            if (!n) continue;
+            const uint64_t m = std::min<uint64_t>(kSamples, n);
+            const uint64_t step = (n + m - 1) / m;
+            hipLaunchKernelGGL(sample_keys_kernel, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0,
+                               c->stream, ow.dptr[s.ids[j]],
+                               static_cast<const hg_span*>(c->mspans.p) + s.soff[j], n, step,
+                               s.ids[j], d + at, m);
+            if ((rr = HG_LAUNCH_STATUS()) != HG_OK) return rr;
+            at += m;
+        }
+        samples[ci].resize(m_tot);
+        return sync_d2h(c, samples[ci].data(), d, m_tot * sizeof(KeyRef));
+    });
+    if (r != HG_OK) return r;
+    std::vector<KeyRef> all;
+    for (auto& v : samples) all.insert(all.end(), v.begin(), v.end());
+    std::vector<std::vector<uint8_t>> keys;
+    if (!all.empty()) {
+        std::sort(all.begin(), all.end(), [](const KeyRef& a, const KeyRef& b) {
+            if (a.p0 != b.p0) return a.p0 < b.p0;
+            if (a.p1 != b.p1) return a.p1 < b.p1;
+            return a.klen < b.klen;
+        });
+        for (uint32_t g = 1; g < nctx; ++g) {  // the splitter's exact bytes from its owner
+            const KeyRef& kr = all[all.size() * g / nctx];
+            const uint32_t o = ow.owner[kr.table];
+            hg_ctx* c = ctxs[o];
+            if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+            hg_span sp;
+            const hg_span* dsp = static_cast<const hg_span*>(c->mspans.p) + ow.sh[o].soff[ow.slot[kr.table]];
+            if ((r = sync_d2h(c, &sp, dsp + kr.rec, sizeof sp)) != HG_OK) return r;
+            std::vector<uint8_t> k(sp.klen);
+            if (sp.klen && (r = sync_d2h(c, k.data(), ow.dptr[kr.table] + sp.off + 16, sp.klen)) != HG_OK)
+                return r;
+            keys.push_back(std::move(k));
+        }
+    }
+    std::sort(keys.begin(), keys.end(),
+              [](const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
+                  return host_key_cmp(a, b) < 0;
+              });
+    keys.erase(std::unique(keys.begin(), keys.end(),
+                           [](const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
+                               return host_key_cmp(a, b) == 0;
+                           }),
+               keys.end());
+    const uint32_t nsplit = (uint32_t)keys.size();
+    const uint32_t nrange = nsplit + 1;
+    // 3. cut points of every table (lower bound of each splitter) on its owner
+    std::vector<uint64_t> kofs(nsplit + 1, 0);
+    std::vector<uint32_t> kls(nsplit + 1, 0);
+    std::vector<uint8_t> kbytes;
+    for (uint32_t s = 0; s < nsplit; ++s) {
+        kofs[s] = kbytes.size();
+        kls[s] = (uint32_t)keys[s].size();
+        kbytes.insert(kbytes.end(), keys[s].begin(), keys[s].end());
+    }
+    std::vector<std::vector<uint64_t>> cut_rec(ntables, std::vector<uint64_t>(nrange + 1, 0)),
+        cut_off(ntables, std::vector<uint64_t>(nrange + 1, 0));
+    std::vector<int> cut_ok(ntables, 1);
+    r = fan_out(nctx, [&](uint32_t ci) {
+        hg_ctx* c = ctxs[ci];
+        const Share& s = ow.sh[ci];
+        if (s.ids.empty()) return (int)HG_OK;
+        if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
+        for (size_t j = 0; j < s.ids.size(); ++j) {  // defaults: one range holds the table
+            const uint32_t t = s.ids[j];
+            for (uint32_t g = 1; g <= nrange; ++g) {
+                cut_rec[t][g] = s.res[j].n_records;
+                cut_off[t][g] = lens[t];
+            }
+        }
+        if (!nsplit) return (int)HG_OK;
+        const size_t kb = (kbytes.size() + 255) & ~(size_t)255;
+        const size_t need = kb + 16 * (nsplit + 1) + 256 + 24 * (size_t)(nsplit + 1) * s.ids.size();
+        int rr = ensure(c, c->x_aux, need);
+        if (rr != HG_OK) return rr;
+        char* d = static_cast<char*>(c->x_aux.p);
+        uint8_t* dk = reinterpret_cast<uint8_t*>(d);
+        uint64_t* dko = reinterpret_cast<uint64_t*>(d + kb);
+        uint32_t* dkl = reinterpret_cast<uint32_t*>(d + kb + 8 * (nsplit + 1));
+        uint64_t* dout = reinterpret_cast<uint64_t*>(d + kb + 16 * (nsplit + 1) + 256);
+        // stream-ordered uploads from pageable host vectors (the runtime stages them)
+        if ((!kbytes.empty() && hipMemcpyAsync(dk, kbytes.data(), kbytes.size(),
+                                               hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
+            hipMemcpyAsync(dko, kofs.data(), 8 * (nsplit + 1), hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess ||
+            hipMemcpyAsync(dkl, kls.data(), 4 * nsplit, hipMemcpyHostToDevice, c->stream) !=
+                hipSuccess)
+            return (int)HG_HIP_FAIL;
+        for (size_t j = 0; j < s.ids.size(); ++j) {
+            hipLaunchKernelGGL(split_points_kernel, dim3((nsplit + 63) / 64), dim3(64), 0, c->stream,
+                               ow.dptr[s.ids[j]], lens[s.ids[j]],
+                               static_cast<const hg_span*>(c->mspans.p) + s.soff[j],
+                               s.res[j].n_records, (const uint8_t*)dk, (const uint64_t*)dko,
+                               (const uint32_t*)dkl, nsplit, dout + 3 * (size_t)nsplit * j);
+            if ((rr = HG_LAUNCH_STATUS()) != HG_OK) return rr;
+        }
+        std::vector<uint64_t> h(3 * (size_t)nsplit * s.ids.size());
+        if ((rr = sync_d2h(c, h.data(), dout, 8 * h.size())) != HG_OK) return rr;
+        for (size_t j = 0; j < s.ids.size(); ++j) {
+            const uint32_t t = s.ids[j];
+            for (uint32_t g = 0; g < nsplit; ++g) {
+                cut_rec[t][g + 1] = h[3 * (nsplit * j + g)];
+                cut_off[t][g + 1] = h[3 * (nsplit * j + g) + 1];
+                if (!h[3 * (nsplit * j + g) + 2]) cut_ok[t] = 0;
+            }
+        }
+        return (int)HG_OK;
+    });
+    if (r != HG_OK) return r;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        for (uint32_t g = 0; g < nrange && cut_ok[t]; ++g)  // lower bounds of unordered keys
+            if (cut_rec[t][g] > cut_rec[t][g + 1] || cut_off[t][g] > cut_off[t][g + 1])
+                cut_ok[t] = 0;
+        if (!cut_ok[t]) {
+            separable = false;
+            return HG_OK;
+        }
+    }
+    // 4. range g on context g: its slice of every table copied from the
+    //    table's owner (bytes and decoded spans, device to device: each byte
+    //    crosses once, nothing is uploaded or decoded again), merged, encoded
+    O.assign(nrange, RangeOut{});
+    r = fan_out(nrange, [&](uint32_t g) {
+        hg_ctx* c = ctxs[g];
+        if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
+        std::vector<uint64_t> pos(ntables), toff(ntables), cnt(ntables), sps(ntables);
+        uint64_t ab = 0, nb = 0;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            pos[t] = ab;
+            ab += (cut_off[t][g + 1] - cut_off[t][g] + 255) & ~255ull;
+            cnt[t] = cut_rec[t][g + 1] - cut_rec[t][g];
+            sps[t] = nb;
+            nb += cnt[t];
+        }
+        if (nb == 0) return (int)HG_OK;
+        int rr = ensure(c, c->x_arena, ab + 256);
+        if (rr == HG_OK) rr = ensure(c, c->x_spans, nb * sizeof(hg_span));
+        if (rr == HG_OK) rr = ensure(c, c->mpairs, nb * sizeof(hg_pair));
+        if (rr != HG_OK) return rr;
+        uint8_t* arena = static_cast<uint8_t*>(c->x_arena.p);
+        hg_span* spans = static_cast<hg_span*>(c->x_spans.p);
+        std::vector<const hg_span*> sp(ntables);
+        for (uint32_t t = 0; t < ntables; ++t) {
+            const uint32_t o = ow.owner[t];
+            const hg_span* osp = static_cast<const hg_span*>(ctxs[o]->mspans.p) + ow.sh[o].soff[ow.slot[t]];
+            if ((rr = copy_dev(c, arena + pos[t], ctxs[o]->device, ow.dptr[t] + cut_off[t][g],
+                               cut_off[t][g + 1] - cut_off[t][g])) != HG_OK ||
+                (rr = copy_dev(c, spans + sps[t], ctxs[o]->device, osp + cut_rec[t][g],
+                               cnt[t] * sizeof(hg_span))) != HG_OK)
+                return rr;
+            // spans keep their table-relative offsets: the slice's table offset
+            // absorbs the cut (mod 2^64), so key and value addresses come out right
+            toff[t] = pos[t] - cut_off[t][g];
+            sp[t] = spans + sps[t];
+        }
+        hg_merge_result mr{};
+        rr = hg_merge_dev(c, ntables, arena, ab, toff.data(), sp.data(), cnt.data(),
+                          static_cast<hg_pair*>(c->mpairs.p), nb, &mr);
+        if (rr != HG_OK) return rr;
+        O[g].n = mr.n_out;
+        O[g].exact = mr.table;
+        if (mr.table) return (int)HG_OK;  // not range-separable: decided after the join
+        uint8_t* dst = dsts ? dsts[g] : nullptr;
+        uint64_t cap = dsts ? caps[g] : ab;
+        if (!dsts) {
+            if ((rr = ensure(c, c->d_out, ab ? ab : 1)) != HG_OK) return rr;
+            dst = static_cast<uint8_t*>(c->d_out.p);
+        }
+        if ((rr = ensure(c, c->d_aux, (mr.n_out ? mr.n_out : 1) * sizeof(uint64_t))) != HG_OK)
+            return rr;
+        uint64_t enc = 0;
+        rr = rt_encode_dev(c, arena, static_cast<const hg_pair*>(c->mpairs.p), mr.n_out, dst, cap,
+                           static_cast<uint64_t*>(c->d_aux.p), 0, nullptr, &enc, true);
+        if (rr != HG_OK) return rr;
+        O[g].bytes = enc;
+        return (int)HG_OK;
+    });
+    if (r != HG_OK) return r;
+    for (const RangeOut& o : O)
+        if (o.exact) separable = false;
+    return HG_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
                           const uint8_t* const* h_tables, const uint64_t* lens, uint8_t* h_out,
                           uint64_t cap, uint64_t* out_len, uint32_t block_stride,
@@ -392,209 +682,29 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
     };
     if (nctx == 1 || ntables == 0) return single();
     if (out_len) *out_len = 0;
-    // 1. decode every table on its context (round-robin), sample its keys
-    std::vector<Share> sh = round_robin(nctx, ntables);
-    std::vector<std::vector<KeyRef>> samples(nctx);
-    constexpr uint64_t kSamples = 256;  // per table
-    int r = fan_out(nctx, [&](uint32_t ci) {
-        hg_ctx* c = ctxs[ci];
-        Share& s = sh[ci];
-        int rr = decode_share(c, s, h_tables, lens);
-        if (rr != HG_OK) return rr;
-        uint64_t m_tot = 0;
-        for (size_t j = 0; j < s.ids.size(); ++j)
-            if (s.res[j].kind == HG_OK && s.res[j].n_records)
-                m_tot += std::min<uint64_t>(kSamples, s.res[j].n_records);
-        if (!m_tot) return (int)HG_OK;
-        if ((rr = ensure(c, c->x_aux, m_tot * sizeof(KeyRef))) != HG_OK) return rr;
-        KeyRef* d = static_cast<KeyRef*>(c->x_aux.p);
-        uint64_t at = 0;
-        for (size_t j = 0; j < s.ids.size(); ++j) {
-            const uint64_t n = s.res[j].n_records;
-            if (s.res[j].kind != HG_OK || !n) continue;
-            const uint64_t m = std::min<uint64_t>(kSamples, n);
-            const uint64_t step = (n + m - 1) / m;
-            hipLaunchKernelGGL(sample_keys_kernel, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0,
-                               c->stream, static_cast<const uint8_t*>(c->d_in.p) + s.aoff[j],
-                               static_cast<const hg_span*>(c->mspans.p) + s.soff[j], n, step,
-                               s.ids[j], d + at, m);
-            at += m;
-        }
-        samples[ci].resize(m_tot);
-        return sync_d2h(c, samples[ci].data(), d, m_tot * sizeof(KeyRef));
-    });
+    enable_peers(ctxs, nctx);
+    // 1. every table uploaded once to its context (round-robin) and decoded there
+    Owned ow;
+    ow.sh = round_robin(nctx, ntables);
+    ow.owner.resize(ntables);
+    ow.slot.resize(ntables);
+    ow.dptr.resize(ntables);
+    int r = fan_out(nctx, [&](uint32_t ci) { return decode_share(ctxs[ci], ow.sh[ci], h_tables, lens); });
     if (r != HG_OK) return r;
-    for (uint32_t ci = 0; ci < nctx; ++ci)  // a table that does not decode: one context reports it
-        for (const hg_decode_result& res : sh[ci].res)
-            if (res.kind != HG_OK) return single();
-    // 2. splitters: quantiles of the sampled keys (16-byte prefix order), then
-    //    their exact bytes, sorted exactly and de-duplicated
-    std::vector<KeyRef> all;
-    for (auto& v : samples) all.insert(all.end(), v.begin(), v.end());
-    if (all.empty()) return single();
-    std::sort(all.begin(), all.end(), [](const KeyRef& a, const KeyRef& b) {
-        if (a.p0 != b.p0) return a.p0 < b.p0;
-        if (a.p1 != b.p1) return a.p1 < b.p1;
-        return a.klen < b.klen;
-    });
-    std::vector<uint32_t> owner(ntables), slot(ntables);
     for (uint32_t ci = 0; ci < nctx; ++ci)
-        for (size_t j = 0; j < sh[ci].ids.size(); ++j) {
-            owner[sh[ci].ids[j]] = ci;
-            slot[sh[ci].ids[j]] = (uint32_t)j;
+        for (size_t j = 0; j < ow.sh[ci].ids.size(); ++j) {
+            const uint32_t t = ow.sh[ci].ids[j];
+            if (ow.sh[ci].res[j].kind != HG_OK) return single();  // one context reports it
+            ow.owner[t] = ci;
+            ow.slot[t] = (uint32_t)j;
+            ow.dptr[t] = static_cast<const uint8_t*>(ctxs[ci]->d_in.p) + ow.sh[ci].aoff[j];
         }
-    std::vector<std::vector<uint8_t>> keys;
-    for (uint32_t g = 1; g < nctx; ++g) {
-        const KeyRef& kr = all[all.size() * g / nctx];
-        hg_ctx* c = ctxs[owner[kr.table]];
-        const Share& s = sh[owner[kr.table]];
-        if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
-        hg_span sp;
-        const hg_span* dsp = static_cast<const hg_span*>(c->mspans.p) + s.soff[slot[kr.table]];
-        if ((r = sync_d2h(c, &sp, dsp + kr.rec, sizeof sp)) != HG_OK) return r;
-        std::vector<uint8_t> k(sp.klen);
-        if (sp.klen) memcpy(k.data(), h_tables[kr.table] + sp.off + 16, sp.klen);
-        keys.push_back(std::move(k));
-    }
-    std::sort(keys.begin(), keys.end(),
-              [](const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
-                  return host_key_cmp(a, b) < 0;
-              });
-    keys.erase(std::unique(keys.begin(), keys.end(),
-                           [](const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
-                               return host_key_cmp(a, b) == 0;
-                           }),
-               keys.end());
-    const uint32_t nsplit = (uint32_t)keys.size();
-    const uint32_t nrange = nsplit + 1;
-    // 3. cut points of every table (lower bound of each splitter), on the
-    //    context holding the table; a cut between records that are not
-    //    strictly increasing sends the whole compaction to one context
-    std::vector<uint64_t> kofs(nsplit + 1, 0);
-    std::vector<uint32_t> kls(nsplit);
-    std::vector<uint8_t> kbytes;
-    for (uint32_t s = 0; s < nsplit; ++s) {
-        kofs[s] = kbytes.size();
-        kls[s] = (uint32_t)keys[s].size();
-        kbytes.insert(kbytes.end(), keys[s].begin(), keys[s].end());
-    }
-    // cut[t][g]: record index and byte offset where range g of table t starts
-    std::vector<std::vector<uint64_t>> cut_rec(ntables, std::vector<uint64_t>(nrange + 1, 0)),
-        cut_off(ntables, std::vector<uint64_t>(nrange + 1, 0));
-    std::vector<int> cut_ok(ntables, 1);
-    r = fan_out(nctx, [&](uint32_t ci) {
-        hg_ctx* c = ctxs[ci];
-        const Share& s = sh[ci];
-        if (s.ids.empty()) return (int)HG_OK;
-        if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
-        const size_t kb = (kbytes.size() + 255) & ~(size_t)255;
-        const size_t need = kb + 16 * (nsplit + 1) + 256 + 24 * (size_t)(nsplit + 1) * s.ids.size();
-        int rr = ensure(c, c->x_aux, need);
-        if (rr != HG_OK) return rr;
-        char* d = static_cast<char*>(c->x_aux.p);
-        uint8_t* dk = reinterpret_cast<uint8_t*>(d);
-        uint64_t* dko = reinterpret_cast<uint64_t*>(d + kb);
-        uint32_t* dkl = reinterpret_cast<uint32_t*>(d + kb + 8 * (nsplit + 1));
-        uint64_t* dout = reinterpret_cast<uint64_t*>(d + kb + 16 * (nsplit + 1) + 256);
-        if ((!kbytes.empty() && hipMemcpy(dk, kbytes.data(), kbytes.size(),
-                                          hipMemcpyHostToDevice) != hipSuccess) ||
-            hipMemcpy(dko, kofs.data(), 8 * (nsplit + 1), hipMemcpyHostToDevice) != hipSuccess ||
-            (nsplit && hipMemcpy(dkl, kls.data(), 4 * nsplit, hipMemcpyHostToDevice) != hipSuccess))
-            return (int)HG_HIP_FAIL;
-        for (size_t j = 0; j < s.ids.size(); ++j)
-            hipLaunchKernelGGL(split_points_kernel, dim3((nsplit + 63) / 64), dim3(64), 0, c->stream,
-                               static_cast<const uint8_t*>(c->d_in.p) + s.aoff[j],
-                               lens[s.ids[j]], static_cast<const hg_span*>(c->mspans.p) + s.soff[j],
-                               s.res[j].n_records, (const uint8_t*)dk, (const uint64_t*)dko,
-                               (const uint32_t*)dkl, nsplit, dout + 3 * (size_t)nsplit * j);
-        std::vector<uint64_t> h(3 * (size_t)nsplit * s.ids.size());
-        if ((rr = sync_d2h(c, h.data(), dout, 8 * h.size())) != HG_OK) return rr;
-        for (size_t j = 0; j < s.ids.size(); ++j) {
-            const uint32_t t = s.ids[j];
-            cut_rec[t][nrange] = s.res[j].n_records;
-            cut_off[t][nrange] = lens[t];
-            for (uint32_t g = 0; g < nsplit; ++g) {
-                cut_rec[t][g + 1] = h[3 * (nsplit * j + g)];
-                cut_off[t][g + 1] = h[3 * (nsplit * j + g) + 1];
-                if (!h[3 * (nsplit * j + g) + 2]) cut_ok[t] = 0;
-            }
-        }
-        return (int)HG_OK;
-    });
-    if (r != HG_OK) return r;
-    for (uint32_t t = 0; t < ntables; ++t) {
-        // lower bounds over unordered keys need not be monotone either
-        for (uint32_t g = 0; g < nrange && cut_ok[t]; ++g)
-            if (cut_rec[t][g] > cut_rec[t][g + 1] || cut_off[t][g] > cut_off[t][g + 1])
-                cut_ok[t] = 0;
-        if (!cut_ok[t]) return single();
-    }
-    // 4. every range on its context: its slice of every table -> decode ->
-    //    merge -> encode (+ record offsets for the block index)
-    struct Out {
-        uint64_t n = 0, bytes = 0;
-        uint32_t exact = 0;
-        int32_t kind = HG_OK;
-    };
-    std::vector<Out> O(nrange);
-    const uint32_t nwork = std::min(nctx, nrange);
-    r = fan_out(nwork, [&](uint32_t w) {
-        for (uint32_t g = w; g < nrange; g += nwork) {  // nrange <= nctx: one range each
-            hg_ctx* c = ctxs[w];
-            std::vector<const uint8_t*> pt(ntables);
-            std::vector<uint64_t> pl(ntables);
-            for (uint32_t t = 0; t < ntables; ++t) {
-                pt[t] = h_tables[t] + cut_off[t][g];
-                pl[t] = cut_off[t][g + 1] - cut_off[t][g];
-            }
-            // reuse hg_compact_host's device pipeline, keeping the output on the
-            // device: decode + merge + encode of the slices
-            Share s;
-            for (uint32_t t = 0; t < ntables; ++t) s.ids.push_back(t);
-            int rr = decode_share(c, s, pt.data(), pl.data());
-            if (rr != HG_OK) return rr;
-            uint64_t nm = 0;
-            std::vector<uint64_t> toff(ntables), counts(ntables);
-            std::vector<const hg_span*> sp(ntables);
-            for (uint32_t t = 0; t < ntables; ++t) {
-                if (s.res[t].kind != HG_OK) return (int)HG_ERR_INTERNAL;  // cut off a boundary
-                toff[t] = s.aoff[t];
-                counts[t] = s.res[t].n_records;
-                sp[t] = static_cast<const hg_span*>(c->mspans.p) + s.soff[t];
-                nm += counts[t];
-            }
-            if ((rr = ensure(c, c->mpairs, (nm ? nm : 1) * sizeof(hg_pair))) != HG_OK) return rr;
-            hg_merge_result mr{};
-            uint64_t arena_len = 0;
-            for (uint32_t t = 0; t < ntables; ++t) arena_len = std::max(arena_len, toff[t] + pl[t]);
-            if (nm == 0) {
-                O[g].n = 0;
-                O[g].bytes = 0;
-                continue;
-            }
-            rr = hg_merge_dev(c, ntables, static_cast<const uint8_t*>(c->d_in.p), arena_len,
-                              toff.data(), sp.data(), counts.data(),
-                              static_cast<hg_pair*>(c->mpairs.p), nm, &mr);
-            if (rr != HG_OK) return rr;
-            O[g].n = mr.n_out;
-            O[g].exact = mr.table;
-            if (mr.table) continue;  // not range-separable: decided after the join
-            uint64_t enc = 0;
-            if ((rr = ensure(c, c->d_out, arena_len ? arena_len : 1)) != HG_OK ||
-                (rr = ensure(c, c->d_aux, (mr.n_out ? mr.n_out : 1) * sizeof(uint64_t))) != HG_OK)
-                return rr;
-            rr = rt_encode_dev(c, static_cast<const uint8_t*>(c->d_in.p),
-                               static_cast<const hg_pair*>(c->mpairs.p), mr.n_out,
-                               static_cast<uint8_t*>(c->d_out.p), arena_len,
-                               static_cast<uint64_t*>(c->d_aux.p), 0, nullptr, &enc, true);
-            if (rr != HG_OK) return rr;
-            O[g].bytes = enc;
-        }
-        return (int)HG_OK;
-    });
-    if (r != HG_OK) return r;
-    for (uint32_t g = 0; g < nrange; ++g)
-        if (O[g].exact) return single();
+    std::vector<RangeOut> O;
+    bool separable = true;
+    if ((r = split_compact(ctxs, nctx, ntables, lens, ow, nullptr, nullptr, O, separable)) != HG_OK)
+        return r;
+    if (!separable) return single();
+    const uint32_t nrange = (uint32_t)O.size();
     // 5. concatenate in key order (output offsets from the slice sizes)
     std::vector<uint64_t> OB(nrange + 1, 0), RB(nrange + 1, 0);
     for (uint32_t g = 0; g < nrange; ++g) {
@@ -607,26 +717,23 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
     if (total > cap) return HG_ERR_CAPACITY;
     const uint64_t nb = h_blocks ? (nrec + block_stride - 1) / block_stride : 0;
     std::vector<uint64_t> bpos(nb + 1, 0);
-    r = fan_out(nwork, [&](uint32_t w) {
-        for (uint32_t g = w; g < nrange; g += nwork) {
-            hg_ctx* c = ctxs[w];
-            if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
-            int rr = O[g].bytes ? d2h_pipelined(c, h_out + OB[g], c->d_out.p, O[g].bytes) : HG_OK;
-            if (rr != HG_OK || !nb || !O[g].n) return rr;
-            // block starts inside this slice: global record b * stride
-            const uint64_t first = (block_stride - RB[g] % block_stride) % block_stride;
-            if (first >= O[g].n) continue;
-            const uint64_t m = (O[g].n - first + block_stride - 1) / block_stride;
-            if ((rr = ensure(c, c->x_aux, m * 8)) != HG_OK) return rr;
-            rr = hgk_gather_stride_launch(static_cast<const uint64_t*>(c->d_aux.p), O[g].n, first,
-                                          block_stride, static_cast<uint64_t*>(c->x_aux.p),
-                                          c->stream);
-            std::vector<uint64_t> h(m);
-            if (rr == HG_OK) rr = sync_d2h(c, h.data(), c->x_aux.p, m * 8);
-            if (rr != HG_OK) return rr;
-            const uint64_t b0 = (RB[g] + first) / block_stride;
-            for (uint64_t j = 0; j < m; ++j) bpos[b0 + j] = OB[g] + h[j];
-        }
+    r = fan_out(nrange, [&](uint32_t g) {
+        hg_ctx* c = ctxs[g];
+        if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
+        int rr = O[g].bytes ? d2h_pipelined(c, h_out + OB[g], c->d_out.p, O[g].bytes) : HG_OK;
+        if (rr != HG_OK || !nb || !O[g].n) return rr;
+        // block starts inside this slice: global record b * stride
+        const uint64_t first = (block_stride - RB[g] % block_stride) % block_stride;
+        if (first >= O[g].n) return (int)HG_OK;
+        const uint64_t m = (O[g].n - first + block_stride - 1) / block_stride;
+        if ((rr = ensure(c, c->x_aux, m * 8)) != HG_OK) return rr;
+        rr = hgk_gather_stride_launch(static_cast<const uint64_t*>(c->d_aux.p), O[g].n, first,
+                                      block_stride, static_cast<uint64_t*>(c->x_aux.p), c->stream);
+        std::vector<uint64_t> h(m);
+        if (rr == HG_OK) rr = sync_d2h(c, h.data(), c->x_aux.p, m * 8);
+        if (rr != HG_OK) return rr;
+        const uint64_t b0 = (RB[g] + first) / block_stride;
+        for (uint64_t j = 0; j < m; ++j) bpos[b0 + j] = OB[g] + h[j];
         return (int)HG_OK;
     });
     if (r != HG_OK) return r;
@@ -635,6 +742,83 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
         h_blocks[b].position = bpos[b];
         h_blocks[b].length = (b + 1 < nb ? bpos[b + 1] : total) - bpos[b];
     }
+    return HG_OK;
+}
+
+int hg_multi_compact_dev(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
+                         const uint32_t* owner, const uint8_t* const* d_tables,
+                         const uint64_t* lens, uint8_t* const* d_outs, const uint64_t* caps,
+                         uint64_t* out_lens, uint64_t* out_recs, hg_merge_result* result) {
+    if (!ctxs || !nctx || !d_outs || !caps || !out_lens || !out_recs ||
+        (ntables && (!owner || !d_tables || !lens)))
+        return HG_ERR_INVALID_ARG;
+    for (uint32_t i = 0; i < nctx; ++i)
+        if (!ctxs[i]) return HG_ERR_INVALID_ARG;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        if (owner[t] >= nctx || (lens[t] && !d_tables[t])) return HG_ERR_INVALID_ARG;
+        if (lens[t] >= kMaxLen) return HG_ERR_TOO_LARGE;
+    }
+    for (uint32_t g = 0; g < nctx; ++g) out_lens[g] = out_recs[g] = 0;
+    enable_peers(ctxs, nctx);
+    // everything on context 0: the tables gathered there (device copies), one
+    // hg_compact_dev -- the reference loop for input that is not range-separable
+    auto single = [&]() -> int {
+        hg_ctx* c = ctxs[0];
+        if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+        std::vector<uint64_t> pos(ntables);
+        uint64_t ab = 0;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            pos[t] = ab;
+            ab += (lens[t] + 255) & ~255ull;
+        }
+        int rr = ensure(c, c->x_arena, ab + 256);
+        if (rr != HG_OK) return rr;
+        uint8_t* arena = static_cast<uint8_t*>(c->x_arena.p);
+        for (uint32_t t = 0; t < ntables; ++t)
+            if ((rr = copy_dev(c, arena + pos[t], ctxs[owner[t]]->device, d_tables[t], lens[t])) != HG_OK)
+                return rr;
+        hg_merge_result res{};
+        uint64_t ol = 0;
+        rr = hg_compact_dev(c, ntables, arena, ab, pos.data(), lens, d_outs[0], caps[0], &ol, 0,
+                            nullptr, &res);
+        out_lens[0] = ol;
+        out_recs[0] = res.n_out;
+        if (result) *result = res;
+        return rr;
+    };
+    if (nctx == 1 || ntables == 0) return single();
+    // 1. every context decodes the tables it holds, in place
+    Owned ow;
+    ow.sh.resize(nctx);
+    ow.owner.assign(owner, owner + ntables);
+    ow.slot.resize(ntables);
+    ow.dptr.assign(d_tables, d_tables + ntables);
+    for (uint32_t t = 0; t < ntables; ++t) {
+        ow.slot[t] = (uint32_t)ow.sh[owner[t]].ids.size();
+        ow.sh[owner[t]].ids.push_back(t);
+    }
+    int r = fan_out(nctx, [&](uint32_t ci) {
+        return decode_share_dev(ctxs[ci], ow.sh[ci], d_tables, lens);
+    });
+    if (r != HG_OK) return r;
+    for (uint32_t ci = 0; ci < nctx; ++ci)
+        for (const hg_decode_result& res : ow.sh[ci].res)
+            if (res.kind != HG_OK) return single();  // reports the table's error
+    std::vector<RangeOut> O;
+    bool separable = true;
+    if ((r = split_compact(ctxs, nctx, ntables, lens, ow, d_outs, caps, O, separable)) != HG_OK) {
+        if (r == HG_ERR_CAPACITY)  // a slice did not fit its caller buffer
+            for (uint32_t g = 0; g < O.size(); ++g) out_lens[g] = O[g].bytes;
+        return r;
+    }
+    if (!separable) return single();
+    uint64_t nrec = 0;
+    for (uint32_t g = 0; g < O.size(); ++g) {
+        out_lens[g] = O[g].bytes;
+        out_recs[g] = O[g].n;
+        nrec += O[g].n;
+    }
+    if (result) *result = hg_merge_result{nrec, HG_OK, 0, 0};
     return HG_OK;
 }
 

@@ -155,7 +155,7 @@ int hg_ctx_destroy(hg_ctx* c) {
     if (c->stream) hipStreamSynchronize(c->stream);
     for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
-                      &c->bws, &c->bstage_d, &c->x_res, &c->x_aux})
+                      &c->bws, &c->bstage_d, &c->x_res, &c->x_aux, &c->x_arena, &c->x_spans})
         if (b->p) hipFree(b->p);
     for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage, &c->bstage})
         if (b->p) hipHostFree(b->p);
@@ -178,7 +178,7 @@ int hg_ctx_trim(hg_ctx* c) {
     if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return HG_HIP_FAIL;
     for (DevBuf* b : {&c->ws, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res, &c->bws,
-                      &c->x_aux}) {
+                      &c->x_aux, &c->x_arena, &c->x_spans}) {
         if (b->p) hipFree(b->p);
         b->p = nullptr;
         b->bytes = 0;

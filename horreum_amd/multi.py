@@ -80,6 +80,32 @@ class MultiEngine:
             raise HorreumGpuError(rc, "hg_multi_decode_file_host")
         return DecodeOut(spans[:min(n.value, cap)], n.value, err.kind, err.offset)
 
+    def compact_dev(self, tables, owner, outs):
+        """hg_multi_compact_dev: `tables` are device uint8 tensors (newest
+        first), table t on context owner[t]'s device; slice g of the
+        compacted table goes to outs[g] (a device uint8 tensor on context g's
+        device).  -> (status, [slice bytes], [slice records], HgMergeResult)."""
+        k, n = len(tables), self.n
+        tp = (ctypes.c_void_p * max(k, 1))(*[t.data_ptr() if t.numel() else 0 for t in tables])
+        ln = (ctypes.c_uint64 * max(k, 1))(*[t.numel() for t in tables])
+        ow = (ctypes.c_uint32 * max(k, 1))(*[int(o) for o in owner])
+        op = (ctypes.c_void_p * n)(*[o.data_ptr() for o in outs])
+        cp = (ctypes.c_uint64 * n)(*[o.numel() for o in outs])
+        ol = (ctypes.c_uint64 * n)()
+        orc = (ctypes.c_uint64 * n)()
+        res = HgMergeResult()
+        ctxs, nctx = self._args()
+        rc = self.lib.hg_multi_compact_dev(ctxs, nctx, k, ctypes.cast(ow, ctypes.c_void_p),
+                                           ctypes.cast(tp, ctypes.c_void_p),
+                                           ctypes.cast(ln, ctypes.c_void_p),
+                                           ctypes.cast(op, ctypes.c_void_p),
+                                           ctypes.cast(cp, ctypes.c_void_p),
+                                           ctypes.cast(ol, ctypes.c_void_p),
+                                           ctypes.cast(orc, ctypes.c_void_p), ctypes.byref(res))
+        if rc in (Status.HIP, Status.INVALID_ARG, Status.INTERNAL, Status.TOO_LARGE):
+            raise HorreumGpuError(rc, "hg_multi_compact_dev")
+        return rc, list(ol), list(orc), res
+
     def compact(self, tables, block_stride=0, out=None):
         """hg_multi_compact_host: SSTableManager::compact's byte work split by
         key range over the contexts (`tables` newest first) -> CompactOut."""

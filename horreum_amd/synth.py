@@ -119,17 +119,25 @@ def span_rows(offs, klens, vlens):
     return out
 
 
-def mixed_sst_host(m, krange, vrange, tomb_frac, seed, layout=False):
+def mixed_sst_host(m, krange, vrange, tomb_frac, seed, layout=False, zero_values=False):
     """numpy SSTable of m records, key lengths uniform in krange = (lo, hi)
     and value lengths in vrange (hi exclusive), tomb_frac of the values
-    tombstones, random key/value bytes (tools/decode_variants.py shapes).
+    tombstones, random key/value bytes (tools/decode_variants.py shapes);
+    zero_values: non-zero key bytes and all-zero value bytes (every 16 value
+    bytes then read as an empty record: the decode guesses' worst case).
     layout: also the generated (offsets, klens, vlens)."""
     rng = np.random.default_rng(seed)
     kl = rng.integers(*krange, m)
     vl = rng.integers(*vrange, m)
     vl[rng.random(m) < tomb_frac] = 0
     offs = np.concatenate([[0], np.cumsum(16 + kl + vl)])
-    buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    if zero_values:
+        buf = np.zeros(int(offs[-1]), np.uint8)
+        nk = int(kl.sum())
+        kpos = np.repeat(offs[:-1] + 16, kl) + (np.arange(nk) - np.repeat(np.cumsum(kl) - kl, kl))
+        buf[kpos] = rng.integers(1, 256, nk, dtype=np.uint8)
+    else:
+        buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
     hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(m, 16)
     for i in range(16):
         buf[offs[:-1] + i] = hdr[:, i]

@@ -379,18 +379,37 @@ int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx,
                               hg_span* h_spans, uint64_t cap,
                               uint64_t* n_out, hg_err* err);
 /* SSTableManager::compact (manager.rs:137-159) split by key range: every
- * table is decoded on context i % nctx and its keys sampled; nctx-1
- * splitter keys are taken from the samples; every context decodes, merges
- * and encodes the slice of every table inside its key range; the output is
- * the concatenation in key order with its block index -- byte-identical to
- * hg_compact_host.  Input that is not strictly increasing (found by a
- * slice's merge or at a cut) and tables that do not decode are compacted by
- * hg_compact_host on ctxs[0], which follows the reference loop exactly. */
+ * table is uploaded once, to context i % nctx, decoded there and its keys
+ * sampled; nctx-1 splitter keys are taken from the samples (the reference's
+ * block first keys are every block_stride-th key, index.rs:55-67); context g
+ * gathers the slice of every table inside key range g -- bytes and decoded
+ * spans, copied device to device from the table's context (xGMI peer copies
+ * across GPUs): nothing is uploaded or decoded twice -- merges and encodes
+ * it; the output is the concatenation in key order with its block index --
+ * byte-identical to hg_compact_host.  Input that is not strictly increasing
+ * (found by a slice's merge or at a cut) and tables that do not decode are
+ * compacted by hg_compact_host on ctxs[0], which follows the reference loop
+ * exactly. */
 int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
                           const uint8_t* const* h_tables, const uint64_t* lens,
                           uint8_t* h_out, uint64_t cap, uint64_t* out_len,
                           uint32_t block_stride, hg_block* h_blocks,
                           hg_merge_result* result);
+
+/* The same split compaction on tables already in device memory: table t is
+ * d_tables[t] (lens[t] bytes) on the device of ctxs[owner[t]], decoded there
+ * in place; range g is merged and encoded on ctxs[g] into d_outs[g] (caps[g]
+ * bytes on that context's device; out_lens[g] bytes, out_recs[g] records;
+ * ranges past the splitters found are empty).  The compacted table is the
+ * concatenation of the slices g = 0 .. nctx-1, byte-identical to
+ * hg_compact_dev.  Input that is not range-separable, and tables that do not
+ * decode, are gathered on ctxs[0] and compacted there by hg_compact_dev
+ * (the reference loop; the whole output, or the error, in slice 0: size
+ * caps[0] for it).  result->n_out = records in all slices. */
+int hg_multi_compact_dev(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
+                         const uint32_t* owner, const uint8_t* const* d_tables,
+                         const uint64_t* lens, uint8_t* const* d_outs, const uint64_t* caps,
+                         uint64_t* out_lens, uint64_t* out_recs, hg_merge_result* result);
 
 /* Number of blocks Index::new produces for n pairs: ceil(n / stride). */
 uint64_t hg_block_count(uint64_t n, uint32_t block_stride);

@@ -126,10 +126,15 @@ def test_merge_parity(engine, k, n_universe, frac, seed, long_prefix):
     assert np.array_equal(got, want)
 
 
-def test_merge_with_empty_tables(engine):
-    tables = sorted_tables(4, 2000, 0.5, 9)
-    tables[1] = []
-    tables[3] = []
+@pytest.mark.parametrize("empty", [(1, 3), (2,), (4,), (1,), (0,), (1, 2), (0, 3, 4), (3, 4)])
+def test_merge_with_empty_tables(engine, empty):
+    """Empty tables anywhere in the priority order -- also where the last
+    merge round's second run would be empty (the last table of 3 or 5, two
+    trailing tables): round 0 merges the non-empty runs only."""
+    k = 5 if max(empty) >= 3 else 3 if max(empty) == 2 else 4
+    tables = sorted_tables(k, 2000, 0.5, 9)
+    for t in empty:
+        tables[t] = []
     datas = encode_tables(tables)
     res, got, _, offs = device_merge(engine, datas)
     want, _ = oracle_merge_pairs(datas, offs)

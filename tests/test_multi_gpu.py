@@ -189,6 +189,59 @@ def test_compact_split_unsorted_falls_back(engine, multi2):
     assert np.array_equal(split.blocks, single.blocks)
 
 
+def _compact_dev_case(engine, multi, tables, owner):
+    import torch
+    datas = [d for d in encode_tables(tables)]
+    dev = [torch.from_numpy(d.copy()).to("cuda:0") if d.size else
+           torch.zeros(0, dtype=torch.uint8, device="cuda:0") for d in datas]
+    total = max(sum(d.size for d in datas), 1)
+    outs = [torch.zeros(total, dtype=torch.uint8, device="cuda:0") for _ in range(multi.n)]
+    torch.cuda.synchronize()
+    rc, ol, orc, res = multi.compact_dev(dev, owner, outs)
+    torch.cuda.synchronize()
+    single = engine.compact_host([d.tobytes() for d in datas])
+    got = np.concatenate([outs[g][:ol[g]].cpu().numpy() for g in range(multi.n)])
+    return rc, got, sum(orc), res, single, ol
+
+
+@pytest.mark.parametrize("k,n_universe,frac,seed", [(8, 20000, 0.3, 41), (5, 9000, 0.6, 42)])
+def test_compact_dev_split_by_key_range(engine, multi3, k, n_universe, frac, seed):
+    """hg_multi_compact_dev: tables resident on their owner contexts, key
+    ranges gathered by device copies (no upload, no second decode), merged
+    and encoded per context: the slices' concatenation is byte-identical to
+    the single-context compaction and to the oracle."""
+    tables = sorted_tables(k, n_universe, frac, seed, long_prefix=seed % 2 == 0)
+    rc, got, nrec, res, single, ol = _compact_dev_case(engine, multi3, tables,
+                                                       [t % 3 for t in range(k)])
+    assert rc == 0 and single.status == 0
+    assert nrec == single.n == res.n_out
+    assert np.array_equal(got, single.data)
+    assert sum(1 for x in ol if x) >= 2  # really split
+
+
+def test_compact_dev_empty_slices(engine, multi3):
+    """A table whose keys all fall in the lowest key range (its other slices
+    are empty), an empty table, and owners that hold several tables."""
+    tables = sorted_tables(4, 6000, 0.5, 43)
+    tables.append([(b"\x00" + bytes([i]), b"low%d" % i) for i in range(40)])  # all in range 0
+    tables.append([])
+    rc, got, nrec, res, single, _ = _compact_dev_case(engine, multi3, tables, [0, 0, 1, 2, 1, 2])
+    assert rc == 0 and single.status == 0
+    assert np.array_equal(got, single.data) and nrec == single.n
+
+
+def test_compact_dev_unsorted_falls_back(engine, multi2):
+    """Not range-separable input: gathered on context 0, the reference loop
+    there; the whole output in slice 0."""
+    tables = sorted_tables(4, 3000, 0.5, 44)
+    tables[1] = tables[1][::-1]
+    tables[2] = tables[2] + tables[2][:30]
+    rc, got, nrec, res, single, ol = _compact_dev_case(engine, multi2, tables, [1, 0, 1, 0])
+    assert rc == single.status == 0
+    assert ol[1] == 0
+    assert np.array_equal(got, single.data) and nrec == single.n
+
+
 # ---- contexts driven from separate Python threads ---------------------------------------
 def test_two_contexts_two_threads():
     """include/horreum_gpu.h: distinct contexts may be used from distinct

@@ -19,6 +19,21 @@ from horreum_amd.engine import Engine  # noqa: E402
 from oracle import oracle  # noqa: E402
 
 
+KEYS = {"cfg2 16B/100B 1GiB": "cfg2", "mixed 16B/8..4096B": "mixed4k",
+        "small mixed 0..24B/0..64B": "small", "medium 8..64B/64..512B": "medium",
+        "large 16B/0..16KiB": "large", "huge 16B/0..64KiB": "huge",
+        "midlarge 16B/400..1200B": "midlarge", "zero small 1..23B/0..63B": "zsmall",
+        "zero midlarge 16B/400..1200B": "zmidlarge"}
+
+
+def selected(label, words):
+    """No words: every workload; a word equal to a workload's key (KEYS)
+    selects that one; other words match label substrings."""
+    if not words:
+        return True
+    return any(w == KEYS.get(label) or (w not in KEYS.values() and w in label) for w in words)
+
+
 def workloads(dev):
     n = 8_134_407
     yield "cfg2 16B/100B 1GiB", synth.fixed_sst(n, 16, 100, seed=2, device=dev)
@@ -66,7 +81,7 @@ def main():
     eng = Engine(0)
     eng.set_stream(torch.cuda.current_stream(eng.device))
     for label, sst in workloads(eng.device):
-        if only and not any(w in label for w in only):
+        if not selected(label, only):
             continue
         L = sst.numel()
         cap = L // 16

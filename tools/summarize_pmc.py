@@ -40,10 +40,27 @@ def counters(d):
     return {k: {c: statistics.median(v) for c, v in cs.items()} for k, cs in out.items()}
 
 
+def source_stamp():
+    """sha256 of the kernel sources and the commit the profile was taken at
+    (bench.py compares them with the sources it runs: current_source)."""
+    import hashlib
+    import subprocess
+    sha = {}
+    for f in ("hg_decode.hip", "hg_encode.hip", "hg_merge.hip"):
+        p = os.path.join(ROOT, "horreum_amd", "csrc", f)
+        sha[f] = hashlib.sha256(open(p, "rb").read()).hexdigest() if os.path.exists(p) else None
+    try:
+        commit = subprocess.run(["git", "-C", ROOT, "rev-parse", "--short", "HEAD"],
+                                capture_output=True, text=True).stdout.strip() or None
+    except OSError:
+        commit = None
+    return {"sha256": sha, "commit": commit or os.environ.get("GIT_COMMIT")}
+
+
 def main():
     out_dir, tag, shapes = sys.argv[1], sys.argv[2], sys.argv[3:]
     for s in shapes:
-        res = {"shape": s, "kernels": {}}
+        res = {"shape": s, "kernels": {}, "_source": source_stamp()}
         st = newest(os.path.join(out_dir, f"{tag}_trace_{s}"), "*kernel_stats.csv")
         if st:
             for r in csv.DictReader(open(st)):
