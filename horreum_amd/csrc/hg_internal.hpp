@@ -47,7 +47,10 @@ extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
-                                hg_merge_result*, void*, void*, hipStream_t);
+                                hg_merge_result*, void*, void*, hipStream_t, int defer);
+extern "C" int hgk_merge_epochs(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
+                                const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
+                                hg_merge_result*, hg_merge_result*, void*, void*, hipStream_t);
 
 namespace hgi {
 

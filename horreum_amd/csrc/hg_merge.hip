@@ -34,6 +34,9 @@
 //      reference loop, step by step, by one wave.
 #include <stdlib.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "hg_device.hpp"
 
 namespace hgm {
@@ -280,7 +283,8 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
 // before it by a decoupled look-back over per-tile status words, and writes
 // its pairs at their final positions; the last tile writes the result.
 struct FinalArgs {
-    unsigned long long* st;  // [ntiles] look-back status (zeroed): flag << 62 | live count
+    unsigned long long* st;  // [ntiles] look-back status (zeroed): flag << 62 | live count;
+                             // st[ntiles]: tiles published so far (the spin budget's progress)
     hg_pair* out;
     uint64_t cap;
     hg_merge_result* result;
@@ -290,19 +294,27 @@ constexpr unsigned long long LB_AGG = 1ull << 62, LB_INCL = 2ull << 62;
 constexpr unsigned long long LB_VAL = (1ull << 62) - 1;
 
 // Live entries of the tiles before tile t (wave 0; every lane gets it) and
-// publication of this tile's inclusive count.  A wait that exceeds its budget
-// flags the merge (err) so the exact loop redoes it: never an endless spin.
+// publication of this tile's inclusive count.  The spin budget counts waits
+// without progress anywhere in the grid (tiles publishing, st[ntiles]), so a
+// busy or shared GPU only makes waits long; a wait over the budget means a
+// stalled grid and flags the merge (err) for a redo: never an endless spin.
+__device__ __forceinline__ void final_publish(const FinalArgs& f, uint32_t t, unsigned long long v) {
+    hgk::st_agent(&f.st[t], v);
+    __hip_atomic_fetch_add(&f.st[f.ntiles], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ uint64_t final_lookback(const FinalArgs& f, uint32_t t, uint64_t agg,
                                    unsigned long long* err) {
     const uint32_t lane = threadIdx.x & 63u;
     if (t == 0) {
-        if (lane == 0) hgk::st_agent(&f.st[0], LB_INCL | agg);
+        if (lane == 0) final_publish(f, 0, LB_INCL | agg);
         return 0;
     }
     if (lane == 0) hgk::st_agent(&f.st[t], LB_AGG | agg);
     uint64_t acc = 0;
     int64_t j0 = (int64_t)t - 1;
     uint32_t spins = 0;
+    unsigned long long seen = hgk::ld_agent(&f.st[f.ntiles]);
     for (;;) {
         const int64_t j = j0 - (int64_t)lane;
         unsigned long long w = j >= 0 ? hgk::ld_agent(&f.st[j]) : LB_INCL;
@@ -312,10 +324,14 @@ __device__ uint64_t final_lookback(const FinalArgs& f, uint32_t t, uint64_t agg,
             const int fi = incl ? __ffsll((long long)incl) - 1 : 63;
             rel = fi >= 63 ? ~0ull : ((1ull << (fi + 1)) - 1ull);
             if (!(__ballot((w >> 62) == 0) & rel)) break;
-            if (++spins > (1u << 22)) {
+            const unsigned long long now = hgk::ld_agent(&f.st[f.ntiles]);
+            if (now != seen) {
+                seen = now;
+                spins = 0;
+            } else if (++spins > (1u << 22)) {
                 if (lane == 0) {
                     atomicMin(err, 0ull);
-                    hgk::st_agent(&f.st[t], LB_INCL | agg);
+                    final_publish(f, t, LB_INCL | agg);
                 }
                 return 0;
             }
@@ -326,7 +342,7 @@ __device__ uint64_t final_lookback(const FinalArgs& f, uint32_t t, uint64_t agg,
         if (incl) break;
         j0 -= 64;
     }
-    if (lane == 0) hgk::st_agent(&f.st[t], LB_INCL | (acc + agg));
+    if (lane == 0) final_publish(f, t, LB_INCL | (acc + agg));
     return acc;
 }
 
@@ -698,22 +714,25 @@ __device__ __forceinline__ MEnt shfl_ent(const MEnt& m, int src) {
     return o;
 }
 
+// start (nullable): heads to begin from (table-local indices), n0: records
+// already emitted before them (the epochs below hand over to this loop).
 __global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt* e,
                                                          const unsigned long long* err,
                                                          ExactHead* hs, hg_pair* out, uint64_t cap,
-                                                         hg_merge_result* result) {
+                                                         hg_merge_result* result,
+                                                         const uint64_t* start, uint64_t n0) {
     if (*err == ~0ull) return;  // every table strictly increasing: the rounds did the merge
     const uint32_t lane = threadIdx.x;
     bool any = false;
     for (uint32_t t = lane; t < a.ntables; t += 64) {
         ExactHead h;
-        h.idx = 0;
+        h.idx = start ? start[t] : 0;
         h.cnt = a.run_off[t + 1] - a.run_off[t];
-        if (h.cnt) h.e = e[a.run_off[t]];
-        any |= h.cnt != 0;
+        if (h.idx < h.cnt) h.e = e[a.run_off[t] + h.idx];
+        any |= h.idx < h.cnt;
         hs[t] = h;
     }
-    uint64_t n = 0;
+    uint64_t n = n0;
     if (__ballot(any)) {
         for (;;) {
             // :209-216 the first minimum head over the tables in priority order
@@ -774,161 +793,458 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt
     }
 }
 
+// ---- 6. epochs: the reference loop on tables that are not strictly increasing --------
+// The loop (manager.rs:199-234) is a newest-wins merge of the tables' heads for
+// as long as every table's remaining sequence is strictly increasing.  Cut
+// each table at its DISORDER points (entries whose key is not greater than
+// the one before): from heads h_t the loop equals the merge of the stretches
+// [h_t, f_t) (f_t = the next disorder point) up to and including the key
+// M = min over the tables with a disorder left of K_t[f_t - 1]; right after
+// emitting M the first table reaches its disorder point.  So an epoch merges
+// the sub-runs [h_t, u_t) (u_t = upper bound of M in the stretch; all of it
+// when no disorder is left) with the parallel rounds, appends the pairs, and
+// moves every head to u_t.  Each epoch consumes at least one disorder point.
+
+// Disorder points: entries g (not the first of their table) with key[g] <=
+// key[g - 1], appended to list (count; at most cap kept).
+__global__ __launch_bounds__(THREADS) void merge_disorder_kernel(MergeArgs a, const MEnt* e,
+                                                                 uint64_t* list,
+                                                                 unsigned long long* count,
+                                                                 uint64_t cap) {
+    const uint64_t g = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
+    if (g >= a.n || g == 0) return;
+    const uint32_t t = run_of(a, g);
+    if (g == a.run_off[t]) return;
+    if (key_cmp(a, e[g - 1], e[g]) >= 0) {
+        const unsigned long long i = atomicAdd(count, 1ull);
+        if (i < cap) list[i] = g;
+    }
+}
+
+// One workgroup: M = the smallest key among the candidate entries cand[0, nc)
+// (wave 0), then for every table t the upper bound u[t] of M in its stretch
+// [lo[t], hi[t]) (table-local; entries strictly increasing there).  nc == 0:
+// u = hi.
+__global__ __launch_bounds__(THREADS) void merge_bound_kernel(MergeArgs a, const MEnt* e,
+                                                              const uint64_t* cand, uint32_t nc,
+                                                              const uint64_t* lo, const uint64_t* hi,
+                                                              uint64_t* u) {
+    __shared__ MEnt m;
+    const uint32_t tid = threadIdx.x;
+    if (tid < 64) {
+        bool have = false;
+        MEnt best;
+        best.p0 = best.p1 = 0;
+        best.klen = best.gd = 0;
+        for (uint32_t i = tid; i < nc; i += 64) {
+            const MEnt x = e[cand[i]];
+            if (!have || key_cmp(a, x, best) < 0) {
+                best = x;
+                have = true;
+            }
+        }
+#pragma unroll 1
+        for (int d = 1; d < 64; d <<= 1) {
+            const MEnt o = shfl_ent(best, (int)(tid ^ (uint32_t)d));
+            const bool oh = __shfl((int)have, (int)(tid ^ (uint32_t)d), 64) != 0;
+            if (oh && (!have || key_cmp(a, o, best) < 0)) {
+                best = o;
+                have = true;
+            }
+        }
+        if (tid == 0) m = best;
+    }
+    __syncthreads();
+    for (uint32_t t = tid; t < a.ntables; t += THREADS) {
+        uint64_t l = lo[t], h = hi[t];
+        if (nc) {  // first entry of [l, h) whose key is > M
+            const MEnt* r = e + a.run_off[t];
+            while (l < h) {
+                const uint64_t mid = l + (h - l) / 2;
+                if (key_cmp(a, r[mid], m) <= 0) l = mid + 1;
+                else h = mid;
+            }
+        } else {
+            l = h;
+        }
+        u[t] = l;
+    }
+}
+
+// defer mode: the merge found input that is not strictly increasing and
+// leaves it to the host's epoch driver (no pairs, n_out 0)
+__global__ void merge_flag_kernel(const unsigned long long* err, hg_merge_result* result) {
+    if (*err == ~0ull) return;
+    hg_merge_result r;
+    r.n_out = 0;
+    r.kind = HG_ERR_UNSORTED;
+    r.table = 0;
+    r.index = 0;
+    *result = r;
+}
+
 }  // namespace hgm
 
 // ---- launcher ----------------------------------------------------------------------------
-// Workspace (device): two entry buffers, tile counts/bases, run offsets for
-// every round, table offsets and span pointers, the error word.
-extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
+// Workspace (device): three entry buffers (the entries, then two ping-pong
+// buffers for the rounds: the epochs keep the entries and gather into the
+// other two), tile counts / bases / look-back words, the staging copy (table
+// offsets, span pointers, run offsets of the tables and of every round), the
+// error word, the exact loop's heads, and the epochs' scratch.
+namespace {
+constexpr uint64_t EPOCH_MAX_DISORDER = 4096;  // more disorder points: the serial loop
+inline uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
+struct MergeWs {
+    hgm::MEnt *e0, *e1, *e2;
+    uint32_t* tile_live;
+    uint64_t* tile_base;
+    unsigned long long* lb_status;
+    uint64_t* d_stage;
+    unsigned long long* err;
+    hgm::ExactHead* heads;
+    uint64_t* dis_list;             // disorder points (EPOCH_MAX_DISORDER)
+    unsigned long long* dis_count;  // [0] count, [1] an epoch's error word
+    uint64_t* ep;                   // 4 * ntables: candidates, lo, hi, u
+    uint64_t* ep_roff;              // an epoch's round offsets
+    hg_merge_result* ep_res;
+    uint64_t bytes;
+};
+MergeWs merge_ws(void* d_ws, uint32_t ntables, uint64_t n) {
     using namespace hgm;
     const uint64_t ntiles = (n + TILE - 1) / TILE + 1;
-    uint64_t b = 2 * ((n * sizeof(MEnt) + 255) & ~255ull);
-    b += ((ntiles * 4 + 255) & ~255ull) + 2 * ((ntiles * 8 + 255) & ~255ull);
-    b += ((5 * (uint64_t)ntables + 72) * 8 + 255) & ~255ull;  // device copy of the staging
-    b += 256;                                                  // error word
-    b += ((uint64_t)ntables * sizeof(ExactHead) + 255) & ~255ull;  // exact-loop heads
-    return b;
+    const uint64_t stage = (5 * (uint64_t)ntables + 72) * 8;
+    char* base = static_cast<char*>(d_ws);
+    char* p = base;
+    MergeWs w;
+    w.e0 = reinterpret_cast<MEnt*>(p);
+    p += al256(n * sizeof(MEnt));
+    w.e1 = reinterpret_cast<MEnt*>(p);
+    p += al256(n * sizeof(MEnt));
+    w.e2 = reinterpret_cast<MEnt*>(p);
+    p += al256(n * sizeof(MEnt));
+    w.tile_live = reinterpret_cast<uint32_t*>(p);
+    p += al256(ntiles * 4);
+    w.tile_base = reinterpret_cast<uint64_t*>(p);
+    p += al256(ntiles * 8);
+    w.lb_status = reinterpret_cast<unsigned long long*>(p);
+    p += al256(ntiles * 8);
+    w.d_stage = reinterpret_cast<uint64_t*>(p);
+    p += al256(stage);
+    w.err = reinterpret_cast<unsigned long long*>(p);
+    p += 256;
+    w.heads = reinterpret_cast<ExactHead*>(p);
+    p += al256((uint64_t)ntables * sizeof(ExactHead));
+    w.dis_list = reinterpret_cast<uint64_t*>(p);
+    p += al256(EPOCH_MAX_DISORDER * 8);
+    w.dis_count = reinterpret_cast<unsigned long long*>(p);
+    p += 256;
+    w.ep = reinterpret_cast<uint64_t*>(p);
+    p += al256(4 * (uint64_t)ntables * 8);
+    w.ep_roff = reinterpret_cast<uint64_t*>(p);
+    p += al256(stage);
+    w.ep_res = reinterpret_cast<hg_merge_result*>(p);
+    p += 256;
+    w.bytes = (uint64_t)(p - base);
+    return w;
+}
+
+// Round structure of nr sorted runs with round-0 offsets r[0..nr]: the
+// offsets of every later round follow in place (round r + 1 pairs up the runs
+// of round r).  Returns the words written.
+uint64_t round_offsets(uint64_t* r, uint64_t nr) {
+    uint64_t words = nr + 1;
+    while (nr > 1) {
+        uint64_t* nxt = r + (nr + 1);
+        const uint64_t m = (nr + 1) / 2;
+        for (uint64_t i = 0; i <= m; ++i) nxt[i] = r[std::min(2 * i, nr)];
+        words += m + 1;
+        r = nxt;
+        nr = m;
+    }
+    return words;
+}
+
+// The merge of nr >= 1 sorted runs of `in` (a.n entries; round offsets at
+// roff on the device): log2(nr) rounds, the last emitting the pairs to
+// fa.out / fa.result; one run: its live entries become pairs directly.  The
+// first round reads `in` and writes b1; later rounds alternate b2, b1 (so
+// `in` is never written unless it is b2).
+int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hgm::MEnt* in,
+                  hgm::MEnt* b1, hgm::MEnt* b2, const MergeWs& w, unsigned long long* err,
+                  hgm::FinalArgs fa, hipStream_t stream) {
+    using namespace hgm;
+    const uint64_t ntiles = (a.n + TILE - 1) / TILE;
+    fa.st = w.lb_status;
+    fa.ntiles = (uint32_t)ntiles;
+    if (nr >= 2) {
+        if (hipMemsetAsync(w.lb_status, 0, (ntiles + 1) * 8, stream) != hipSuccess)
+            return HG_HIP_FAIL;
+        MEnt* cur = in;
+        MEnt* nxt = b1;
+        while (nr > 1) {
+            LevelArgs l;
+            l.roff = roff;
+            l.nruns = (uint32_t)nr;
+            // tile_base is free in the rounds: the round's splits
+            const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
+            hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
+                               (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)err);
+            if (nr == 2)  // the last round emits the pairs
+                hipLaunchKernelGGL(merge_level_kernel<true>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
+                                   stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
+                                   err, fa);
+            else
+                hipLaunchKernelGGL(merge_level_kernel<false>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
+                                   stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
+                                   err, fa);
+            roff += nr + 1;
+            nr = (nr + 1) / 2;
+            cur = nxt;
+            nxt = nxt == b1 ? b2 : b1;
+        }
+        return HG_LAUNCH_STATUS();
+    }
+    const MEnt* cur = in;
+    hipLaunchKernelGGL(merge_count_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)cur, w.tile_live);
+    hipLaunchKernelGGL(merge_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)w.tile_live,
+                       (uint32_t)ntiles, w.tile_base, fa.result);
+    hipLaunchKernelGGL(merge_emit_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)cur, (const uint64_t*)w.tile_base, fa.out, fa.cap,
+                       (const unsigned long long*)err);
+    return HG_LAUNCH_STATUS();
+}
+
+int sync_copy(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t s) {
+    if (!n) return HG_OK;
+    if (hipMemcpyAsync(dst, src, n, k, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
+        return HG_HIP_FAIL;
+    return HG_OK;
+}
+}  // namespace
+
+extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
+    return merge_ws(nullptr, ntables, n).bytes;
 }
 
 // Host arrays: table_off[ntables], spans[ntables] (device pointers),
 // counts[ntables].  `staging` is pinned host memory of at least
-// hgk_merge_staging_bytes(ntables) bytes (copied to the device on `stream`).
-// [table_off | span ptrs | run offsets of every round]: the rounds' offset
-// lists total at most 2 * ntables + 2 * ceil(log2 ntables) + 2 words.
+// hgk_merge_staging_bytes(ntables) bytes (copied to the device on `stream`):
+// [table_off | span ptrs | run offsets of the tables | of every round].
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t ntables) {
     return (5 * (uint64_t)ntables + 72) * 8;
 }
 
+// defer: on input that is not strictly increasing, leave the result as
+// HG_ERR_UNSORTED (n_out 0, no pairs) for hgk_merge_epochs instead of running
+// the serial reference loop on the device.
 extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint32_t ntables,
                                 const uint64_t* table_off, const hg_span* const* spans,
                                 const uint64_t* counts, hg_pair* d_out, uint64_t cap,
                                 hg_merge_result* d_result, void* d_ws, void* staging,
-                                hipStream_t stream) {
+                                hipStream_t stream, int defer) {
     using namespace hgm;
     if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
     uint64_t n = 0;
     for (uint32_t t = 0; t < ntables; ++t) n += counts[t];
     if (n >= MAX_ENTRIES) return HG_ERR_TOO_LARGE;  // entries carry a 31-bit global index
-    // host staging: [table_off | span ptrs | run offsets of every round]
     uint64_t* h = static_cast<uint64_t*>(staging);
     uint64_t* h_toff = h;
     uint64_t* h_sp = h + ntables;
-    uint64_t* h_roff = h + 2 * (uint64_t)ntables;  // table run offsets, then every round's
-    uint64_t nr = 0, total_roff = 0, nruns0 = 0;
+    uint64_t* r = h + 2 * (uint64_t)ntables;  // run offsets of the tables (entry layout)
     for (uint32_t t = 0; t < ntables; ++t) {
         h_toff[t] = table_off[t];
         h_sp[t] = reinterpret_cast<uint64_t>(spans[t]);
     }
-    {  // [ntables + 1] run offsets of the tables (entry layout; empty runs
-       // included), then per round r its nr runs (nr + 1 offsets).  Round 0
-       // merges the NON-EMPTY runs only: an empty run as the last round's B
-       // side would have sent that round down the odd-run copy path, which
-       // emits no pairs (and publishes no look-back status).
-        uint64_t* r = h_roff;
-        r[0] = 0;
-        for (uint32_t t = 0; t < ntables; ++t) r[t + 1] = r[t] + counts[t];
-        uint64_t* r0 = r + ntables + 1;
-        r0[0] = 0;
-        for (uint32_t t = 0; t < ntables; ++t)
-            if (counts[t]) r0[++nr] = r[t + 1];
-        total_roff = (uint64_t)ntables + 1 + nr + 1;
-        nruns0 = nr;  // non-empty runs (round 0)
-        r = r0;
-        while (nr > 1) {
-            uint64_t* nxt = r + (nr + 1);
-            const uint64_t m = (nr + 1) / 2;
-            for (uint64_t i = 0; i <= m; ++i) nxt[i] = r[min(2 * i, nr)];
-            total_roff += m + 1;
-            r = nxt;
-            nr = m;
-        }
-    }
-    const uint64_t stage_words = 2 * (uint64_t)ntables + total_roff;
+    r[0] = 0;
+    for (uint32_t t = 0; t < ntables; ++t) r[t + 1] = r[t] + counts[t];
+    // Round 0 merges the NON-EMPTY runs only: an empty run as the last round's
+    // B side would send that round down the odd-run copy path, which emits no
+    // pairs (and publishes no look-back status).
+    uint64_t* r0 = r + ntables + 1;
+    uint64_t nruns0 = 0;
+    r0[0] = 0;
+    for (uint32_t t = 0; t < ntables; ++t)
+        if (counts[t]) r0[++nruns0] = r[t + 1];
+    const uint64_t stage_words = 3 * (uint64_t)ntables + 1 + round_offsets(r0, nruns0);
     if (stage_words * 8 > hgk_merge_staging_bytes(ntables)) return HG_ERR_INTERNAL;
-    char* ws = static_cast<char*>(d_ws);
-    const uint64_t ntiles = (n + TILE - 1) / TILE;
-    MEnt* e0 = reinterpret_cast<MEnt*>(ws);
-    MEnt* e1 = reinterpret_cast<MEnt*>(ws + ((n * sizeof(MEnt) + 255) & ~255ull));
-    char* p = ws + 2 * ((n * sizeof(MEnt) + 255) & ~255ull);
-    uint32_t* tile_live = reinterpret_cast<uint32_t*>(p);
-    p += ((ntiles + 1) * 4 + 255) & ~255ull;
-    uint64_t* tile_base = reinterpret_cast<uint64_t*>(p);
-    p += ((ntiles + 1) * 8 + 255) & ~255ull;
-    unsigned long long* lb_status = reinterpret_cast<unsigned long long*>(p);
-    p += ((ntiles + 1) * 8 + 255) & ~255ull;
-    uint64_t* d_stage = reinterpret_cast<uint64_t*>(p);
-    p += (stage_words * 8 + 255) & ~255ull;
-    unsigned long long* err = reinterpret_cast<unsigned long long*>(p);
-    p += 256;
-    ExactHead* heads = reinterpret_cast<ExactHead*>(p);
-    if (hipMemcpyAsync(d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
+    const MergeWs w = merge_ws(d_ws, ntables, n);
+    if (hipMemcpyAsync(w.d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
         return HG_HIP_FAIL;
-    if (hipMemsetAsync(err, 0xFF, 8, stream) != hipSuccess) return HG_HIP_FAIL;
-
+    if (hipMemsetAsync(w.err, 0xFF, 8, stream) != hipSuccess) return HG_HIP_FAIL;
     MergeArgs a;
     a.arena = d_arena;
     a.arena_len = arena_len;
-    a.table_off = d_stage;
-    a.spans = reinterpret_cast<const hg_span* const*>(d_stage + ntables);
-    a.run_off = d_stage + 2 * (uint64_t)ntables;
+    a.table_off = w.d_stage;
+    a.spans = reinterpret_cast<const hg_span* const*>(w.d_stage + ntables);
+    a.run_off = w.d_stage + 2 * (uint64_t)ntables;
     a.ntables = ntables;
     a.n = n;
     if (n == 0) {
         // every table empty: the reference's unwrap on None (manager.rs:213)
-        hg_merge_result r{0, HG_ERR_EMPTY_MERGE, 0, 0};
-        return hipMemcpyAsync(d_result, &r, sizeof r, hipMemcpyHostToDevice, stream) == hipSuccess
+        hg_merge_result res{0, HG_ERR_EMPTY_MERGE, 0, 0};
+        return hipMemcpyAsync(d_result, &res, sizeof res, hipMemcpyHostToDevice, stream) == hipSuccess
                    ? HG_OK
                    : HG_HIP_FAIL;
     }
     const uint32_t g1 = (uint32_t)((n + THREADS - 1) / THREADS);
-    hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, e0, err);
-    MEnt* cur = e0;
-    MEnt* nxt = e1;
-    const uint64_t* roff = a.run_off + ntables + 1;  // round 0: the non-empty runs
-    uint64_t nruns = nruns0;
+    hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, w.e0, w.err);
     FinalArgs fa;
-    fa.st = lb_status;
     fa.out = d_out;
     fa.cap = cap;
     fa.result = d_result;
-    fa.ntiles = (uint32_t)ntiles;
-    if (nruns0 >= 2 && hipMemsetAsync(lb_status, 0, ntiles * 8, stream) != hipSuccess)
-        return HG_HIP_FAIL;
-    while (nruns > 1) {
-        LevelArgs l;
-        l.roff = roff;
-        l.nruns = (uint32_t)nruns;
-        // tile_base is free until the final count/scan: the round's splits
-        const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
-        hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
-                           (const MEnt*)cur, tile_base, ntiles, (const unsigned long long*)err);
-        if (nruns == 2)  // the last round emits the pairs
-            hipLaunchKernelGGL(merge_level_kernel<true>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
-                               stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)tile_base,
-                               err, fa);
-        else
-            hipLaunchKernelGGL(merge_level_kernel<false>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
-                               stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)tile_base,
-                               err, fa);
-        roff += nruns + 1;
-        nruns = (nruns + 1) / 2;
-        MEnt* t = cur;
-        cur = nxt;
-        nxt = t;
-    }
-    if (nruns0 >= 2) {  // pairs and result written by the last round
-        hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)e0,
-                           (const unsigned long long*)err, heads, d_out, cap, d_result);
-        return HG_LAUNCH_STATUS();
-    }
-    hipLaunchKernelGGL(merge_count_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
-                       (const MEnt*)cur, tile_live);
-    hipLaunchKernelGGL(merge_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)tile_live,
-                       (uint32_t)ntiles, tile_base, d_result);
-    hipLaunchKernelGGL(merge_emit_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
-                       (const MEnt*)cur, (const uint64_t*)tile_base, d_out, cap,
-                       (const unsigned long long*)err);
-    hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)e0,
-                       (const unsigned long long*)err, heads, d_out, cap, d_result);
+    // the rounds ping-pong between e1 and e2, so e0 keeps the entries for the
+    // exact loop / the epochs (the first round reads e0)
+    int rc = launch_rounds(a, a.run_off + ntables + 1, nruns0, w.e0, w.e1, w.e2, w, w.err, fa,
+                           stream);
+    if (rc != HG_OK) return rc;
+    if (defer)
+        hipLaunchKernelGGL(merge_flag_kernel, dim3(1), dim3(1), 0, stream,
+                           (const unsigned long long*)w.err, d_result);
+    else
+        hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)w.e0,
+                           (const unsigned long long*)w.err, w.heads, d_out, cap, d_result,
+                           (const uint64_t*)nullptr, (uint64_t)0);
     return HG_LAUNCH_STATUS();
+}
+
+// After hgk_merge_launch(defer) reported HG_ERR_UNSORTED (same arguments and
+// workspace, stream synchronized): the reference loop by epochs (see
+// merge_bound_kernel): disorder points listed on the device, then per epoch
+// the bound of M and every table's cut (one small kernel, one sync), the
+// sub-runs gathered (device copies) and merged by the parallel rounds, the
+// pairs appended.  More than EPOCH_MAX_DISORDER disorder points: the serial
+// loop.  Synchronous; the result goes to d_result and *h_result.
+extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint32_t ntables,
+                                const uint64_t* table_off, const hg_span* const* spans,
+                                const uint64_t* counts, hg_pair* d_out, uint64_t cap,
+                                hg_merge_result* d_result, hg_merge_result* h_result, void* d_ws,
+                                void* staging, hipStream_t stream) {
+    using namespace hgm;
+    (void)table_off;
+    (void)spans;
+    uint64_t n = 0;
+    std::vector<uint64_t> ro(ntables + 1, 0);
+    for (uint32_t t = 0; t < ntables; ++t) ro[t + 1] = ro[t] + counts[t];
+    n = ro[ntables];
+    const MergeWs w = merge_ws(d_ws, ntables, n);
+    MergeArgs a;  // as hgk_merge_launch staged it (its staging copy is still in place)
+    a.arena = d_arena;
+    a.arena_len = arena_len;
+    a.table_off = w.d_stage;
+    a.spans = reinterpret_cast<const hg_span* const*>(w.d_stage + ntables);
+    a.run_off = w.d_stage + 2 * (uint64_t)ntables;
+    a.ntables = ntables;
+    a.n = n;
+    uint64_t* h = static_cast<uint64_t*>(staging);  // free: the stream is synchronized
+    // 1. disorder points
+    if (hipMemsetAsync(w.dis_count, 0, 8, stream) != hipSuccess) return HG_HIP_FAIL;
+    hipLaunchKernelGGL(merge_disorder_kernel, dim3((uint32_t)((n + THREADS - 1) / THREADS)),
+                       dim3(THREADS), 0, stream, a, (const MEnt*)w.e0, w.dis_list, w.dis_count,
+                       EPOCH_MAX_DISORDER);
+    int rc = HG_LAUNCH_STATUS();
+    if (rc == HG_OK) rc = sync_copy(h, w.dis_count, 8, hipMemcpyDeviceToHost, stream);
+    if (rc != HG_OK) return rc;
+    const uint64_t D = h[0];
+    auto finish = [&](hg_merge_result res) -> int {
+        *h_result = res;
+        return sync_copy(d_result, h_result, sizeof res, hipMemcpyHostToDevice, stream);
+    };
+    // D == 0: the tables are strictly increasing after all -- the error word
+    // came from a look-back wait over its budget (contention), not from the
+    // order check -- and the one epoch below is the whole merge again.
+    // an epoch costs a few launches and host round trips (~0.1-0.2 ms), the
+    // serial loop ~1-2 us per record: many disorder points -> the serial loop
+    if (D > EPOCH_MAX_DISORDER || D > n / 128 + 1 || getenv("HG_MERGE_SERIAL")) {  // (A/B: serial)
+        hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)w.e0,
+                           (const unsigned long long*)w.err, w.heads, d_out, cap, d_result,
+                           (const uint64_t*)nullptr, (uint64_t)0);
+        if ((rc = HG_LAUNCH_STATUS()) != HG_OK) return rc;
+        return sync_copy(h_result, d_result, sizeof(hg_merge_result), hipMemcpyDeviceToHost, stream);
+    }
+    std::vector<uint64_t> dl(D);
+    if ((rc = sync_copy(dl.data(), w.dis_list, D * 8, hipMemcpyDeviceToHost, stream)) != HG_OK)
+        return rc;
+    std::sort(dl.begin(), dl.end());
+    std::vector<std::vector<uint64_t>> dis(ntables);  // table-local disorder points, ascending
+    for (uint64_t g : dl) {
+        const uint32_t t = (uint32_t)(std::upper_bound(ro.begin(), ro.end(), g) - ro.begin()) - 1;
+        dis[t].push_back(g - ro[t]);
+    }
+    // 2. epochs
+    std::vector<uint64_t> hd(ntables, 0), f(ntables), u(ntables);
+    uint64_t N = 0, epochs = 0;
+    uint64_t* dcand = w.ep;
+    uint64_t* dlo = w.ep + ntables;
+    uint64_t* dhi = w.ep + 2 * (uint64_t)ntables;
+    uint64_t* du = w.ep + 3 * (uint64_t)ntables;
+    unsigned long long* ep_err = w.dis_count + 1;
+    for (;;) {
+        uint32_t nc = 0;
+        bool left = false;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            const uint64_t cnt = counts[t];
+            auto it = std::upper_bound(dis[t].begin(), dis[t].end(), hd[t]);
+            f[t] = it == dis[t].end() ? cnt : *it;
+            left |= hd[t] < cnt;
+            if (f[t] < cnt) h[nc++] = ro[t] + f[t] - 1;  // candidates for M
+        }
+        if (!left) break;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            h[ntables + t] = hd[t];
+            h[2 * (uint64_t)ntables + t] = f[t];
+        }
+        if (hipMemcpyAsync(w.ep, h, 3 * (uint64_t)ntables * 8, hipMemcpyHostToDevice, stream) !=
+            hipSuccess)
+            return HG_HIP_FAIL;
+        hipLaunchKernelGGL(merge_bound_kernel, dim3(1), dim3(THREADS), 0, stream, a,
+                           (const MEnt*)w.e0, (const uint64_t*)dcand, nc, (const uint64_t*)dlo,
+                           (const uint64_t*)dhi, du);
+        if ((rc = HG_LAUNCH_STATUS()) != HG_OK) return rc;
+        if ((rc = sync_copy(u.data(), du, (uint64_t)ntables * 8, hipMemcpyDeviceToHost, stream)) !=
+            HG_OK)
+            return rc;
+        // the epoch's sub-runs [hd, u), gathered in priority order
+        uint64_t ne = 0, nre = 0;
+        h[0] = 0;
+        for (uint32_t t = 0; t < ntables; ++t) {
+            const uint64_t len = u[t] - hd[t];
+            if (u[t] < hd[t] || u[t] > f[t]) return HG_ERR_INTERNAL;
+            if (!len) continue;
+            if (hipMemcpyAsync(w.e1 + ne, w.e0 + ro[t] + hd[t], len * sizeof(MEnt),
+                               hipMemcpyDeviceToDevice, stream) != hipSuccess)
+                return HG_HIP_FAIL;
+            ne += len;
+            h[++nre] = ne;
+        }
+        if (!ne) return HG_ERR_INTERNAL;  // every epoch consumes a disorder point
+        const uint64_t words = round_offsets(h, nre);
+        if (words * 8 > hgk_merge_staging_bytes(ntables)) return HG_ERR_INTERNAL;
+        if (hipMemcpyAsync(w.ep_roff, h, words * 8, hipMemcpyHostToDevice, stream) != hipSuccess ||
+            hipMemsetAsync(ep_err, 0xFF, 8, stream) != hipSuccess)
+            return HG_HIP_FAIL;
+        MergeArgs ae = a;
+        ae.n = ne;
+        FinalArgs fa;
+        fa.out = d_out + std::min(N, cap);
+        fa.cap = cap > N ? cap - N : 0;
+        fa.result = w.ep_res;
+        if ((rc = launch_rounds(ae, w.ep_roff, nre, w.e1, w.e2, w.e1, w, ep_err, fa, stream)) !=
+            HG_OK)
+            return rc;
+        struct {
+            hg_merge_result r;
+            unsigned long long e;
+        } er;
+        if ((rc = sync_copy(&er.r, w.ep_res, sizeof er.r, hipMemcpyDeviceToHost, stream)) != HG_OK ||
+            (rc = sync_copy(&er.e, ep_err, 8, hipMemcpyDeviceToHost, stream)) != HG_OK)
+            return rc;
+        if (er.e != ~0ull || er.r.kind != HG_OK) return HG_ERR_INTERNAL;
+        N += er.r.n_out;
+        for (uint32_t t = 0; t < ntables; ++t) hd[t] = u[t];
+        ++epochs;
+    }
+    // table = 2: the epochs produced the output (index = their number); D == 0
+    // (a look-back over its budget, sorted input): the one epoch was a plain redo
+    return finish(hg_merge_result{N, HG_OK, D ? 2u : 0u, D ? epochs : 0});
 }

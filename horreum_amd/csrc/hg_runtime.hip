@@ -910,10 +910,16 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
 }
 
 // ---- merge (compaction) ------------------------------------------------------------
-int hg_merge_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
-                       const uint64_t* table_off, const hg_span* const* d_spans,
-                       const uint64_t* counts, hg_pair* d_out, uint64_t cap,
-                       hg_merge_result* d_result) {
+}  // extern "C"
+
+namespace {
+// hg_merge_dev_async with the choice of what happens on input that is not
+// strictly increasing: defer = 0 runs the serial reference loop on the device
+// (the async API's contract); defer = 1 leaves HG_ERR_UNSORTED for
+// merge_epochs (the synchronous paths).
+int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
+                const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
+                hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, int defer) {
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
@@ -933,20 +939,41 @@ int hg_merge_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint
             if (counts[t] && !d_spans[t]) return HG_ERR_INVALID_ARG;
             n += counts[t];
         }
-        int r = ensure(c, c->mws, hgk_merge_workspace_bytes(ntables, n) +
-                                      hgk_merge_staging_bytes(ntables) + 4096);
+        int r = ensure(c, c->mws, hgk_merge_workspace_bytes(ntables, n) + 4096);
         if (r != HG_OK) return r;
         // the previous call's argument copy must have left the pinned staging
         if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_HIP_FAIL;
         if (ensure_pin(c->mstage, hgk_merge_staging_bytes(ntables) + 4096) != HG_OK)
             return HG_HIP_FAIL;
         r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
-                             d_result, c->mws.p, c->mstage.p, c->stream);
+                             d_result, c->mws.p, c->mstage.p, c->stream, defer);
         if (r != HG_OK) return r;
     }
     if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
     c->mstage_busy = true;
     return HG_OK;
+}
+
+// After merge_async(defer) reported HG_ERR_UNSORTED (stream synchronized):
+// the reference loop by epochs (hgk_merge_epochs) on the same workspace.
+int merge_epochs(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
+                 const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
+                 hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, hg_merge_result* res) {
+    if (c->mstage_busy && hipEventSynchronize(c->mstage_ev) != hipSuccess) return HG_HIP_FAIL;
+    c->mstage_busy = false;
+    return hgk_merge_epochs(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
+                            d_result, res, c->mws.p, c->mstage.p, c->stream);
+}
+}  // namespace
+
+extern "C" {
+
+int hg_merge_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
+                       const uint64_t* table_off, const hg_span* const* d_spans,
+                       const uint64_t* counts, hg_pair* d_out, uint64_t cap,
+                       hg_merge_result* d_result) {
+    return merge_async(c, ntables, d_arena, arena_len, table_off, d_spans, counts, d_out, cap,
+                       d_result, 0);
 }
 
 int hg_merge_dev(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
@@ -955,14 +982,18 @@ int hg_merge_dev(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t a
     if (!c) return HG_ERR_INVALID_ARG;
     if (ensure(c, c->mres, 64) != HG_OK) return HG_HIP_FAIL;
     hg_merge_result* dres_m = static_cast<hg_merge_result*>(c->mres.p);
-    int r = hg_merge_dev_async(c, ntables, d_arena, arena_len, table_off, d_spans, counts, d_out,
-                               cap, dres_m);
+    int r = merge_async(c, ntables, d_arena, arena_len, table_off, d_spans, counts, d_out, cap,
+                        dres_m, 1);
     if (r != HG_OK) return r;
     if (hipMemcpyAsync(c->hres.p, dres_m, sizeof(hg_merge_result), hipMemcpyDeviceToHost,
                        c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return HG_HIP_FAIL;
-    const hg_merge_result res = *static_cast<hg_merge_result*>(c->hres.p);
+    hg_merge_result res = *static_cast<hg_merge_result*>(c->hres.p);
+    if (res.kind == HG_ERR_UNSORTED &&
+        (r = merge_epochs(c, ntables, d_arena, arena_len, table_off, d_spans, counts, d_out, cap,
+                          dres_m, &res)) != HG_OK)
+        return r;
     if (result) *result = res;
     if (res.kind != HG_OK) return res.kind;
     return res.n_out > cap ? HG_ERR_CAPACITY : HG_OK;
@@ -1031,24 +1062,39 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     hg_encode_result* dres_e =
         reinterpret_cast<hg_encode_result*>(static_cast<char*>(c->mres.p) + 64);
     hg_pair* pairs = static_cast<hg_pair*>(c->mpairs.p);
-    r = hg_merge_dev_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm,
-                           dres_m);
+    // tables that are not strictly increasing: the merge reports HG_ERR_UNSORTED
+    // with no output (the encode then writes nothing) and the epochs below run
+    // the reference loop; otherwise merge and encode run back to back
+    r = merge_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm, dres_m,
+                    1);
     if (r != HG_OK) return r;
-    if (nm == 0) {
-        if (hipMemsetAsync(dres_e, 0, sizeof(hg_encode_result), c->stream) != hipSuccess)
-            return HG_HIP_FAIL;
-    } else {
-        r = hgk_encode_launch_ex(arena, pairs, nm, &dres_m->n_out, true, d_out, cap,
-                                 d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, 0,
-                                 block_stride, d_blk, dres_e,
-                                 reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
-        if (r != HG_OK) return r;
-    }
+    auto encode = [&]() -> int {
+        if (nm == 0)
+            return hipMemsetAsync(dres_e, 0, sizeof(hg_encode_result), c->stream) == hipSuccess
+                       ? HG_OK
+                       : HG_HIP_FAIL;
+        return hgk_encode_launch_ex(arena, pairs, nm, &dres_m->n_out, true, d_out, cap,
+                                    d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, 0,
+                                    block_stride, d_blk, dres_e,
+                                    reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+    };
+    if ((r = encode()) != HG_OK) return r;
     char* h = static_cast<char*>(c->hres.p);
     if (hipMemcpyAsync(h, c->mres.p, 128, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         return HG_HIP_FAIL;
     *res = *reinterpret_cast<const hg_merge_result*>(h);
+    if (res->kind == HG_ERR_UNSORTED) {
+        hg_merge_result er2{};
+        if ((r = merge_epochs(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs,
+                              nm, dres_m, &er2)) != HG_OK ||
+            (r = encode()) != HG_OK)
+            return r;
+        if (hipMemcpyAsync(h, c->mres.p, 128, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            return HG_HIP_FAIL;
+        *res = *reinterpret_cast<const hg_merge_result*>(h);
+    }
     const hg_encode_result er = *reinterpret_cast<const hg_encode_result*>(h + 64);
     if (res->kind != HG_OK) return res->kind;
     if (res->n_out > nm) return HG_ERR_INTERNAL;  // the merge never grows the record count

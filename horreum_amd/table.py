@@ -26,6 +26,8 @@ Quirks kept from the reference:
 """
 import mmap
 import os
+import weakref
+from collections import OrderedDict
 
 import numpy as np
 
@@ -148,6 +150,47 @@ class PersistedFile:
         os.remove(self.path)
 
 
+class _ResidentLRU:
+    """Tables kept resident in HBM for batched lookups, per engine, least
+    recently used first: once their bytes (table + spans + key index) pass
+    the budget (HG_RESIDENT_BYTES, default 32 GiB) the oldest are released
+    (their next get_many uploads them again)."""
+
+    def __init__(self, budget):
+        self.budget = budget
+        self.items = OrderedDict()  # id(table) -> (weakref(table), bytes)
+        self.total = 0
+
+    def touch(self, table, nbytes):
+        key = id(table)
+        if key in self.items:
+            self.items.move_to_end(key)
+            return
+        self.items[key] = (weakref.ref(table), nbytes)
+        self.total += nbytes
+        while self.total > self.budget and len(self.items) > 1:
+            _, (ref, b) = self.items.popitem(last=False)
+            self.total -= b
+            old = ref()
+            if old is not None:
+                old._resident = None
+
+    def drop(self, table):
+        item = self.items.pop(id(table), None)
+        if item is not None:
+            self.total -= item[1]
+
+
+_LRUS = weakref.WeakKeyDictionary()  # engine -> _ResidentLRU
+
+
+def _lru(engine):
+    lru = _LRUS.get(engine)
+    if lru is None:
+        lru = _LRUS[engine] = _ResidentLRU(int(os.environ.get("HG_RESIDENT_BYTES", 32 << 30)))
+    return lru
+
+
 class SSTable:
     """src/sstable/table.rs:7-90."""
 
@@ -203,15 +246,26 @@ class SSTable:
 
     def resident(self, engine=None):
         """The table in HBM for batched lookups: uploaded, decoded and
-        indexed by the first call, reused by every later one."""
+        indexed by the first call, reused by later ones while it stays within
+        the engine's resident budget (least recently used tables go first)."""
         from .engine import default_engine
         eng = engine or default_engine()
         if self._resident is None or self._resident[0] is not eng:
-            rt = eng.resident_table(self.file.read_bytes(eng))
+            data = self.file.read_bytes(eng)
+            rt = eng.resident_table(data)
             if rt.kind != 0:
                 raise DecodeError(rt.kind, rt.offset, rt.n)
             self._resident = (eng, rt)
+            _lru(eng).touch(self, len(data) + 48 * int(rt.n))  # bytes + spans + key index
+        else:
+            _lru(eng).touch(self, 0)
         return self._resident[1]
+
+    def release(self):
+        """Free the table's resident HBM state (it is rebuilt on demand)."""
+        if self._resident is not None:
+            _lru(self._resident[0]).drop(self)
+        self._resident = None
 
     def get_many(self, keys, engine=None):
         """SSTable::get for a batch of keys in one device launch against the
@@ -243,5 +297,5 @@ class SSTable:
         return self.size
 
     def delete(self):
-        self._resident = None
+        self.release()
         self.file.delete()

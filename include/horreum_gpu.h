@@ -116,9 +116,12 @@ typedef struct hg_encode_result {
 
 /* Result of a merge / compaction.  kind: HG_OK, HG_ERR_CAPACITY,
  * HG_ERR_EMPTY_MERGE, or a decode error of an input table (table, index =
- * failing byte offset).  On HG_OK from hg_merge_dev*, table = 1 when the
- * input was not strictly increasing and the serial reference loop produced
- * the output, else 0. */
+ * failing byte offset).  On HG_OK, table says how the reference loop
+ * (manager.rs:199-234) was followed: 0 the parallel newest-wins merge
+ * (every table strictly increasing); for input that is not, 1 the serial
+ * loop on the device (hg_merge_dev_async, or many disorder points), 2 epochs
+ * of the parallel merge cut at the tables' disorder points (the synchronous
+ * entry points; index = the number of epochs). */
 typedef struct hg_merge_result {
     uint64_t n_out;  /* merged records (tombstones included) */
     int32_t kind;

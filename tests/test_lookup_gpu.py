@@ -159,3 +159,30 @@ def test_get_many_equals_get_on_duplicates(engine, tmp_path, stride):
         assert (g is None) == (want is None), k
         if want is not None:
             assert g == pairs[want], k
+
+
+def test_resident_tables_lru_budget(engine, tmp_path):
+    """Resident lookup state is bounded per engine: past the byte budget the
+    least recently used table is released (and rebuilt on its next batch);
+    results never change."""
+    from horreum_amd import table as tmod
+    lru = tmod._lru(engine)
+    old_budget = lru.budget
+    tabs = []
+    try:
+        for i in range(3):
+            pairs = [InternalPair(b"k%05d" % j + bytes([i]), b"v" * (j % 50 + 1)) for j in range(3000)]
+            tabs.append((SSTable.new(PersistedFile.new(tmp_path / f"t{i}", pairs, engine), pairs,
+                                     0, 10, engine), pairs))
+        one = tabs[0][0].file.read_bytes(engine).size + 48 * 3000
+        lru.budget = int(one * 1.5)  # room for one table
+        for t, pairs in tabs + tabs[:1]:
+            keys = [p.key for p in pairs[::97]] + [b"absent"]
+            assert t.get_many(keys, engine) == [t.get(k, engine) for k in keys]
+        assert tabs[0][0]._resident is not None       # the last one used
+        assert tabs[1][0]._resident is None and tabs[2][0]._resident is None
+        assert lru.total <= lru.budget
+    finally:
+        lru.budget = old_budget
+        for t, _ in tabs:
+            t.release()

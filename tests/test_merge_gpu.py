@@ -334,7 +334,7 @@ def test_compact_dev(engine, stride, unsorted):
     blocks = engine.empty(24 * (wn // stride + 2)) if stride else None
     c = engine.compact_dev(arena, offs, [d.size for d in datas], out, stride, blocks)
     assert c.status == 0 and c.kind == 0 and c.n == wn
-    assert c.table == (1 if unsorted else 0)
+    assert c.table in ((1, 2) if unsorted else (0,))
     assert np.array_equal(c.data.cpu().numpy(), want)
     if stride:
         assert np.array_equal(c.blocks.cpu().numpy().view(wblocks.dtype), wblocks)
@@ -345,3 +345,92 @@ def test_compact_dev(engine, stride, unsorted):
     # a table that does not decode: its index and the decoder's error
     c3 = engine.compact_dev(arena, offs, [d.size for d in datas[:-1]] + [datas[-1].size - 3], out)
     assert c3.kind in (1, 2) and c3.status == c3.kind and c3.table == len(datas) - 1
+
+
+# ---- epochs: the reference loop cut at the tables' disorder points -----------------------
+def _keyed_tables(sizes, seed, universe=None):
+    """Sorted unique 8-byte big-endian keys per table (value = table id)."""
+    rng = np.random.default_rng(seed)
+    universe = universe or 2 * max(sizes)
+    uni = np.unique(rng.integers(0, 1 << 40, size=universe, dtype=np.uint64))
+    out = []
+    for t, s in enumerate(sizes):
+        keys = np.sort(rng.choice(uni, size=min(s, uni.size), replace=False))
+        out.append(keys)
+    return out
+
+
+def _encode_keyed(keys, t, dup_at=None, swap_at=None):
+    keys = list(keys)
+    if dup_at is not None:
+        keys.insert(dup_at, keys[dup_at])  # a duplicate key: a disorder point
+    if swap_at is not None:
+        keys[swap_at], keys[swap_at + 1] = keys[swap_at + 1], keys[swap_at]
+    keys = np.array(keys, dtype=np.uint64)
+    n = keys.size
+    kb = keys.astype(">u8").view(np.uint8).reshape(-1, 8)
+    arena = np.concatenate([kb, np.full((n, 8), t, np.uint8)], axis=1).reshape(-1)
+    pairs = np.zeros(n, dtype=oracle.PAIR_DTYPE)
+    pairs["key_off"] = np.arange(n) * 16
+    pairs["val_off"] = np.arange(n) * 16 + 8
+    pairs["klen"] = 8
+    pairs["vlen"] = 8
+    return oracle.encode(arena, pairs)[0]
+
+
+def _timed_merge(engine, datas, reps=3):
+    import time
+    import torch
+    device_merge(engine, datas)
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res, got, _, offs = device_merge(engine, datas)
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[reps // 2], res, got, offs
+
+
+def test_merge_epochs_one_late_duplicate(engine):
+    """One duplicate key late in a 1 M-record table among 4 tables: the
+    reference loop by 2 epochs of the parallel merge (not the serial loop),
+    record for record the oracle's, and within 10x of the sorted merge's
+    time (both timed around the same decode + merge helper)."""
+    keys = _keyed_tables([1_000_000, 300_000, 300_000, 300_000], seed=51)
+    sorted_d = [_encode_keyed(k, t) for t, k in enumerate(keys)]
+    dup_d = list(sorted_d)
+    dup_d[0] = _encode_keyed(keys[0], 0, dup_at=900_000)
+    t_sorted, res0, _, _ = _timed_merge(engine, sorted_d)
+    t_dup, res, got, offs = _timed_merge(engine, dup_d)
+    want, rc = oracle_merge_pairs(dup_d, offs)
+    assert rc == 0 and res.status == 0 and res.n == want.size
+    assert np.array_equal(got, want)
+    assert (res.table, res.index) == (2, 2)
+    assert t_dup < 10 * t_sorted + 0.05, (t_dup, t_sorted)
+
+
+def test_merge_epochs_disorder_in_every_table(engine):
+    """One inversion (adjacent swap) in each of 6 tables: 7 epochs."""
+    sizes = [120_000, 50_000, 80_000, 20_000, 60_000, 90_000]
+    keys = _keyed_tables(sizes, seed=52, universe=400_000)
+    rng = np.random.default_rng(53)
+    datas = [_encode_keyed(k, t, swap_at=int(rng.integers(1, k.size - 2)))
+             for t, k in enumerate(keys)]
+    res, got, _, offs = device_merge(engine, datas)
+    want, rc = oracle_merge_pairs(datas, offs)
+    assert rc == 0 and res.status == 0 and res.n == want.size
+    assert np.array_equal(got, want)
+    assert res.table == 2 and res.index >= 2
+
+
+def test_merge_epochs_then_compact(engine):
+    """The epochs inside hg_compact_host (decode -> merge -> encode): output
+    == serialize_flatten of the oracle's compact_inner output."""
+    keys = _keyed_tables([40_000, 30_000, 20_000], seed=54)
+    datas = [_encode_keyed(keys[0], 0, dup_at=30_000), _encode_keyed(keys[1], 1, swap_at=100),
+             _encode_keyed(keys[2], 2)]
+    out = engine.compact_host([d.tobytes() for d in datas], block_stride=7)
+    want, wblocks, wn = oracle.compacted_table(datas, block_stride=7)
+    assert out.status == 0 and out.n == wn and out.table == 2
+    assert np.array_equal(out.data, want)
+    assert np.array_equal(out.blocks, wblocks)
