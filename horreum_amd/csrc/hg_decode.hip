@@ -120,6 +120,12 @@ struct DecodeArgs {
     struct SpecBatch* sbatch;
     const struct SpecPiece* spiece;
     struct SpecPiece* spiece_rw;     // the same records (splice_repair rewrites its batch's)
+    // compaction mode (kpre_tag != 0): stride pieces of the pre-pass leave the
+    // key prefix of each record (key_prefix_be) in their unused span-scratch
+    // slot and set their piece tag (piece_tags) to kpre_tag; the general
+    // engine clears the tags of the pieces whose scratch it takes (hg_merge.hip's
+    // entry builder reads a prefix only under a current tag, else the key)
+    uint32_t kpre_tag;
     struct DecodeCtl* ctl;
     unsigned long long* gsum;    // records per group of SPEC_GROUP pre-pass batches
     unsigned long long* link;    // per adjacent pre-pass batch pair: arrivals | exit - x0
@@ -127,6 +133,9 @@ struct DecodeArgs {
     uint32_t sbp;                // pieces per pre-pass batch (SPEC_BP_MIN..SPEC_BP)
     uint32_t q;                  // pre-pass batches per general batch (bp / sbp)
 };
+
+// The piece tags (decode_layout: right after the piece records).
+__device__ __forceinline__ uint32_t* piece_tags(const DecodeArgs& a);
 
 // Bytes of the piece at `base` where records may start: up to `stop` (the
 // piece's bytes up to `len` are still staged and readable).
@@ -158,11 +167,11 @@ constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
     return nspec - c->bad_rev;       // bad_rev 0 (nothing bad) -> nspec
 }
-struct SpecPiece {                // one per piece of an ok pre-pass batch
-    uint64_t x, R;
-    uint32_t kl, vl, count, pad;  // pad: SP_STRIDE, or SP_HOP (count spans in scratch)
-};
-enum : uint32_t { SP_STRIDE = 0, SP_HOP = 1 };
+static_assert(PIECE_BYTES == 16384 && PIECE_RECS == 1024, "piece geometry (hg_device.hpp)");
+__device__ __forceinline__ uint32_t* piece_tags(const DecodeArgs& a) {
+    return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.spiece_rw) +
+                                       (((uint64_t)a.npieces * sizeof(SpecPiece) + 255) & ~255ull));
+}
 // SpecBatch.pad (diagnostics, tools/spec_diag.py): how the pre-pass batch went
 enum : uint32_t { SB_STRIDE = 1, SB_STRIDE_BROKE = 2, SB_HOP_SMALL = 3, SB_HOP_DEAD = 4, SB_HOP = 5,
                   SB_LW = 6, SB_LW_DEAD = 7 };
@@ -1596,7 +1605,10 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         }
         __syncthreads();  // s.pred_ok / s.xk are reused below
     }
-    if (tid < np) s.halo[tid] = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
+    if (tid < np) {
+        s.halo[tid] = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
+        piece_tags(a)[p0 + tid] = 0;  // the general engine takes these pieces' scratch slots
+    }
     if (tid == 0) {  // is the predecessor batch's exit already published?
         s.pred_ok = b == 0;
         s.pred_exit = a.entry;
@@ -2932,6 +2944,23 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             o.pad = 0;
             sp[p] = o;
         }
+        if (a.kpre_tag && ps.kind == PK_STRIDE) {  // compaction mode: key prefixes from LDS
+            const uint32_t xr = (uint32_t)(X - base), R = (uint32_t)ps.R;
+            hg_span* slot = a.scratch + (size_t)p * MAX_REC_PIECE;
+            for (uint32_t t = tid; t < ps.count; t += THREADS) {
+                const uint32_t kp = xr + t * R + 16;  // key start, piece-relative
+                uint64_t lo, hi;
+                if (kp + 16 <= PIECE + 16) {           // staged (the halo holds 16 more bytes)
+                    lds_header(data, kp, lo, hi);
+                } else {
+                    const uint4 v = load16(a, base + kp);
+                    lo = ((uint64_t)v.y << 32) | v.x;
+                    hi = ((uint64_t)v.w << 32) | v.z;
+                }
+                *reinterpret_cast<uint4*>(slot + t) = key_prefix_be(lo, hi, ps.kl);
+            }
+            if (tid == 0) piece_tags(a)[p] = a.kpre_tag;
+        }
         total += ps.count;
         X = ps.kind == PK_EMPTY ? X : X + (uint64_t)ps.count * ps.R;
     }
@@ -3052,7 +3081,7 @@ __global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_multi(const Deco
 namespace {
 struct DecodeLayout {
     uint64_t npieces, nbatches, status_words, scratch_off, nspec, sbatch_off, spiece_off, bytes;
-    uint64_t gsum_off, link_off, status_off;
+    uint64_t gsum_off, link_off, status_off, ptag_off;
 };
 DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
@@ -3069,12 +3098,23 @@ DecodeLayout decode_layout(uint64_t len) {
     l.scratch_off = (l.status_off + l.status_words * 8 + 255) & ~255ull;
     l.sbatch_off = l.scratch_off + l.npieces * MAX_REC_PIECE * sizeof(hg_span);
     l.spiece_off = l.sbatch_off + ((l.nspec * sizeof(SpecBatch) + 255) & ~255ull);
-    l.bytes = l.spiece_off + ((l.npieces * sizeof(SpecPiece) + 255) & ~255ull);
+    l.ptag_off = l.spiece_off + ((l.npieces * sizeof(SpecPiece) + 255) & ~255ull);
+    l.bytes = l.ptag_off + ((l.npieces * 4 + 255) & ~255ull);
     return l;
 }
 }  // namespace
 
 extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) { return decode_layout(len).bytes; }
+
+// Where a table's workspace keeps its span scratch, piece records and piece
+// tags (compaction mode: the merge's entry builder reads key prefixes there).
+extern "C" void hgk_decode_ws_layout(uint64_t len, uint64_t* scratch_off, uint64_t* spiece_off,
+                                     uint64_t* ptag_off) {
+    const DecodeLayout l = decode_layout(len);
+    *scratch_off = l.scratch_off;
+    *spiece_off = l.spiece_off;
+    *ptag_off = l.ptag_off;
+}
 
 // Diagnostics (tools/spec_diag.py): geometry of the last launch.
 static uint64_t g_last_launch[8];
@@ -3159,7 +3199,7 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
                           hg_decode_result* d_result, void* d_ws, uint32_t* d_diag, uint32_t bp,
                           uint32_t sbp, uint64_t& zero_bytes, uint64_t begin = 0,
                           uint64_t stop = ~0ull, uint64_t entry = 0, bool range = false,
-                          uint64_t rlen = ~0ull) {
+                          uint64_t rlen = ~0ull, uint32_t kpre_tag = 0) {
     using namespace hgk;
     if (stop > len) stop = len;
     if (rlen > len) rlen = len;
@@ -3201,6 +3241,7 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     a.sbatch = reinterpret_cast<SpecBatch*>(ws + l.sbatch_off);
     a.spiece = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
     a.spiece_rw = reinterpret_cast<SpecPiece*>(ws + l.spiece_off);
+    a.kpre_tag = kpre_tag;
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
     a.q = a.bp / a.sbp;
     zero_bytes = (l.status_off + 2 * (uint64_t)a.nbatches * 8 + 7) & ~7ull;
@@ -3327,7 +3368,7 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
                                        const uint64_t* lens, hg_span* const* d_spans,
                                        const uint64_t* caps, hg_decode_result* d_results,
                                        void* d_ws, const uint64_t* ws_off, void* h_stage,
-                                       void* d_stage, hipStream_t stream) {
+                                       void* d_stage, hipStream_t stream, uint32_t kpre_tag) {
     using namespace hgk;
     if (ntab == 0) return HG_OK;
     uint64_t total_pieces = 0;
@@ -3346,7 +3387,8 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
     pre_s[0] = pre_d[0] = 0;
     for (uint32_t i = 0; i < ntab; ++i) {
         args[i] = make_args(d_tables[i], lens[i], d_spans[i], caps[i], d_results + i,
-                            static_cast<char*>(d_ws) + ws_off[i], nullptr, bp, sbp, zb[i]);
+                            static_cast<char*>(d_ws) + ws_off[i], nullptr, bp, sbp, zb[i], 0,
+                            ~0ull, 0, false, ~0ull, kpre_tag);
         const uint32_t gs = lens[i] ? args[i].nspec : 0;
         const uint32_t gd = lens[i] ? (args[i].nbatches > args[i].nspec ? args[i].nbatches
                                                                           : args[i].nspec)

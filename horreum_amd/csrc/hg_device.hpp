@@ -11,6 +11,27 @@ namespace hgk {
 
 constexpr uint64_t V40 = (1ull << 40) - 1;  // 40-bit positions/counts in status words
 
+// Decode pieces and their pre-pass records (hg_decode.hip), shared with the
+// merge's entry builder (hg_merge.hip), which takes key prefixes the decode
+// pre-pass left in the span scratch of stride pieces (compaction mode).
+constexpr uint32_t PIECE_BYTES = 16384;
+constexpr uint32_t PIECE_RECS = PIECE_BYTES / 16;  // most records starting in a piece
+struct SpecPiece {                // one per piece of an ok pre-pass batch
+    uint64_t x, R;
+    uint32_t kl, vl, count, pad;  // pad: SP_STRIDE, or SP_HOP (count spans in scratch)
+};
+enum : uint32_t { SP_STRIDE = 0, SP_HOP = 1 };
+
+// Key prefix of a record as merge entries compare it: bytes [0, 16) of the
+// key, big-endian, zero past klen; lo / hi = the key's first 16 bytes read
+// little-endian (bytes past the key arbitrary).
+__device__ __forceinline__ uint4 key_prefix_be(uint64_t lo, uint64_t hi, uint32_t kl) {
+    if (kl < 8) lo &= kl ? (~0ull >> (64 - 8 * kl)) : 0ull;
+    if (kl < 16) hi &= kl <= 8 ? 0ull : (~0ull >> (64 - 8 * (kl - 8)));
+    const uint64_t p0 = __builtin_bswap64(lo), p1 = __builtin_bswap64(hi);
+    return make_uint4((uint32_t)p0, (uint32_t)(p0 >> 32), (uint32_t)p1, (uint32_t)(p1 >> 32));
+}
+
 // Status word: [63:62] flag | [61:40] aux (22 bits) | [39:0] value (40 bits).
 // Every word a look-back reads is written whole by ONE 8-byte agent-scope
 // atomic store (a granule, cdna_hip_programming.md G16 R2), so a reader sees

@@ -20,7 +20,7 @@ extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t);
 extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t);
 extern "C" int hgk_decode_launch_multi(uint32_t, const uint8_t* const*, const uint64_t*,
                                        hg_span* const*, const uint64_t*, hg_decode_result*, void*,
-                                       const uint64_t*, void*, void*, hipStream_t);
+                                       const uint64_t*, void*, void*, hipStream_t, uint32_t);
 extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
                                  uint64_t*, uint32_t, hg_block*, hg_encode_result*,
                                  unsigned long long*, hipStream_t);
@@ -43,11 +43,13 @@ extern "C" int hgk_keyindex_launch(const uint8_t*, uint64_t, const hg_span*, uin
 extern "C" int hgk_lookup_launch(const uint8_t*, const hg_span*, const void*, uint64_t,
                                  uint32_t, const uint8_t*, const hg_key*, uint64_t,
                                  hg_lookup_result*, hipStream_t);
+extern "C" void hgk_decode_ws_layout(uint64_t, uint64_t*, uint64_t*, uint64_t*);
 extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
-                                hg_merge_result*, void*, void*, hipStream_t, int defer);
+                                hg_merge_result*, void*, void*, hipStream_t, int defer,
+                                const uint64_t* kp, uint32_t kp_tag);
 extern "C" int hgk_merge_epochs(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
                                 hg_merge_result*, hg_merge_result*, void*, void*, hipStream_t);
@@ -99,6 +101,7 @@ struct hg_ctx {
     // multi-context driver (hg_multi.hip): decode results, gathered offsets
     hgi::DevBuf x_res, x_aux;
     hgi::DevBuf x_arena, x_spans;  // split compaction: this context's key-range slices
+    uint32_t kpre_calls = 0;       // compaction-mode decode tags (hg_decode.hip kpre_tag)
 };
 
 namespace hgi {

@@ -67,6 +67,13 @@ struct MergeArgs {
     const uint64_t* run_off;     // [ntables + 1] entry offsets of the tables' runs
     uint32_t ntables;
     uint64_t n;                  // total entries
+    // compaction mode (kp_tag != 0): per table, the decode workspace's span
+    // scratch, piece records and piece tags, where the decode pre-pass left the
+    // key prefixes of stride pieces (hg_decode.hip, DecodeArgs::kpre_tag)
+    const uint64_t* kp_scratch;
+    const uint64_t* kp_spiece;
+    const uint64_t* kp_ptag;
+    uint32_t kp_tag;
 };
 
 
@@ -128,6 +135,28 @@ __device__ __forceinline__ MEnt make_ent(const MergeArgs& a, uint64_t g, uint32_
     sp.off = ((uint64_t)spv.y << 32) | spv.x;
     sp.klen = spv.z;
     sp.vlen = spv.w;
+    if (a.kp_tag) {  // the decode pre-pass's key prefix, if its piece was a current stride run
+        // the tag and the piece record are loaded together (one round trip,
+        // both L2-resident), then the prefix: span -> piece -> prefix
+        const uint64_t piece = sp.off / hgk::PIECE_BYTES;
+        const uint32_t tag = reinterpret_cast<const uint32_t*>(a.kp_ptag[t])[piece];
+        const hgk::SpecPiece q = reinterpret_cast<const hgk::SpecPiece*>(a.kp_spiece[t])[piece];
+        if (tag == a.kp_tag) {
+            if (q.pad == hgk::SP_STRIDE && sp.off >= q.x && q.R) {
+                const uint64_t d = sp.off - q.x, j = d / q.R;
+                if (j * q.R == d && j < q.count) {
+                    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                        reinterpret_cast<const hg_span*>(a.kp_scratch[t]) + piece * hgk::PIECE_RECS + j));
+                    MEnt m;
+                    m.p0 = ((uint64_t)v.y << 32) | v.x;
+                    m.p1 = ((uint64_t)v.w << 32) | v.z;
+                    m.klen = sp.klen;
+                    m.gd = (uint32_t)g;
+                    return m;
+                }
+            }
+        }
+    }
     const uint64_t kofs = a.table_off[t] + sp.off + 16;
     const uint8_t* k = a.arena + kofs;
     uint64_t w0 = 0, w1 = 0;
@@ -914,7 +943,7 @@ struct MergeWs {
 MergeWs merge_ws(void* d_ws, uint32_t ntables, uint64_t n) {
     using namespace hgm;
     const uint64_t ntiles = (n + TILE - 1) / TILE + 1;
-    const uint64_t stage = (5 * (uint64_t)ntables + 72) * 8;
+    const uint64_t stage = (8 * (uint64_t)ntables + 72) * 8;
     char* base = static_cast<char*>(d_ws);
     char* p = base;
     MergeWs w;
@@ -1033,17 +1062,22 @@ extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t ntables, uint64_t n) {
 // hgk_merge_staging_bytes(ntables) bytes (copied to the device on `stream`):
 // [table_off | span ptrs | run offsets of the tables | of every round].
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t ntables) {
-    return (5 * (uint64_t)ntables + 72) * 8;
+    return (8 * (uint64_t)ntables + 72) * 8;
 }
 
 // defer: on input that is not strictly increasing, leave the result as
 // HG_ERR_UNSORTED (n_out 0, no pairs) for hgk_merge_epochs instead of running
 // the serial reference loop on the device.
+// kp (nullable): [3 * ntables] device pointers -- per table the decode
+// workspace's span scratch, piece records, piece tags -- and kp_tag, the
+// decode's compaction-mode tag: merge entries take the key prefixes the
+// decode pre-pass left there (merge_prep_kernel, make_ent).
 extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint32_t ntables,
                                 const uint64_t* table_off, const hg_span* const* spans,
                                 const uint64_t* counts, hg_pair* d_out, uint64_t cap,
                                 hg_merge_result* d_result, void* d_ws, void* staging,
-                                hipStream_t stream, int defer) {
+                                hipStream_t stream, int defer, const uint64_t* kp,
+                                uint32_t kp_tag) {
     using namespace hgm;
     if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
     uint64_t n = 0;
@@ -1067,8 +1101,11 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     r0[0] = 0;
     for (uint32_t t = 0; t < ntables; ++t)
         if (counts[t]) r0[++nruns0] = r[t + 1];
-    const uint64_t stage_words = 3 * (uint64_t)ntables + 1 + round_offsets(r0, nruns0);
+    const uint64_t rwords = 3 * (uint64_t)ntables + 1 + round_offsets(r0, nruns0);
+    const uint64_t stage_words = rwords + (kp ? 3 * (uint64_t)ntables : 0);
     if (stage_words * 8 > hgk_merge_staging_bytes(ntables)) return HG_ERR_INTERNAL;
+    if (kp)
+        for (uint64_t i = 0; i < 3 * (uint64_t)ntables; ++i) h[rwords + i] = kp[i];
     const MergeWs w = merge_ws(d_ws, ntables, n);
     if (hipMemcpyAsync(w.d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
         return HG_HIP_FAIL;
@@ -1081,6 +1118,10 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     a.run_off = w.d_stage + 2 * (uint64_t)ntables;
     a.ntables = ntables;
     a.n = n;
+    a.kp_scratch = kp ? w.d_stage + rwords : nullptr;
+    a.kp_spiece = kp ? w.d_stage + rwords + ntables : nullptr;
+    a.kp_ptag = kp ? w.d_stage + rwords + 2 * (uint64_t)ntables : nullptr;
+    a.kp_tag = kp ? kp_tag : 0;
     if (n == 0) {
         // every table empty: the reference's unwrap on None (manager.rs:213)
         hg_merge_result res{0, HG_ERR_EMPTY_MERGE, 0, 0};
@@ -1137,6 +1178,8 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
     a.run_off = w.d_stage + 2 * (uint64_t)ntables;
     a.ntables = ntables;
     a.n = n;
+    a.kp_scratch = a.kp_spiece = a.kp_ptag = nullptr;  // the entries exist (e0)
+    a.kp_tag = 0;
     uint64_t* h = static_cast<uint64_t*>(staging);  // free: the stream is synchronized
     // 1. disorder points
     if (hipMemsetAsync(w.dis_count, 0, 8, stream) != hipSuccess) return HG_HIP_FAIL;

@@ -284,6 +284,40 @@ static int rt_ensure_aux(hg_ctx* c, int want) {
     return HG_OK;
 }
 
+// The one-launch batched decode.  kpre_tag != 0: compaction mode (stride
+// pieces leave key prefixes for the merge, see hg_decode.hip); ws_off (if
+// given) receives every table's workspace offset in c->bws.
+static int batch_one_launch(hg_ctx* c, uint32_t ntables, const uint8_t* const* d_tables,
+                            const uint64_t* lens, hg_span* const* d_spans, const uint64_t* caps,
+                            hg_decode_result* d_results, uint32_t kpre_tag,
+                            std::vector<uint64_t>* ws_off) {
+    if (ntables == 0) return HG_OK;
+    std::vector<uint64_t> off(ntables);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < ntables; ++i) {
+        off[i] = total;
+        total += (hgk_decode_workspace_bytes(lens[i]) + 255) & ~255ull;
+    }
+    const uint64_t sb = hgk_decode_multi_stage_bytes(ntables);
+    int r = ensure(c, c->bws, total ? total : 256);
+    if (r == HG_OK) r = ensure(c, c->bstage_d, sb);
+    if (r == HG_OK && !c->bstage_ev &&
+        hipEventCreateWithFlags(&c->bstage_ev, hipEventDisableTiming) != hipSuccess)
+        r = HG_HIP_FAIL;
+    // the previous call's arguments may still be in flight from the pinned stage
+    if (r == HG_OK && c->bstage_busy && hipEventSynchronize(c->bstage_ev) != hipSuccess)
+        r = HG_HIP_FAIL;
+    if (r == HG_OK && ensure_pin(c->bstage, sb) != HG_OK) r = HG_HIP_FAIL;
+    if (r == HG_OK)
+        r = hgk_decode_launch_multi(ntables, d_tables, lens, d_spans, caps, d_results, c->bws.p,
+                                    off.data(), c->bstage.p, c->bstage_d.p, c->stream, kpre_tag);
+    if (r != HG_OK) return r;
+    if (hipEventRecord(c->bstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
+    c->bstage_busy = true;
+    if (ws_off) *ws_off = std::move(off);
+    return HG_OK;
+}
+
 int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const* d_tables,
                               const uint64_t* lens, hg_span* const* d_spans,
                               const uint64_t* caps, hg_decode_result* d_results) {
@@ -295,34 +329,8 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
     }
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     const char* mode = getenv("HG_DECODE_BATCH");
-    if (!(mode && strcmp(mode, "streams") == 0)) {
-        if (ntables == 0) return HG_OK;
-        uint64_t* off = static_cast<uint64_t*>(malloc(sizeof(uint64_t) * ntables));
-        if (!off) return HG_ERR_INTERNAL;
-        uint64_t total = 0;
-        for (uint32_t i = 0; i < ntables; ++i) {
-            off[i] = total;
-            total += (hgk_decode_workspace_bytes(lens[i]) + 255) & ~255ull;
-        }
-        const uint64_t sb = hgk_decode_multi_stage_bytes(ntables);
-        int r = ensure(c, c->bws, total ? total : 256);
-        if (r == HG_OK) r = ensure(c, c->bstage_d, sb);
-        if (r == HG_OK && !c->bstage_ev &&
-            hipEventCreateWithFlags(&c->bstage_ev, hipEventDisableTiming) != hipSuccess)
-            r = HG_HIP_FAIL;
-        // the previous call's arguments may still be in flight from the pinned stage
-        if (r == HG_OK && c->bstage_busy && hipEventSynchronize(c->bstage_ev) != hipSuccess)
-            r = HG_HIP_FAIL;
-        if (r == HG_OK && ensure_pin(c->bstage, sb) != HG_OK) r = HG_HIP_FAIL;
-        if (r == HG_OK)
-            r = hgk_decode_launch_multi(ntables, d_tables, lens, d_spans, caps, d_results, c->bws.p,
-                                        off, c->bstage.p, c->bstage_d.p, c->stream);
-        free(off);
-        if (r != HG_OK) return r;
-        if (hipEventRecord(c->bstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
-        c->bstage_busy = true;
-        return HG_OK;
-    }
+    if (!(mode && strcmp(mode, "streams") == 0))
+        return batch_one_launch(c, ntables, d_tables, lens, d_spans, caps, d_results, 0, nullptr);
     int fan = 4;
     if (const char* e = getenv("HG_DECODE_STREAMS")) fan = atoi(e);
     fan = std::max(1, std::min<int>(fan, hg_ctx::kAux));
@@ -919,7 +927,8 @@ namespace {
 // merge_epochs (the synchronous paths).
 int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
                 const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
-                hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, int defer) {
+                hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, int defer,
+                const uint64_t* kp = nullptr, uint32_t kp_tag = 0) {
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
@@ -946,7 +955,7 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
         if (ensure_pin(c->mstage, hgk_merge_staging_bytes(ntables) + 4096) != HG_OK)
             return HG_HIP_FAIL;
         r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
-                             d_result, c->mws.p, c->mstage.p, c->stream, defer);
+                             d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag);
         if (r != HG_OK) return r;
     }
     if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
@@ -1032,10 +1041,36 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
         caps[t] = lens[t] / 16;
         spans += caps[t];
     }
-    // 1. one batched decode chain for all tables, one sync for the counts
+    // 1. one batched decode chain for all tables, one sync for the counts; in
+    //    compaction mode its stride pieces leave key prefixes for the merge
+    //    entries (kp: per table the decode workspace's scratch, piece records
+    //    and piece tags) -- the entry builder then reads spans, not key lines
+    std::vector<uint64_t> kp;
+    uint32_t kp_tag = 0;
+    const char* kmode = getenv("HG_COMPACT_KPRE");
+    const bool use_kp = !(kmode && strcmp(kmode, "0") == 0) && !getenv("HG_DECODE_BATCH");
     if (ntables) {
         hg_decode_result* dr = static_cast<hg_decode_result*>(c->d_aux.p);
-        r = hg_decode_batch_dev_async(c, ntables, dt.data(), lens, ds.data(), caps.data(), dr);
+        if (use_kp) {
+            if (++c->kpre_calls == 0) ++c->kpre_calls;  // 0 means "off"
+            kp_tag = c->kpre_calls;
+            std::vector<uint64_t> wso;
+            r = batch_one_launch(c, ntables, dt.data(), lens, ds.data(), caps.data(), dr, kp_tag,
+                                 &wso);
+            if (r == HG_OK) {
+                kp.resize(3 * (size_t)ntables);
+                for (uint32_t t = 0; t < ntables; ++t) {
+                    uint64_t so, po, to;
+                    hgk_decode_ws_layout(lens[t], &so, &po, &to);
+                    const uint64_t b = reinterpret_cast<uint64_t>(c->bws.p) + wso[t];
+                    kp[t] = b + so;
+                    kp[ntables + t] = b + po;
+                    kp[2 * (size_t)ntables + t] = b + to;
+                }
+            }
+        } else {
+            r = hg_decode_batch_dev_async(c, ntables, dt.data(), lens, ds.data(), caps.data(), dr);
+        }
         if (r == HG_OK &&
             (hipMemcpyAsync(hr.data(), dr, ntables * sizeof(hg_decode_result),
                             hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
@@ -1066,7 +1101,7 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     // with no output (the encode then writes nothing) and the epochs below run
     // the reference loop; otherwise merge and encode run back to back
     r = merge_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm, dres_m,
-                    1);
+                    1, kp.empty() ? nullptr : kp.data(), kp_tag);
     if (r != HG_OK) return r;
     auto encode = [&]() -> int {
         if (nm == 0)

@@ -25,7 +25,10 @@ def short(name):
 
 def main():
     out, tag = sys.argv[1], sys.argv[2]
-    res = {"tag": tag, "calls_per_run": CALLS, "kernels": {}}
+    dest = sys.argv[3] if len(sys.argv) > 3 else f"{tag}_pmc_compaction.json"
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    from summarize_pmc import source_stamp
+    res = {"tag": tag, "calls_per_run": CALLS, "kernels": {}, "_source": source_stamp()}
     stats = glob.glob(os.path.join(out, f"{tag}_ctrace", "**", "*kernel_stats.csv"), recursive=True)
     for r in csv.DictReader(open(stats[0])):
         if not r["Name"].startswith(OURS):
@@ -59,7 +62,7 @@ def main():
     res["traffic_bytes_per_call"] = rd + wr
     if res.get("algorithmic_bytes"):
         res["traffic_over_algorithmic"] = round((rd + wr) / res["algorithmic_bytes"], 3)
-    path = os.path.join(ROOT, "profiles", f"{tag}_pmc_compaction.json")
+    path = os.path.join(ROOT, "profiles", dest)
     with open(path, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
