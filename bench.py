@@ -209,9 +209,18 @@ def cpu_all_cores(host_sample, seconds=2.0):
         tot += t
         k += 1
     enc = k * 304_000_000 / tot / GIB
-    ok = bool(np.array_equal(spans[:1000], oracle.decode(host_sample[:132000])[0]))
+    cp = np.empty_like(host_sample)  # the CPU roofline: memcpy on the same threads
+    tot, k = 0.0, 0
+    while k == 0 or tot < seconds:
+        tot += oracle.mt_memcpy(cp, host_sample, threads)
+        k += 1
+    mcp = k * host_sample.size / tot / GIB
+    ok = bool(np.array_equal(spans[:1000], oracle.decode(host_sample[:132000])[0])
+              and np.array_equal(cp[:4096], host_sample[:4096]))
+    del cp
     return {"cores": threads, "nproc": nproc, "affinity": aff, "kind": "port (tuned)",
             "decode_cfg2_GiB_s": round(dec, 3), "encode_cfg3_1M_GiB_s": round(enc, 3),
+            "memcpy_GiB_s": round(mcp, 3),
             "sample": f"decode: the same {host_sample.size} B cfg 2 sample; encode: 1 M pairs of "
                       f"32 B / 256 B; hgo_mt_decode / hgo_mt_encode, >= {seconds} s each",
             "parity_spot": ok}

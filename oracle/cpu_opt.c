@@ -194,3 +194,38 @@ uint64_t hgo_mt_encode(const uint8_t* arena, const hg_pair* pairs, uint64_t n, u
     if (seconds) *seconds = now_s() - t0;
     return base;
 }
+
+/* CPU roofline (BASELINE.md CPU-roof): n bytes copied by nthreads threads,
+ * one contiguous slice each (memcpy, the libc's widest path). */
+typedef struct {
+    uint8_t* dst;
+    const uint8_t* src;
+    uint64_t n;
+} cpy_job;
+
+static void* cpy_worker(void* arg) {
+    cpy_job* j = (cpy_job*)arg;
+    memcpy(j->dst, j->src, j->n);
+    return NULL;
+}
+
+void hgo_mt_memcpy(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t nthreads,
+                   double* seconds) {
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    cpy_job jobs[256];
+    pthread_t th[256];
+    const double t0 = now_s();
+    const uint64_t per = (n / nthreads + 63) & ~63ull;
+    for (uint32_t t = 0; t < nthreads; ++t) {
+        const uint64_t lo = per * t < n ? per * t : n;
+        const uint64_t hi = per * (t + 1) < n ? per * (t + 1) : n;
+        jobs[t].dst = dst + lo;
+        jobs[t].src = src + lo;
+        jobs[t].n = hi - lo;
+        if (t) pthread_create(&th[t], NULL, cpy_worker, &jobs[t]);
+    }
+    cpy_worker(&jobs[0]);
+    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
+    if (seconds) *seconds = now_s() - t0;
+}

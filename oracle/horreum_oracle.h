@@ -72,6 +72,8 @@ uint64_t hgo_bench_encode_owned(const uint8_t* arena, const hg_pair* pairs,
  * threads; returns bytes written.  *seconds = wall time of the call. */
 uint64_t hgo_mt_decode(const uint8_t* bytes, uint64_t len, hg_span* spans, uint64_t cap,
                        hg_span* scratch, uint32_t nthreads, double* seconds);
+void hgo_mt_memcpy(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t nthreads,
+                   double* seconds);
 uint64_t hgo_mt_encode(const uint8_t* arena, const hg_pair* pairs, uint64_t n, uint8_t* out,
                        uint32_t nthreads, double* seconds);
 

@@ -55,6 +55,8 @@ def lib():
         L.hgo_mt_decode.restype = u64
         L.hgo_mt_encode.argtypes = [vp, vp, u64, vp, u32, ctypes.POINTER(ctypes.c_double)]
         L.hgo_mt_encode.restype = u64
+        L.hgo_mt_memcpy.argtypes = [vp, vp, u64, u32, ctypes.POINTER(ctypes.c_double)]
+        L.hgo_mt_memcpy.restype = None
         _lib = L
     return _lib
 
@@ -222,6 +224,13 @@ def mt_decode(data, nthreads, spans=None, scratch=None):
     n = lib().hgo_mt_decode(_p(buf), buf.size, _p(spans), spans.size, _p(scratch), nthreads,
                             ctypes.byref(t))
     return spans, n, t.value
+
+
+def mt_memcpy(dst, src, nthreads):
+    """Multi-threaded host memcpy (the CPU roofline row) -> seconds."""
+    t = ctypes.c_double()
+    lib().hgo_mt_memcpy(_p(dst), _p(src), min(dst.size, src.size), nthreads, ctypes.byref(t))
+    return t.value
 
 
 def mt_encode(arena, pairs, nthreads, out=None):
