@@ -2283,22 +2283,84 @@ __device__ __forceinline__ uint32_t lw_fetch_chunk(const DecodeArgs& a, uint64_t
 // Granule zero masks of the staged chunk into zm (conflict-free: lane l reads
 // granules l, l+64, l+128, l+192 and the halo's).  These masks are a large
 // share of the mode's VALU work (zmask4: one multiply gathers the flags).
+#ifndef HG_LW_MASK_LOADS_FIRST
+#define HG_LW_MASK_LOADS_FIRST 1
+#endif
 __device__ __forceinline__ void lw_chunk_masks(const uint8_t* buf, uint16_t* zm) {
     const uint32_t lane = threadIdx.x & 63u;
+#if HG_LW_MASK_LOADS_FIRST
+    uint4 g[5];  // every read issued before the first mask store (one LDS round trip, not five)
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) g[q] = *reinterpret_cast<const uint4*>(buf + (q * 64 + lane) * 16);
+    g[4] = *reinterpret_cast<const uint4*>(buf + LW_CHUNK + (lane & 3u) * 16);
+    uint32_t m[5];
+#pragma unroll
+    for (uint32_t q = 0; q < 5; ++q) m[q] = zmask16(g[q]);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) zm[q * 64 + lane] = (uint16_t)m[q];
+    if (lane < 4) zm[256 + lane] = (uint16_t)m[4];
+#else
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q)
         zm[q * 64 + lane] = (uint16_t)zmask16(*reinterpret_cast<const uint4*>(buf + (q * 64 + lane) * 16));
     if (lane < 4)
         zm[256 + lane] = (uint16_t)zmask16(*reinterpret_cast<const uint4*>(buf + LW_CHUNK + lane * 16));
+#endif
     lw_wave_sync();
 }
 
 // Candidate mask of this lane's segment and the next lane's first bit from
 // the granule masks: bit j of the 80 zero-mask bits z1:z0 <=> byte j is zero,
 // candidate j <=> bytes [j+8-hz, j+8) and [j+16-hz, j+16) are zero.
+// HG_LW_LEAN: the lane-walk mode filters candidates with 4 high zero bytes
+// (hz' = 4) whatever the table's hz: a lane walk runs in 32-bit arithmetic,
+// where a record whose klen or vlen needs more than 32 bits is dead anyway, so
+// no position on a live path is dropped (and for hz > 4 the extra candidates
+// are positions a walk reads as records longer than the file).  Then a
+// position's mask bit says exactly "header readable, klen and vlen < 2^32":
+// walks test that bit instead of reading and checking the high words, and the
+// masks need two fixed doubling steps in 32-bit funnel shifts.
+#ifndef HG_LW_LEAN
+#define HG_LW_LEAN 1
+#endif
+__device__ __forceinline__ void lw_masks4(const uint16_t* zm, uint32_t seg0, uint32_t clen,
+                                          uint64_t rem, uint64_t& cm0, uint64_t& nextbit) {
+    cm0 = 0;
+    nextbit = 0;
+    if (seg0 >= clen || rem < 16) return;
+    const uint32_t gi = seg0 / 16;  // zero-byte bits of bytes seg0 .. seg0 + 79: d0, d1, d2 (16)
+    const uint2 z = *reinterpret_cast<const uint2*>(&zm[gi]);
+    uint32_t d0 = z.x, d1 = z.y, d2 = zm[gi + 4];
+    d0 &= __builtin_amdgcn_alignbit(d1, d0, 1);  // bit j: bytes j, j+1 zero
+    d1 &= __builtin_amdgcn_alignbit(d2, d1, 1);
+    d2 &= d2 >> 1;
+    d0 &= __builtin_amdgcn_alignbit(d1, d0, 2);  // bit j: bytes j .. j+3 zero
+    d1 &= __builtin_amdgcn_alignbit(d2, d1, 2);
+    d2 &= d2 >> 2;
+    // candidate j <=> bytes [j+4, j+8) and [j+12, j+16) zero
+    uint64_t c = ((uint64_t)(__builtin_amdgcn_alignbit(d2, d1, 4) & __builtin_amdgcn_alignbit(d2, d1, 12)) << 32) |
+                 (__builtin_amdgcn_alignbit(d1, d0, 4) & __builtin_amdgcn_alignbit(d1, d0, 12));
+    const uint64_t c64 = (d2 >> 4) & (d2 >> 12) & 1u;
+    const uint32_t n = min(seg0 + SEG, clen) - seg0;
+    if (n < 64) c &= (1ull << n) - 1ull;
+    const uint64_t plim = rem - 16;
+    if (plim < seg0) {
+        c = 0;
+    } else if (plim - seg0 < 63) {
+        c &= (2ull << (plim - seg0)) - 1ull;
+    }
+    const uint32_t q = seg0 + SEG;
+    nextbit = (q < clen && (uint64_t)q <= plim) ? c64 : 0ull;
+    cm0 = c;
+}
+
 __device__ __forceinline__ void lw_masks(const uint16_t* zm, uint32_t seg0, uint32_t clen,
                                          uint64_t rem, uint32_t hz, uint64_t& cm0,
                                          uint64_t& nextbit) {
+    if (HG_LW_LEAN) {
+        lw_masks4(zm, seg0, clen, rem, cm0, nextbit);
+        return;
+    }
     cm0 = 0;
     nextbit = 0;
     if (seg0 >= clen || rem < 16) return;
@@ -2409,8 +2471,9 @@ __device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, const uint16_t
         while (cm && tries++ < LW_TRIES) {
             const uint32_t p = seg0 + (uint32_t)(__ffsll((long long)cm) - 1);
             cm &= cm - 1;
-            uint32_t k0, k1, v0, v1;
-            lds_header32(data, p, k0, k1, v0, v1);
+            uint32_t k0, k1 = 0, v0, v1 = 0;
+            if (HG_LW_LEAN) lds_kv32(data, p, k0, v0);  // high words zero by the mask
+            else lds_header32(data, p, k0, k1, v0, v1);
             const uint64_t body = (uint64_t)k0 + v0;
             if ((k1 | v1) || body >= HG_FAR_CAND || body > rem - p - 16) continue;
             const uint64_t nx = (uint64_t)p + 16 + body;
@@ -2447,11 +2510,37 @@ __device__ __forceinline__ uint32_t walk_pos(const LWalk& w, uint32_t i) {
 }
 
 __device__ __forceinline__ void lw_walk(const uint8_t* data, uint32_t lim, uint32_t x,
-                                        uint32_t segend, LWalk& w) {
+                                        uint32_t segend, uint32_t seg0, uint64_t cm, LWalk& w) {
     w.cnt = 0;
     w.dead = false;
     w.p01 = w.p23 = 0;
     uint32_t cur = x;
+    if (HG_LW_LEAN) {  // positions in [seg0, segend): the mask bit is "readable, high words zero"
+        const uint32_t lim16 = lim - 16;
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+            if (cur >= segend) break;
+            if (!((cm >> (cur - seg0)) & 1u)) {
+                w.dead = true;
+                break;
+            }
+            uint32_t k0, v0;
+            lds_kv32(data, cur, k0, v0);
+            const uint32_t room = lim16 - cur;
+            if (k0 > room || v0 > room - k0) {
+                w.dead = true;
+                break;
+            }
+            if (it == 0) w.p01 = cur;
+            if (it == 1) w.p01 |= cur << 16;
+            if (it == 2) w.p23 = cur;
+            if (it == 3) w.p23 |= cur << 16;
+            ++w.cnt;
+            cur += 16 + k0 + v0;
+        }
+        w.exit = cur;
+        return;
+    }
 #pragma unroll
     for (int it = 0; it < 4; ++it) {
         if (cur >= segend) break;
@@ -2545,7 +2634,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     else if (in_chunk) g = lw_guess(data, zm, seg0, segend, clen, rem, a.hz, cm0, nb);
     if (HG_LW_ZERO && g != NO_GUESS && (g & LW_ZERO_HDR))  // rare: a lane inside zero bytes
         g = lw_guess_nz(data, zm, seg0, clen, rem, cm0, nb);
-    if (in_chunk && g != NO_GUESS) lw_walk(data, lim, g, segend, w);
+    if (in_chunk && g != NO_GUESS) lw_walk(data, lim, g, segend, seg0, cm0, w);
     LW_STAMP(1);
     // chain marks: which lane guesses some lane's walk exits on
     const bool valid0 = in_chunk && g != NO_GUESS && !w.dead;
@@ -2597,7 +2686,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
             } else {                                 // after it one round each)
                 if (st != 0 || g == NO_GUESS || seed != g) {
                     g = seed;
-                    lw_walk(data, lim, g, segend, w);
+                    lw_walk(data, lim, g, segend, seg0, cm0, w);
                 }
                 st = 0;
                 nev = w.dead ? 0u : w.exit;
@@ -3020,6 +3109,14 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
 __device__ void lw_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t b) {
     __shared__ SpecSmem s;
     __shared__ uint64_t lw_alt[(PIECE + 512) / 8];  // lane-walk chunk buffers of waves 2 and 3
+#ifdef HG_LW_PAD  // occupancy experiments (A/B builds): extra LDS per workgroup
+    __shared__ uint8_t lw_pad[HG_LW_PAD];
+    if (a.len == 3) {
+        lw_pad[threadIdx.x] = (uint8_t)threadIdx.x;
+        __syncthreads();
+        if (a.sdiag) a.sdiag[0] = lw_pad[(threadIdx.x + 1) & 255u];
+    }
+#endif
     if (__builtin_amdgcn_readfirstlane(sb[b].pad) != SB_HOP_SMALL) return;
     const uint32_t p0 = b * a.sbp;
     const uint32_t np = min(a.sbp, a.npieces - p0);

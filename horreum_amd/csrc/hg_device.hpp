@@ -67,7 +67,26 @@ __device__ __forceinline__ uint32_t zflags(uint32_t x) {
     return __umulhi(~t & 0x80808080u, 0x02040810u);
 }
 __device__ __forceinline__ uint32_t zmask4(uint32_t x) { return zflags(x) & 0xFu; }
+#ifndef HG_ZDOT
+#define HG_ZDOT 1
+#endif
+// zmask16 by dot products (HG_ZDOT): the byte flags (0x80 or 0) of two dwords
+// weighted 1, 2, 4, 8 and 16, 32, 64, 128 by two v_dot4_u32_u8 sum to 128 x the
+// mask byte, so four dot products and two shifts replace four multiplies and
+// their combining shifts.
+__device__ __forceinline__ uint32_t zbyte_flags(uint32_t x) {
+    return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+}
 __device__ __forceinline__ uint32_t zmask16(uint4 v) {
+    if (HG_ZDOT) {
+        const uint32_t lo = __builtin_amdgcn_udot4(
+            zbyte_flags(v.y), 0x80402010u,
+            __builtin_amdgcn_udot4(zbyte_flags(v.x), 0x08040201u, 0u, false), false);
+        const uint32_t hi = __builtin_amdgcn_udot4(
+            zbyte_flags(v.w), 0x80402010u,
+            __builtin_amdgcn_udot4(zbyte_flags(v.z), 0x08040201u, 0u, false), false);
+        return (lo >> 7) | (hi << 1);
+    }
     return (((zflags(v.x) | (zflags(v.y) << 4)) & 0xFFu) | (zflags(v.z) << 8) |
             (zflags(v.w) << 12)) & 0xFFFFu;
 }
@@ -100,6 +119,16 @@ __device__ __forceinline__ void lds_header32(const uint8_t* lds, uint32_t p, uin
     k1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
     v0 = __builtin_amdgcn_alignbyte(a3, a2, sh);
     v1 = __builtin_amdgcn_alignbyte(a4, a3, sh);
+}
+
+// The low halves of klen and vlen only (four dword reads): for positions whose
+// high words are known to be zero.
+__device__ __forceinline__ void lds_kv32(const uint8_t* lds, uint32_t p, uint32_t& k0,
+                                         uint32_t& v0) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + (p & ~3u));
+    const uint32_t sh = p & 3u;
+    k0 = __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+    v0 = __builtin_amdgcn_alignbyte(w[3], w[2], sh);
 }
 
 // Wave-level inclusive max / sum scans over u32 by DPP (row shifts 1, 2, 4, 8
