@@ -187,30 +187,104 @@ __device__ __forceinline__ MEnt make_ent(const MergeArgs& a, uint64_t g, uint32_
 
 // One entry per record, and (step 2, fused) each table strictly increasing:
 // an entry is compared with its predecessor in the same table -- the
-// neighbouring thread's entry through LDS, or for the workgroup's first
-// entry the predecessor rebuilt.  err[0] = lowest offending global entry
-// index (initialised to ~0).
+// neighbouring entry through LDS, or for the workgroup's first entry the
+// predecessor rebuilt.  err[0] = lowest offending global entry index
+// (initialised to ~0).  PREP_U entries per thread (g = workgroup base + u *
+// THREADS + tid), built in stages so the PREP_U dependent load chains of
+// make_ent (span -> piece tag and record -> prefix) overlap: one entry per
+// thread left each thread three HBM round trips deep with nothing else in flight.
+#ifndef HG_PREP_U
+#define HG_PREP_U 2
+#endif
+constexpr uint32_t PREP_U = HG_PREP_U;
+
 __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* e,
                                                              unsigned long long* err) {
-    __shared__ MEnt sh[THREADS];
+    __shared__ MEnt sh[THREADS * PREP_U];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const uint32_t tid = threadIdx.x;
-    const uint64_t g = (uint64_t)blockIdx.x * THREADS + tid;
-    const bool ok = g < a.n;
+    const uint64_t gb = (uint64_t)blockIdx.x * THREADS * PREP_U;
     // the workgroup's first run by a uniform search (scalar loads), then the
-    // rare lane past a run boundary steps forward
-    uint32_t t = run_of(a, (uint64_t)blockIdx.x * THREADS);
-    while (t + 1 < a.ntables && a.run_off[t + 1] <= g) ++t;
-    MEnt m;
-    if (ok) {
-        m = make_ent(a, g, t);
+    // rare entry past a run boundary steps forward
+    uint32_t t = run_of(a, gb);
+    uint32_t tt[PREP_U];
+    hg_span sp[PREP_U];
+    bool ok[PREP_U];
+#pragma unroll
+    for (uint32_t u = 0; u < PREP_U; ++u) {  // stage 1: spans
+        const uint64_t g = gb + u * THREADS + tid;
+        ok[u] = g < a.n;
+        while (t + 1 < a.ntables && a.run_off[t + 1] <= g) ++t;
+        tt[u] = t;
+        if (ok[u]) {
+            const u32x4 v = __builtin_nontemporal_load(
+                reinterpret_cast<const u32x4*>(a.spans[t] + (g - a.run_off[t])));
+            sp[u].off = ((uint64_t)v.y << 32) | v.x;
+            sp[u].klen = v.z;
+            sp[u].vlen = v.w;
+        }
+    }
+    int64_t pj[PREP_U];  // stage 2: the prefix slot of a current stride piece, else -1
+#pragma unroll
+    for (uint32_t u = 0; u < PREP_U; ++u) {
+        pj[u] = -1;
+        if (!ok[u] || !a.kp_tag) continue;
+        const uint64_t piece = sp[u].off / hgk::PIECE_BYTES;
+        const uint32_t tag = reinterpret_cast<const uint32_t*>(a.kp_ptag[tt[u]])[piece];
+        const hgk::SpecPiece q = reinterpret_cast<const hgk::SpecPiece*>(a.kp_spiece[tt[u]])[piece];
+        if (tag == a.kp_tag && q.pad == hgk::SP_STRIDE && sp[u].off >= q.x && q.R) {
+            const uint64_t d = sp[u].off - q.x, j = d / q.R;
+            if (j * q.R == d && j < q.count) pj[u] = (int64_t)(piece * hgk::PIECE_RECS + j);
+        }
+    }
+    u32x4 kv[PREP_U];  // stage 3: the prefix, or the key's first 16 bytes
+#pragma unroll
+    for (uint32_t u = 0; u < PREP_U; ++u) {
+        kv[u] = u32x4{0, 0, 0, 0};
+        if (!ok[u]) continue;
+        if (pj[u] >= 0) {
+            kv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                reinterpret_cast<const hg_span*>(a.kp_scratch[tt[u]]) + pj[u]));
+        } else {
+            const uint64_t kofs = a.table_off[tt[u]] + sp[u].off + 16;
+            if (kofs + 16 <= a.arena_len)
+                kv[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.arena + kofs));
+        }
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < PREP_U; ++u) {  // stage 4: entries
+        if (!ok[u]) continue;
+        const uint64_t g = gb + u * THREADS + tid;
+        MEnt m;
+        if (pj[u] >= 0) {
+            m.p0 = ((uint64_t)kv[u].y << 32) | kv[u].x;
+            m.p1 = ((uint64_t)kv[u].w << 32) | kv[u].z;
+            m.klen = sp[u].klen;
+            m.gd = (uint32_t)g;
+        } else if (a.table_off[tt[u]] + sp[u].off + 32 <= a.arena_len) {
+            uint64_t r0 = ((uint64_t)kv[u].y << 32) | kv[u].x, r1 = ((uint64_t)kv[u].w << 32) | kv[u].z;
+            const uint32_t kl = sp[u].klen;
+            if (kl < 8) r0 &= kl ? (~0ull >> (64 - 8 * kl)) : 0ull;
+            if (kl < 16) r1 &= kl <= 8 ? 0ull : (~0ull >> (64 - 8 * (kl - 8)));
+            m.p0 = bswap64(r0);
+            m.p1 = bswap64(r1);
+            m.klen = kl;
+            m.gd = (uint32_t)g;
+        } else {
+            m = make_ent(a, g, tt[u]);  // the key's 16 bytes run past the arena
+        }
         e[g] = m;
-        sh[tid] = m;
+        sh[u * THREADS + tid] = m;
     }
     __syncthreads();
-    if (!ok || g == 0) return;
-    if (g == a.run_off[t]) return;  // first record of its table
-    const MEnt prev = tid ? sh[tid - 1] : make_ent(a, g - 1, t);
-    if (key_cmp(a, prev, m) >= 0) atomicMin(err, (unsigned long long)g);
+#pragma unroll
+    for (uint32_t u = 0; u < PREP_U; ++u) {
+        const uint64_t g = gb + u * THREADS + tid;
+        if (!ok[u] || g == 0 || g == a.run_off[tt[u]]) continue;  // first record of its table
+        const uint32_t l = u * THREADS + tid;
+        const MEnt prev = l ? sh[l - 1] : make_ent(a, g - 1, tt[u]);
+        if (key_cmp(a, prev, sh[l]) >= 0) atomicMin(err, (unsigned long long)g);
+    }
 }
 
 // ---- 3. one merge round ---------------------------------------------------------------
@@ -1129,7 +1203,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                    ? HG_OK
                    : HG_HIP_FAIL;
     }
-    const uint32_t g1 = (uint32_t)((n + THREADS - 1) / THREADS);
+    const uint32_t g1 = (uint32_t)((n + THREADS * PREP_U - 1) / (THREADS * PREP_U));
     hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, w.e0, w.err);
     FinalArgs fa;
     fa.out = d_out;
