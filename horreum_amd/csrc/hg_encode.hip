@@ -428,6 +428,140 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
     }
 }
 
+// ---- whole-record gather (compaction) ------------------------------------------------
+// When every pair is a whole source record -- its header the 16 bytes before
+// key_off, val_off == key_off + klen: pairs emitted by the merge of decoded
+// tables -- the output is those records' bytes verbatim, in pair order (the
+// header a record carries is the one encode_kernel would write: the decoder
+// took klen / vlen from it and rejects high words).  Output pieces are then
+// 16 bytes aligned in the OUTPUT: a piece takes the bytes of the record it
+// starts in and, where a record boundary falls inside it, of the next record,
+// whose window is read from n1 bytes before that record's start so its bytes
+// land in place and one v_bfi per dword merges the two.  encode_kernel's
+// record-relative pieces had paid header synthesis, key|value straddles and
+// tail parts (4-byte stores) on every record: ~190 VALU per wave-piece on the
+// cfg 5 leg, a VALU-bound gather.  A tile owns the pieces that START in its
+// byte range; the last one may finish with the next tile's first record.
+#ifndef HG_ENC_REC_U
+#define HG_ENC_REC_U 2
+#endif
+constexpr uint32_t REC_U = HG_ENC_REC_U;  // pieces per lane per step (their loads overlap)
+
+struct RecSmem {
+    uint64_t src[ENC_TILE + 1];  // arena offset of each record's header (+ the next tile's first)
+    uint64_t off[ENC_TILE + 2];  // tile-relative output offsets (off[nrec] = tile bytes)
+    uint64_t scan_tmp64[ENC_NW];
+    uint64_t tile_base;
+};
+
+// 16 bytes of the arena from p, never outside [0, len): a window past either
+// end is read in bounds and shifted (rare: records at the arena's edges).
+__device__ __forceinline__ uint4 arena16(const uint8_t* arena, uint64_t len, int64_t p) {
+    if (p >= 0 && (uint64_t)p + 16 <= len) return *reinterpret_cast<const uint4*>(arena + p);
+    uint8_t b[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t q = p + i;
+        b[i] = (q >= 0 && (uint64_t)q < len) ? arena[q] : 0;
+    }
+    uint4 v;
+    v.x = b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24);
+    v.y = b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24);
+    v.z = b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24);
+    v.w = b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24);
+    return v;
+}
+
+// Byte mask of dword i for the bytes of a 16-byte piece below n (n in [0, 16]).
+__device__ __forceinline__ uint32_t lowbytes_mask(uint32_t n, uint32_t i) {
+    const int32_t k = (int32_t)n - 4 * (int32_t)i;  // bytes of dword i below n
+    return k >= 4 ? ~0u : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
+}
+
+__global__ __launch_bounds__(ENC_THREADS) void encode_records_kernel(EncodeArgs a,
+                                                                     uint64_t arena_len) {
+    __shared__ RecSmem s;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t t = blockIdx.x;
+    a.n = enc_count(a.n, a.n_dev);
+    if ((uint64_t)t * ENC_TILE >= a.n) return;  // grid sized for the upper bound
+    const uint64_t r0 = (uint64_t)t * ENC_TILE;
+    const uint32_t nrec = (uint32_t)min((uint64_t)ENC_TILE, a.n - r0);
+    // ---- descriptors -> record sources and sizes, next tile's first record
+    uint64_t sz = 0;
+    if (tid < nrec) {
+        const hg_pair p = a.pairs[r0 + tid];
+        s.src[tid] = p.key_off - 16;
+        sz = 16ull + p.klen + p.vlen;
+    }
+    if (tid == 0) s.src[nrec] = r0 + nrec < a.n ? a.pairs[r0 + nrec].key_off - 16 : 0ull;
+    uint64_t tot;
+    const uint64_t loff = block_excl_scan64(sz, s.scan_tmp64, tot);
+    if (tid < nrec) s.off[tid] = loff;
+    if (tid == 0) s.off[nrec] = tot;
+    if (tid < 64) {  // the tile's output offset: its group's base + the tiles before it there
+        const uint32_t g = t / ENC_GROUP, j = t % ENC_GROUP;
+        const uint64_t v = tid < j ? a.tile_sum[(uint64_t)g * ENC_GROUP + tid] : 0ull;
+        const uint64_t b = wave_sum<uint64_t>(v) + a.group_base[g];
+        if (tid == 0) s.tile_base = b;
+    }
+    __syncthreads();
+    const uint64_t tb = s.tile_base;
+    if (a.rec_off && tid < nrec) a.rec_off[r0 + tid] = a.rec_base + tb + loff;
+    const bool has_next = r0 + nrec < a.n;  // a piece may run into the next tile's first record
+    // pieces starting in [tb, tb + tot): P in [ceil(tb / 16), ceil((tb + tot) / 16))
+    const uint64_t pa = (tb + 15) >> 4, pe = (tb + tot + 15) >> 4;
+    const uint32_t np = (uint32_t)(pe - pa);
+    const float scale = tot ? (float)nrec / (float)tot : 0.f;
+    for (uint32_t i0 = 0; i0 < np; i0 += ENC_THREADS * REC_U) {
+        uint4 w1[REC_U], w2[REC_U];
+        uint32_t n1[REC_U];
+        uint64_t o[REC_U];
+        bool live[REC_U], two[REC_U];
+#pragma unroll
+        for (uint32_t u = 0; u < REC_U; ++u) {
+            const uint32_t i = i0 + u * ENC_THREADS + tid;
+            live[u] = i < np;
+            const uint64_t ob = 16 * (pa + (live[u] ? i : 0)) - tb;  // tile-relative piece start
+            o[u] = ob;
+            uint32_t r = min((uint32_t)((float)ob * scale), nrec - 1);  // interpolate, then walk
+            while (r > 0 && s.off[r] > ob) --r;
+            while (r + 1 < nrec && s.off[r + 1] <= ob) ++r;
+            const uint64_t rem = s.off[r + 1] - ob;  // record r's bytes from the piece start
+            n1[u] = rem < 16 ? (uint32_t)rem : 16u;
+            two[u] = n1[u] < 16 && (r + 1 < nrec || has_next);
+            w1[u] = arena16(a.arena, arena_len, (int64_t)(s.src[r] + (ob - s.off[r])));
+            w2[u] = two[u] ? arena16(a.arena, arena_len, (int64_t)s.src[r + 1] - (int64_t)n1[u])
+                           : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < REC_U; ++u) {
+            if (!live[u]) continue;
+            uint4 v = w1[u];
+            if (n1[u] < 16) {
+                v.x = (v.x & lowbytes_mask(n1[u], 0)) | (w2[u].x & ~lowbytes_mask(n1[u], 0));
+                v.y = (v.y & lowbytes_mask(n1[u], 1)) | (w2[u].y & ~lowbytes_mask(n1[u], 1));
+                v.z = (v.z & lowbytes_mask(n1[u], 2)) | (w2[u].z & ~lowbytes_mask(n1[u], 2));
+                v.w = (v.w & lowbytes_mask(n1[u], 3)) | (w2[u].w & ~lowbytes_mask(n1[u], 3));
+            }
+            const uint64_t O = tb + o[u];  // absolute output offset of the piece
+            // bytes of the piece that exist: the output ends after the last
+            // record (no next record), and nothing at or past cap is written
+            uint64_t lim = two[u] || n1[u] == 16 ? 16ull : n1[u];
+            if (O >= a.cap) continue;
+            if (a.cap - O < lim) lim = a.cap - O;
+            uint8_t* dst = a.out + O;
+            if (lim == 16) {
+                st_stream16(dst, v);
+            } else {
+                const unsigned __int128 wv = ((unsigned __int128)(((uint64_t)v.w << 32) | v.z) << 64) |
+                                             (((uint64_t)v.y << 32) | v.x);
+                store_part(dst, wv, (uint32_t)lim);
+            }
+        }
+    }
+}
+
 // Output bytes per tile and per group of ENC_GROUP tiles: tsum[t] = sum over
 // the tile's records of 16 + klen + vlen; gsum[t / ENC_GROUP] += tsum[t]
 // (gsum zeroed before launch).
@@ -546,11 +680,14 @@ extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t n) {
 // merge's output count, so merge and encode run without a host round trip
 // (grids are sized for n).  gather: pairs point into several tables (merged
 // order), sources are read with the default cache policy.
-extern "C" int hgk_encode_launch_ex(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
-                                    const uint64_t* d_n, bool gather, uint8_t* d_out, uint64_t cap,
-                                    uint64_t* d_rec_off, uint64_t rec_base, uint32_t block_stride,
-                                    hg_block* d_blocks, hg_encode_result* d_result,
-                                    unsigned long long* d_status, hipStream_t stream) {
+namespace {
+// mode 0: streaming sources (a table's own pairs), 1: gathered pairs, 2:
+// whole records gathered (encode_records_kernel; rec_arena_len = arena bytes)
+int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                       const uint64_t* d_n, int mode, uint64_t rec_arena_len, uint8_t* d_out,
+                       uint64_t cap, uint64_t* d_rec_off, uint64_t rec_base,
+                       uint32_t block_stride, hg_block* d_blocks, hg_encode_result* d_result,
+                       unsigned long long* d_status, hipStream_t stream) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
@@ -580,7 +717,10 @@ extern "C" int hgk_encode_launch_ex(const uint8_t* d_arena, const hg_pair* d_pai
     a.tile_sum = tsum;
     a.group_base = gsum;
     a.n_dev = d_n;
-    if (gather)
+    if (mode == 2)
+        hipLaunchKernelGGL(encode_records_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream, a,
+                           rec_arena_len);
+    else if (mode == 1)
         hipLaunchKernelGGL(encode_kernel<false>, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream, a);
     else
         hipLaunchKernelGGL(encode_kernel<true>, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream, a);
@@ -594,6 +734,29 @@ extern "C" int hgk_encode_launch_ex(const uint8_t* d_arena, const hg_pair* d_pai
         if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     }
     return HG_OK;
+}
+
+}  // namespace
+
+extern "C" int hgk_encode_launch_ex(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                                    const uint64_t* d_n, bool gather, uint8_t* d_out, uint64_t cap,
+                                    uint64_t* d_rec_off, uint64_t rec_base, uint32_t block_stride,
+                                    hg_block* d_blocks, hg_encode_result* d_result,
+                                    unsigned long long* d_status, hipStream_t stream) {
+    return encode_launch_mode(d_arena, d_pairs, n, d_n, gather ? 1 : 0, 0, d_out, cap, d_rec_off,
+                              rec_base, block_stride, d_blocks, d_result, d_status, stream);
+}
+
+// Pairs that are whole source records in an arena of arena_len bytes (the
+// compaction's merged pairs): encode_records_kernel gathers the records.
+extern "C" int hgk_encode_launch_records(const uint8_t* d_arena, uint64_t arena_len,
+                                         const hg_pair* d_pairs, uint64_t n, const uint64_t* d_n,
+                                         uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
+                                         uint32_t block_stride, hg_block* d_blocks,
+                                         hg_encode_result* d_result, unsigned long long* d_status,
+                                         hipStream_t stream) {
+    return encode_launch_mode(d_arena, d_pairs, n, d_n, 2, arena_len, d_out, cap, d_rec_off, 0,
+                              block_stride, d_blocks, d_result, d_status, stream);
 }
 
 extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,

@@ -31,6 +31,10 @@ extern "C" int hgk_encode_launch_at(const uint8_t*, const hg_pair*, uint64_t, ui
 extern "C" int hgk_encode_launch_ex(const uint8_t*, const hg_pair*, uint64_t, const uint64_t*, bool,
                                     uint8_t*, uint64_t, uint64_t*, uint64_t, uint32_t, hg_block*,
                                     hg_encode_result*, unsigned long long*, hipStream_t);
+extern "C" int hgk_encode_launch_records(const uint8_t*, uint64_t, const hg_pair*, uint64_t,
+                                         const uint64_t*, uint8_t*, uint64_t, uint64_t*, uint32_t,
+                                         hg_block*, hg_encode_result*, unsigned long long*,
+                                         hipStream_t);
 extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
                                         hipStream_t);
 extern "C" int hgk_encode_size_launch(const hg_pair*, uint64_t, hg_encode_result*, unsigned long long*,

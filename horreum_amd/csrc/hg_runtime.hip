@@ -1108,10 +1108,18 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
             return hipMemsetAsync(dres_e, 0, sizeof(hg_encode_result), c->stream) == hipSuccess
                        ? HG_OK
                        : HG_HIP_FAIL;
-        return hgk_encode_launch_ex(arena, pairs, nm, &dres_m->n_out, true, d_out, cap,
-                                    d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, 0,
-                                    block_stride, d_blk, dres_e,
-                                    reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+        // the merged pairs are whole records of the decoded tables: gathered as
+        // records (HG_COMPACT_ENCODE=pairs: the general gather, for A/B runs)
+        const char* em = getenv("HG_COMPACT_ENCODE");
+        if (em && strcmp(em, "pairs") == 0)
+            return hgk_encode_launch_ex(arena, pairs, nm, &dres_m->n_out, true, d_out, cap,
+                                        d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, 0,
+                                        block_stride, d_blk, dres_e,
+                                        reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+        return hgk_encode_launch_records(arena, arena_len, pairs, nm, &dres_m->n_out, d_out, cap,
+                                         d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr,
+                                         block_stride, d_blk, dres_e,
+                                         reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
     };
     if ((r = encode()) != HG_OK) return r;
     char* h = static_cast<char*>(c->hres.p);
