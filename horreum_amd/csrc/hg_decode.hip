@@ -162,15 +162,24 @@ struct DecodeCtl {
     uint32_t progress;            // general batches published (INCL / ERR): the look-back's
                                   // waits restart their budget whenever it moves
     uint32_t repairs;             // pre-pass batches spliced onto their predecessor's exit
+    unsigned long long kp_count;  // compaction mode: records emitted from stride pieces whose
+                                  // key prefixes are current (their bases in piece_bases)
 };
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
     return nspec - c->bad_rev;       // bad_rev 0 (nothing bad) -> nspec
 }
 static_assert(PIECE_BYTES == 16384 && PIECE_RECS == 1024, "piece geometry (hg_device.hpp)");
+static_assert(offsetof(DecodeCtl, kp_count) == DECODE_CTL_KPCOUNT_OFF, "hg_device.hpp");
 __device__ __forceinline__ uint32_t* piece_tags(const DecodeArgs& a) {
     return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.spiece_rw) +
                                        (((uint64_t)a.npieces * sizeof(SpecPiece) + 255) & ~255ull));
+}
+// Compaction mode: the record index of each emitted stride piece's first
+// record, tagged (kpre_tag & 0xFFFFFF) << 40 (right after the piece tags).
+__device__ __forceinline__ uint64_t* piece_bases(const DecodeArgs& a) {
+    return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(piece_tags(a)) +
+                                       (((uint64_t)a.npieces * 4 + 255) & ~255ull));
 }
 // SpecBatch.pad (diagnostics, tools/spec_diag.py): how the pre-pass batch went
 enum : uint32_t { SB_STRIDE = 1, SB_STRIDE_BROKE = 2, SB_HOP_SMALL = 3, SB_HOP_DEAD = 4, SB_HOP = 5,
@@ -1277,6 +1286,7 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
         __syncthreads();
         return end;
     }
+    unsigned long long kp_n = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint64_t g = uni(pbase[i]);
         const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
@@ -1288,8 +1298,16 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
         } else {
             for (uint32_t t = tid; t < cnt; t += THREADS)
                 if (g + t < a.cap) write_span(a.spans, g + t, a.obase + x + t * R, kl, vl);
+            // compaction mode: a stride piece whose key prefixes the pre-pass left
+            // keeps its first record's index, so the merge builds its entries per
+            // piece (hg_merge.hip, merge_kent_kernel) instead of per record
+            if (a.kpre_tag && tid == 0 && cnt && piece_tags(a)[q0 + i] == a.kpre_tag) {
+                piece_bases(a)[q0 + i] = ((uint64_t)(a.kpre_tag & 0xFFFFFFu) << 40) | g;
+                kp_n += cnt;
+            }
         }
     }
+    if (kp_n) atomicAdd(&a.ctl->kp_count, kp_n);  // thread 0: the batch's kept pieces
     const uint64_t end = uni(pbase[SPEC_BP]);
     __syncthreads();
     return end;
@@ -2737,6 +2755,57 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     return true;
 }
 
+// One lane's exact walk of the staged chunk from X (records of a few hundred
+// bytes: a dozen dependent LDS header reads per 4 KiB cost less than the
+// lanes' masks, guesses and relaxation): the positions go to pos (the chunk's
+// mask rows, unused in this mode), then the wave stores the spans, one
+// instruction per 64 records.  A record this 32-bit walk cannot read takes
+// lw_chunk_serial (exact 64-bit walk).  Same contract as lw_chunk with X exact.
+#ifndef HG_LW_SER
+#define HG_LW_SER 0  // > 0: after a chunk of at most this many records, walk the next by one lane
+#endif
+__device__ __forceinline__ bool lw_chunk_walk(const DecodeArgs& a, const uint8_t* data,
+                                              uint16_t* pos, uint64_t cb, uint32_t clen, uint64_t X,
+                                              hg_span* out, uint64_t& entry, uint32_t& count,
+                                              uint64_t& exit, uint32_t& nstores) {
+    const uint32_t lane = threadIdx.x & 63u;
+    nstores = 0;
+    count = 0;
+    entry = X;
+    if (clen == 0 || X >= cb + clen) {
+        exit = X;
+        return true;
+    }
+    const uint32_t lim = (uint32_t)min(a.len - cb, (uint64_t)1 << 31);
+    uint32_t n = 0, ok = 1, cur = (uint32_t)(X - cb);
+    if (lane == 0) {
+        while (cur < clen) {
+            if (cur + 16 > lim) {
+                ok = 0;
+                break;
+            }
+            uint32_t k0, k1, v0, v1;
+            lds_header32(data, cur, k0, k1, v0, v1);
+            const uint32_t room = lim - cur - 16;
+            if ((k1 | v1) || k0 > room || v0 > room - k0) {
+                ok = 0;
+                break;
+            }
+            pos[n++] = (uint16_t)cur;
+            cur += 16 + k0 + v0;
+        }
+    }
+    if (!__shfl(ok, 0, 64)) return lw_chunk_serial(a, data, cb, clen, X, out, count, exit, nstores);
+    count = __shfl(n, 0, 64);
+    exit = cb + __shfl(cur, 0, 64);
+    lw_wave_sync();
+    if (out) {
+        for (uint32_t i = lane; i < count; i += 64) lw_store_span(out, i, data, cb, pos[i]);
+        nstores = (count + 63) / 64;
+    }
+    return true;
+}
+
 // This wave's quarter [pb, pe) of the batch's pieces, entered at X (exact;
 // LW_GUESS: through the lead-in chunk before pb), streamed chunk by chunk
 // through the wave's two LDS chunk buffers: piece records into sp[], spans
@@ -2763,11 +2832,13 @@ __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint
     bool ok = true;
     total = 0;
     entry = X;
+    bool ser = false;  // HG_LW_SER: the last chunk's records were few, walk this one by one lane
     for (uint64_t k = k0; k < k1; ++k) {
         uint8_t* const cur = bufs + ((k - k0) & 1u) * LW_CBUF;
         uint8_t* const nxt = bufs + ((k - k0 + 1) & 1u) * LW_CBUF;
         if (k + 1 < k1) lw_fetch_chunk(a, (k + 1) * LW_CHUNK, nxt);  // in flight meanwhile
-        lw_chunk_masks(cur, zm);
+        const bool walk1 = HG_LW_SER && ser && x != LW_GUESS;
+        if (!walk1) lw_chunk_masks(cur, zm);
         LW_STAMP(0);
         const uint64_t cb = k * LW_CHUNK;
         const uint32_t clen = a.stop > cb ? (uint32_t)min((uint64_t)LW_CHUNK, a.stop - cb) : 0u;
@@ -2776,10 +2847,13 @@ __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint
         hg_span* out = is_lead ? nullptr : a.scratch + (size_t)piece * MAX_REC_PIECE + pcount;
         uint64_t en = 0, ex = 0;
         uint32_t cnt = 0, nst = 0;
-        if (!lw_chunk(s, a, cur, zm, sg, tg, cb, clen, x, out, en, cnt, ex, nst)) {
+        const bool okc = walk1 ? lw_chunk_walk(a, cur, zm, cb, clen, x, out, en, cnt, ex, nst)
+                               : lw_chunk(s, a, cur, zm, sg, tg, cb, clen, x, out, en, cnt, ex, nst);
+        if (!okc) {
             ok = false;
             break;
         }
+        if (HG_LW_SER && clen == LW_CHUNK) ser = cnt <= HG_LW_SER;
         if (is_lead) {
             entry = ex;
             x = ex;
@@ -3204,7 +3278,7 @@ __global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_multi(const Deco
 namespace {
 struct DecodeLayout {
     uint64_t npieces, nbatches, status_words, scratch_off, nspec, sbatch_off, spiece_off, bytes;
-    uint64_t gsum_off, link_off, status_off, ptag_off;
+    uint64_t gsum_off, link_off, status_off, ptag_off, pbase_off;
 };
 DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
@@ -3222,7 +3296,8 @@ DecodeLayout decode_layout(uint64_t len) {
     l.sbatch_off = l.scratch_off + l.npieces * MAX_REC_PIECE * sizeof(hg_span);
     l.spiece_off = l.sbatch_off + ((l.nspec * sizeof(SpecBatch) + 255) & ~255ull);
     l.ptag_off = l.spiece_off + ((l.npieces * sizeof(SpecPiece) + 255) & ~255ull);
-    l.bytes = l.ptag_off + ((l.npieces * 4 + 255) & ~255ull);
+    l.pbase_off = l.ptag_off + ((l.npieces * 4 + 255) & ~255ull);
+    l.bytes = l.pbase_off + ((l.npieces * 8 + 255) & ~255ull);
     return l;
 }
 }  // namespace
@@ -3232,11 +3307,12 @@ extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) { return decode_lay
 // Where a table's workspace keeps its span scratch, piece records and piece
 // tags (compaction mode: the merge's entry builder reads key prefixes there).
 extern "C" void hgk_decode_ws_layout(uint64_t len, uint64_t* scratch_off, uint64_t* spiece_off,
-                                     uint64_t* ptag_off) {
+                                     uint64_t* ptag_off, uint64_t* pbase_off) {
     const DecodeLayout l = decode_layout(len);
     *scratch_off = l.scratch_off;
     *spiece_off = l.spiece_off;
     *ptag_off = l.ptag_off;
+    *pbase_off = l.pbase_off;
 }
 
 // Diagnostics (tools/spec_diag.py): geometry of the last launch.
