@@ -162,24 +162,15 @@ struct DecodeCtl {
     uint32_t progress;            // general batches published (INCL / ERR): the look-back's
                                   // waits restart their budget whenever it moves
     uint32_t repairs;             // pre-pass batches spliced onto their predecessor's exit
-    unsigned long long kp_count;  // compaction mode: records emitted from stride pieces whose
-                                  // key prefixes are current (their bases in piece_bases)
 };
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
     return nspec - c->bad_rev;       // bad_rev 0 (nothing bad) -> nspec
 }
 static_assert(PIECE_BYTES == 16384 && PIECE_RECS == 1024, "piece geometry (hg_device.hpp)");
-static_assert(offsetof(DecodeCtl, kp_count) == DECODE_CTL_KPCOUNT_OFF, "hg_device.hpp");
 __device__ __forceinline__ uint32_t* piece_tags(const DecodeArgs& a) {
     return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(a.spiece_rw) +
                                        (((uint64_t)a.npieces * sizeof(SpecPiece) + 255) & ~255ull));
-}
-// Compaction mode: the record index of each emitted stride piece's first
-// record, tagged (kpre_tag & 0xFFFFFF) << 40 (right after the piece tags).
-__device__ __forceinline__ uint64_t* piece_bases(const DecodeArgs& a) {
-    return reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(piece_tags(a)) +
-                                       (((uint64_t)a.npieces * 4 + 255) & ~255ull));
 }
 // SpecBatch.pad (diagnostics, tools/spec_diag.py): how the pre-pass batch went
 enum : uint32_t { SB_STRIDE = 1, SB_STRIDE_BROKE = 2, SB_HOP_SMALL = 3, SB_HOP_DEAD = 4, SB_HOP = 5,
@@ -1286,7 +1277,6 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
         __syncthreads();
         return end;
     }
-    unsigned long long kp_n = 0;
     for (uint32_t i = 0; i < n; ++i) {
         const uint64_t g = uni(pbase[i]);
         const uint64_t x = uni(pc[i].x), R = uni(pc[i].R);
@@ -1298,16 +1288,8 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
         } else {
             for (uint32_t t = tid; t < cnt; t += THREADS)
                 if (g + t < a.cap) write_span(a.spans, g + t, a.obase + x + t * R, kl, vl);
-            // compaction mode: a stride piece whose key prefixes the pre-pass left
-            // keeps its first record's index, so the merge builds its entries per
-            // piece (hg_merge.hip, merge_kent_kernel) instead of per record
-            if (a.kpre_tag && tid == 0 && cnt && piece_tags(a)[q0 + i] == a.kpre_tag) {
-                piece_bases(a)[q0 + i] = ((uint64_t)(a.kpre_tag & 0xFFFFFFu) << 40) | g;
-                kp_n += cnt;
-            }
         }
     }
-    if (kp_n) atomicAdd(&a.ctl->kp_count, kp_n);  // thread 0: the batch's kept pieces
     const uint64_t end = uni(pbase[SPEC_BP]);
     __syncthreads();
     return end;
@@ -2761,8 +2743,14 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
 // mask rows, unused in this mode), then the wave stores the spans, one
 // instruction per 64 records.  A record this 32-bit walk cannot read takes
 // lw_chunk_serial (exact 64-bit walk).  Same contract as lw_chunk with X exact.
+// After a full chunk of at most HG_LW_SER records, the stream walks its next
+// chunk by one lane (0: never).  Measured (tools/decode_variants.py, same box,
+// 2 rounds): 400-1200 B records with zero-byte values 0.745 -> 0.390 ms (their
+// lanes' guesses fall into the zero runs), 0-16 KiB values 0.212 -> 0.209;
+// small, 8 B-4 KiB and 400-1200 B random values unchanged; a threshold of 12
+// made medium records (8-64 B keys, 64-512 B values) 2.5 % slower.
 #ifndef HG_LW_SER
-#define HG_LW_SER 0  // > 0: after a chunk of at most this many records, walk the next by one lane
+#define HG_LW_SER 8
 #endif
 __device__ __forceinline__ bool lw_chunk_walk(const DecodeArgs& a, const uint8_t* data,
                                               uint16_t* pos, uint64_t cb, uint32_t clen, uint64_t X,
@@ -3273,12 +3261,181 @@ __global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_multi(const Deco
     decode_body<false>(a, blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
 }
 
+// ---- compaction mode: merge entries ------------------------------------------------
+// The merge's entries (hg_merge.hip MEnt: the key's bytes [0, 16) big-endian,
+// klen, entry index g = run_off[t] + record) with its order check fused (each
+// entry against its predecessor in the table), one workgroup per pre-pass
+// batch of the batched decode -- instead of merge_prep_kernel's per-record
+// span -> piece tag -> prefix load chains (124 us on the cfg 5 leg).  A batch
+// the resolved prefix emitted (its general batch wholly before the first
+// unresolved pre-pass batch) whose pieces are all stride runs with the key
+// prefixes the pre-pass left (current tag) takes its records' indices from the
+// pre-pass counts (spec_base) and its prefixes from the pieces' scratch slots:
+// contiguous loads and stores.  Any other batch finds the records starting in
+// its bytes by a search over the table's spans and reads each key through its
+// span.  Every record starts in exactly one batch, so the tables are covered.
+struct KEnt {  // hg_merge.hip MEnt
+    uint64_t p0, p1;
+    uint32_t klen, gd;
+};
+static_assert(sizeof(KEnt) == 24, "merge entry layout");
+
+// Entry of record i of the table (its key's first 16 bytes through its span).
+__device__ __forceinline__ KEnt kent_of(const DecodeArgs& a, uint64_t i, uint64_t g) {
+    const hg_span sp = a.spans[i];
+    const uint64_t ko = sp.off - a.obase + 16;
+    uint64_t lo = 0, hi = 0;
+    if (ko + 16 <= a.len) {
+        const uint4 w = *reinterpret_cast<const uint4*>(a.sst + ko);
+        lo = ((uint64_t)w.y << 32) | w.x;
+        hi = ((uint64_t)w.w << 32) | w.z;
+    } else {
+        for (uint32_t k = 0; k < 16 && ko + k < a.len; ++k) {
+            const uint64_t b = a.sst[ko + k];
+            if (k < 8) lo |= b << (8 * k);
+            else hi |= b << (8 * (k - 8));
+        }
+    }
+    const uint4 v = key_prefix_be(lo, hi, sp.klen);
+    KEnt e;
+    e.p0 = ((uint64_t)v.y << 32) | v.x;
+    e.p1 = ((uint64_t)v.w << 32) | v.z;
+    e.klen = sp.klen;
+    e.gd = (uint32_t)g;
+    return e;
+}
+
+// Key order of records xi, yi of the table (Vec<u8> Ord, src/format.rs:5).
+__device__ int kent_cmp(const DecodeArgs& a, const KEnt& x, uint64_t xi, const KEnt& y, uint64_t yi) {
+    if (x.p0 != y.p0) return x.p0 < y.p0 ? -1 : 1;
+    if (x.p1 != y.p1) return x.p1 < y.p1 ? -1 : 1;
+    if (x.klen <= 16 || y.klen <= 16) return x.klen < y.klen ? -1 : x.klen > y.klen ? 1 : 0;
+    const uint8_t* kx = a.sst + (a.spans[xi].off - a.obase) + 16;
+    const uint8_t* ky = a.sst + (a.spans[yi].off - a.obase) + 16;
+    const uint32_t m = min(x.klen, y.klen);
+    for (uint32_t i = 16; i < m; ++i)
+        if (kx[i] != ky[i]) return kx[i] < ky[i] ? -1 : 1;
+    return x.klen < y.klen ? -1 : x.klen > y.klen ? 1 : 0;
+}
+
+// First record of the table (n records) whose span starts at or after `off`
+// (spans ascend): a 64-ary search by one wave, every lane gets it.
+__device__ uint64_t span_lower_bound(const DecodeArgs& a, uint64_t n, uint64_t off) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t lo = 0, hi = n;  // answer in [lo, hi]
+    while (hi - lo > 64) {
+        const uint64_t step = (hi - lo) / 64;
+        const uint64_t probe = lo + (uint64_t)(lane + 1) * step;  // <= lo + 64 step <= hi
+        const bool below = probe < hi && a.spans[probe].off < off;
+        const unsigned long long m = __ballot(below);
+        const uint32_t k = m ? 64u - (uint32_t)__clzll((long long)m) : 0u;  // lanes 0..k-1 below
+        const uint64_t nlo = k ? lo + (uint64_t)k * step + 1 : lo;
+        hi = k < 64 ? min(hi, lo + (uint64_t)(k + 1) * step) : hi;
+        lo = nlo;
+    }
+    const bool below = lo + lane < hi && a.spans[lo + lane].off < off;
+    return lo + (uint64_t)__popcll(__ballot(below));
+}
+
+constexpr uint32_t KE_U = 4;  // records per thread per step (their loads overlap)
+__global__ __launch_bounds__(THREADS) void decode_entries_multi(const DecodeArgs* tabs, uint32_t ntab,
+                                                                const uint32_t* pre,
+                                                                const uint64_t* run_off, KEnt* ent,
+                                                                unsigned long long* err) {
+    __shared__ KEnt st[THREADS * KE_U];
+    __shared__ uint64_t pb[SPEC_BP + 1];  // fast: batch-relative index of each piece's first record
+    __shared__ uint32_t pkl[SPEC_BP];
+    __shared__ KEnt last;                 // the record before the step's first
+    __shared__ uint64_t srange[2];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
+    const DecodeArgs& a = tabs[t];
+    const uint32_t e = blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]);
+    if (e >= a.nspec) return;
+    const uint32_t q0 = e * a.sbp, n = min(a.sbp, a.npieces - q0);
+    const uint64_t nrec = run_off[t + 1] - run_off[t];
+    bool ok = a.kpre_tag != 0 && min((e / a.q + 1) * a.q, a.nspec) <= first_bad(a.ctl, a.nspec);
+    uint32_t cnt = 0;
+    if (ok && tid < n) {
+        const SpecPiece q = a.spiece[q0 + tid];
+        cnt = q.count;
+        ok = cnt == 0 || (q.pad == SP_STRIDE && piece_tags(a)[q0 + tid] == a.kpre_tag);
+        pkl[tid] = q.kl;
+    }
+    const bool fast = !__syncthreads_or(!ok);
+    if (tid < 64) {
+        uint64_t r_lo, r_hi;
+        if (fast) {
+            const uint32_t incl = dpp_sum_incl(cnt);  // n <= SPEC_BP = 64: wave 0 holds them
+            if (tid < n) pb[tid + 1] = incl;
+            r_lo = spec_base(a, e);
+            r_hi = r_lo + __builtin_amdgcn_readlane((int)incl, 63);
+        } else {  // the records starting in the batch's bytes
+            r_lo = span_lower_bound(a, nrec, a.obase + (uint64_t)q0 * PIECE);
+            r_hi = q0 + n >= a.npieces ? nrec
+                                       : span_lower_bound(a, nrec, a.obase + (uint64_t)(q0 + n) * PIECE);
+        }
+        if (tid == 0) {
+            pb[0] = 0;
+            srange[0] = r_lo;
+            srange[1] = r_hi;
+            if (r_lo > 0 && r_lo < r_hi) last = kent_of(a, r_lo - 1, run_off[t] + r_lo - 1);
+        }
+    }
+    __syncthreads();
+    const uint64_t r_lo = srange[0], total = srange[1] - r_lo, g0 = run_off[t] + r_lo;
+    for (uint64_t r0 = 0; r0 < total; r0 += THREADS * KE_U) {
+        KEnt m[KE_U];
+#pragma unroll
+        for (uint32_t u = 0; u < KE_U; ++u) {
+            const uint64_t r = r0 + u * THREADS + tid;
+            m[u] = KEnt{};
+            if (r >= total) continue;
+            if (fast) {
+                uint32_t lo = 0, hi = n;  // the piece: last i with pb[i] <= r (empty pieces
+                while (hi - lo > 1) {     // share their successor's base: the search passes them)
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (pb[mid] <= r) lo = mid;
+                    else hi = mid;
+                }
+                typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
+                    a.scratch + (size_t)(q0 + lo) * MAX_REC_PIECE + (r - pb[lo])));
+                m[u].p0 = ((uint64_t)v.y << 32) | v.x;
+                m[u].p1 = ((uint64_t)v.w << 32) | v.z;
+                m[u].klen = pkl[lo];
+                m[u].gd = (uint32_t)(g0 + r);
+            } else {
+                m[u] = kent_of(a, r_lo + r, g0 + r);
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < KE_U; ++u) st[u * THREADS + tid] = m[u];
+        __syncthreads();
+        const uint32_t nv = (uint32_t)min((uint64_t)THREADS * KE_U, total - r0);
+#pragma unroll
+        for (uint32_t u = 0; u < KE_U; ++u) {  // order check against the predecessor
+            const uint32_t l = u * THREADS + tid;
+            const uint64_t r = r_lo + r0 + l;  // the record
+            if (l >= nv || r == 0) continue;
+            const KEnt pv = l ? st[l - 1] : last;
+            if (kent_cmp(a, pv, r - 1, m[u], r) >= 0) atomicMin(err, (unsigned long long)(run_off[t] + r));
+        }
+        const uint64_t* s8 = reinterpret_cast<const uint64_t*>(st);
+        uint64_t* o8 = reinterpret_cast<uint64_t*>(ent + g0 + r0);
+        for (uint32_t w = tid; w < 3 * nv; w += THREADS) o8[w] = s8[w];
+        __syncthreads();
+        if (tid == 0) last = st[nv - 1];
+        __syncthreads();
+    }
+}
+
 }  // namespace hgk
 
 namespace {
 struct DecodeLayout {
     uint64_t npieces, nbatches, status_words, scratch_off, nspec, sbatch_off, spiece_off, bytes;
-    uint64_t gsum_off, link_off, status_off, ptag_off, pbase_off;
+    uint64_t gsum_off, link_off, status_off, ptag_off;
 };
 DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
@@ -3296,8 +3453,7 @@ DecodeLayout decode_layout(uint64_t len) {
     l.sbatch_off = l.scratch_off + l.npieces * MAX_REC_PIECE * sizeof(hg_span);
     l.spiece_off = l.sbatch_off + ((l.nspec * sizeof(SpecBatch) + 255) & ~255ull);
     l.ptag_off = l.spiece_off + ((l.npieces * sizeof(SpecPiece) + 255) & ~255ull);
-    l.pbase_off = l.ptag_off + ((l.npieces * 4 + 255) & ~255ull);
-    l.bytes = l.pbase_off + ((l.npieces * 8 + 255) & ~255ull);
+    l.bytes = l.ptag_off + ((l.npieces * 4 + 255) & ~255ull);
     return l;
 }
 }  // namespace
@@ -3307,12 +3463,11 @@ extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t len) { return decode_lay
 // Where a table's workspace keeps its span scratch, piece records and piece
 // tags (compaction mode: the merge's entry builder reads key prefixes there).
 extern "C" void hgk_decode_ws_layout(uint64_t len, uint64_t* scratch_off, uint64_t* spiece_off,
-                                     uint64_t* ptag_off, uint64_t* pbase_off) {
+                                     uint64_t* ptag_off) {
     const DecodeLayout l = decode_layout(len);
     *scratch_off = l.scratch_off;
     *spiece_off = l.spiece_off;
     *ptag_off = l.ptag_off;
-    *pbase_off = l.pbase_off;
 }
 
 // Diagnostics (tools/spec_diag.py): geometry of the last launch.
@@ -3619,4 +3774,34 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
         hipLaunchKernelGGL(decode_multi, dim3(pre_d[ntab]), dim3(THREADS), 0, stream, dargs, dpre_d,
                            ntab);
     return HG_LAUNCH_STATUS();
+}
+
+// Compaction mode, after hgk_decode_launch_multi(kpre_tag) of ntab tables:
+// the merge entries of every table (decode_entries_multi) into d_ent at
+// d_run_off[t] + record, order violations into *d_err (atomicMin of the entry
+// index).  d_stage: that call's device staging; nspec_total: its pre-pass grid
+// (hgk_decode_multi_geometry).
+extern "C" int hgk_decode_entries_launch(const void* d_stage, uint32_t ntab, uint32_t nspec_total,
+                                         const uint64_t* d_run_off, void* d_ent,
+                                         unsigned long long* d_err, hipStream_t stream) {
+    using namespace hgk;
+    if (!nspec_total) return HG_OK;
+    const char* ds = static_cast<const char*>(d_stage);
+    const uint64_t args_b = ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256;
+    const uint64_t zb_b = ((uint64_t)ntab * 8 + 255) / 256 * 256;
+    hipLaunchKernelGGL(decode_entries_multi, dim3(nspec_total), dim3(THREADS), 0, stream,
+                       reinterpret_cast<const DecodeArgs*>(ds), ntab,
+                       reinterpret_cast<const uint32_t*>(ds + args_b + zb_b), d_run_off,
+                       static_cast<KEnt*>(d_ent), d_err);
+    return HG_LAUNCH_STATUS();
+}
+
+// The pre-pass grid of the last hgk_decode_launch_multi whose host staging is
+// h_stage (read back from it: the caller keeps it until the entries launch).
+extern "C" uint32_t hgk_decode_multi_geometry(const void* h_stage, uint32_t ntab) {
+    using namespace hgk;
+    const char* hs = static_cast<const char*>(h_stage);
+    const uint64_t args_b = ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256;
+    const uint64_t zb_b = ((uint64_t)ntab * 8 + 255) / 256 * 256;
+    return reinterpret_cast<const uint32_t*>(hs + args_b + zb_b)[ntab];
 }

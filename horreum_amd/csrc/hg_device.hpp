@@ -21,9 +21,6 @@ struct SpecPiece {                // one per piece of an ok pre-pass batch
     uint32_t kl, vl, count, pad;  // pad: SP_STRIDE, or SP_HOP (count spans in scratch)
 };
 enum : uint32_t { SP_STRIDE = 0, SP_HOP = 1 };
-// Byte offset of DecodeCtl::kp_count in a decode workspace (compaction mode:
-// records emitted from stride pieces with current key prefixes).
-constexpr uint32_t DECODE_CTL_KPCOUNT_OFF = 16;
 
 // Key prefix of a record as merge entries compare it: bytes [0, 16) of the
 // key, big-endian, zero past klen; lo / hi = the key's first 16 bytes read

@@ -47,7 +47,11 @@ extern "C" int hgk_keyindex_launch(const uint8_t*, uint64_t, const hg_span*, uin
 extern "C" int hgk_lookup_launch(const uint8_t*, const hg_span*, const void*, uint64_t,
                                  uint32_t, const uint8_t*, const hg_key*, uint64_t,
                                  hg_lookup_result*, hipStream_t);
-extern "C" void hgk_decode_ws_layout(uint64_t, uint64_t*, uint64_t*, uint64_t*, uint64_t*);
+extern "C" void hgk_decode_ws_layout(uint64_t, uint64_t*, uint64_t*, uint64_t*);
+extern "C" int hgk_decode_entries_launch(const void* d_stage, uint32_t ntab, uint32_t nspec_total,
+                                         const uint64_t* d_run_off, void* d_ent,
+                                         unsigned long long* d_err, hipStream_t stream);
+extern "C" uint32_t hgk_decode_multi_geometry(const void* h_stage, uint32_t ntab);
 extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,

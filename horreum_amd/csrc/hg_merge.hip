@@ -75,22 +75,7 @@ struct MergeArgs {
     const uint64_t* kp_spiece;
     const uint64_t* kp_ptag;
     uint32_t kp_tag;
-    // and the piece bases and decode control words (DecodeCtl::kp_count): a
-    // table whose records all came from such pieces gets its entries per piece
-    // (merge_kent_kernel), the others per record (merge_prep_kernel)
-    const uint64_t* kp_pbase;
-    const uint64_t* kp_ctl;
-    const uint64_t* kp_poff;     // [ntables + 1] piece offsets of the tables (the kent grid)
 };
-
-// Compaction mode: every record of table t came from a stride piece whose key
-// prefixes and first-record index are current (the decode counted them).
-__device__ __forceinline__ bool kent_table(const MergeArgs& a, uint32_t t) {
-    if (!a.kp_tag || !a.kp_pbase) return false;
-    const unsigned long long c = *reinterpret_cast<const unsigned long long*>(
-        a.kp_ctl[t] + hgk::DECODE_CTL_KPCOUNT_OFF);
-    return c == a.run_off[t + 1] - a.run_off[t];
-}
 
 
 __device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
@@ -232,7 +217,6 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
         ok[u] = g < a.n;
         while (t + 1 < a.ntables && a.run_off[t + 1] <= g) ++t;
         tt[u] = t;
-        if (ok[u] && kent_table(a, t)) ok[u] = false;  // built (and checked) by merge_kent_kernel
         if (ok[u]) {
             const u32x4 v = __builtin_nontemporal_load(
                 reinterpret_cast<const u32x4*>(a.spans[t] + (g - a.run_off[t])));
@@ -301,71 +285,6 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
         const uint32_t l = u * THREADS + tid;
         const MEnt prev = l ? sh[l - 1] : make_ent(a, g - 1, tt[u]);
         if (key_cmp(a, prev, sh[l]) >= 0) atomicMin(err, (unsigned long long)g);
-    }
-}
-
-// Entries of the tables kent_table() accepts, one wave per decode piece: the
-// piece's records are j = 0 .. count-1 at table index base + j (base kept by
-// the decode), their key prefixes in the piece's scratch slot -- contiguous
-// prefix loads and entry stores, no per-record span -> piece -> prefix chain
-// (merge_prep_kernel: 124 us on the cfg 5 leg, latency-bound).  The order
-// check of merge_prep_kernel is fused the same way: each entry against its
-// predecessor (the lane before; for a piece's first record, the previous
-// record rebuilt by make_ent).
-constexpr uint32_t KENT_WAVES = THREADS / 64;
-__global__ __launch_bounds__(THREADS) void merge_kent_kernel(MergeArgs a, MEnt* e,
-                                                             unsigned long long* err) {
-    __shared__ MEnt sh[KENT_WAVES][64];
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint64_t P = (uint64_t)blockIdx.x * KENT_WAVES + wid;
-    if (P >= a.kp_poff[a.ntables]) return;
-    uint32_t lo = 0, hi = a.ntables;  // the table: last t with kp_poff[t] <= P
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.kp_poff[mid] <= P) lo = mid;
-        else hi = mid;
-    }
-    const uint32_t t = lo;
-    if (!kent_table(a, t)) return;
-    const uint64_t p = P - a.kp_poff[t];
-    if (reinterpret_cast<const uint32_t*>(a.kp_ptag[t])[p] != a.kp_tag) return;
-    const uint64_t pb = reinterpret_cast<const uint64_t*>(a.kp_pbase[t])[p];
-    if ((pb >> 40) != (a.kp_tag & 0xFFFFFFu)) return;
-    const hgk::SpecPiece q = reinterpret_cast<const hgk::SpecPiece*>(a.kp_spiece[t])[p];
-    if (q.pad != hgk::SP_STRIDE || q.count == 0) return;
-    const uint64_t base = pb & ((1ull << 40) - 1);
-    const uint64_t g0 = a.run_off[t] + base;
-    const u32x4* pf = reinterpret_cast<const u32x4*>(
-        reinterpret_cast<const hg_span*>(a.kp_scratch[t]) + p * hgk::PIECE_RECS);
-    MEnt prev;  // the record before the chunk's first (none for the table's first)
-    if (base > 0) prev = make_ent(a, g0 - 1, t);
-    for (uint32_t j0 = 0; j0 < q.count; j0 += 64) {
-        const uint32_t j = j0 + lane, nv = min(64u, q.count - j0);
-        MEnt m;
-        if (j < q.count) {
-            const u32x4 v = __builtin_nontemporal_load(pf + j);
-            m.p0 = ((uint64_t)v.y << 32) | v.x;
-            m.p1 = ((uint64_t)v.w << 32) | v.z;
-            m.klen = q.kl;
-            m.gd = (uint32_t)(g0 + j);
-            sh[wid][lane] = m;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        if (j < q.count && (base > 0 || j > 0)) {
-            const MEnt pv = lane ? sh[wid][lane - 1] : prev;
-            if (key_cmp(a, pv, m) >= 0) atomicMin(err, (unsigned long long)(g0 + j));
-        }
-        const uint64_t* s8 = reinterpret_cast<const uint64_t*>(sh[wid]);
-        uint64_t* o8 = reinterpret_cast<uint64_t*>(e + g0 + j0);
-#pragma unroll
-        for (uint32_t k = 0; k < 3; ++k)
-            if (lane + 64 * k < 3 * nv) o8[lane + 64 * k] = s8[lane + 64 * k];
-        prev = sh[wid][nv - 1];
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -1080,6 +999,9 @@ __global__ void merge_flag_kernel(const unsigned long long* err, hg_merge_result
 // error word, the exact loop's heads, and the epochs' scratch.
 namespace {
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t ntables);
+extern "C" int hgk_decode_entries_launch(const void* d_stage, uint32_t ntab, uint32_t nspec_total,
+                                         const uint64_t* d_run_off, void* d_ent,
+                                         unsigned long long* d_err, hipStream_t stream);
 constexpr uint64_t EPOCH_MAX_DISORDER = 4096;  // more disorder points: the serial loop
 inline uint64_t al256(uint64_t b) { return (b + 255) & ~255ull; }
 struct MergeWs {
@@ -1259,17 +1181,12 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     for (uint32_t t = 0; t < ntables; ++t)
         if (counts[t]) r0[++nruns0] = r[t + 1];
     const uint64_t rwords = 3 * (uint64_t)ntables + 1 + round_offsets(r0, nruns0);
-    // kp: 5 groups of per-table pointers, then the tables' piece offsets
-    const uint64_t stage_words = rwords + (kp ? 6 * (uint64_t)ntables + 1 : 0);
+    // kp: 3 groups of per-table pointers (then the decode's staging and grid)
+    const uint64_t stage_words = rwords + (kp ? 3 * (uint64_t)ntables : 0);
     if (stage_words * 8 > hgk_merge_staging_bytes(ntables)) return HG_ERR_INTERNAL;
-    uint64_t kent_pieces = 0;
-    if (kp) {
-        for (uint64_t i = 0; i < 5 * (uint64_t)ntables; ++i) h[rwords + i] = kp[i];
-        uint64_t* po = h + rwords + 5 * (uint64_t)ntables;
-        po[0] = 0;
-        for (uint32_t t = 0; t < ntables; ++t) po[t + 1] = po[t] + kp[5 * (uint64_t)ntables + t];
-        kent_pieces = po[ntables];
-    }
+    const uint32_t kent_grid = kp ? (uint32_t)kp[3 * (uint64_t)ntables + 1] : 0u;
+    if (kp)
+        for (uint64_t i = 0; i < 3 * (uint64_t)ntables; ++i) h[rwords + i] = kp[i];
     const MergeWs w = merge_ws(d_ws, ntables, n);
     if (hipMemcpyAsync(w.d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
         return HG_HIP_FAIL;
@@ -1286,9 +1203,6 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     a.kp_spiece = kp ? w.d_stage + rwords + ntables : nullptr;
     a.kp_ptag = kp ? w.d_stage + rwords + 2 * (uint64_t)ntables : nullptr;
     a.kp_tag = kp ? kp_tag : 0;
-    a.kp_pbase = kp ? w.d_stage + rwords + 3 * (uint64_t)ntables : nullptr;
-    a.kp_ctl = kp ? w.d_stage + rwords + 4 * (uint64_t)ntables : nullptr;
-    a.kp_poff = kp ? w.d_stage + rwords + 5 * (uint64_t)ntables : nullptr;
     if (n == 0) {
         // every table empty: the reference's unwrap on None (manager.rs:213)
         hg_merge_result res{0, HG_ERR_EMPTY_MERGE, 0, 0};
@@ -1296,16 +1210,20 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                    ? HG_OK
                    : HG_HIP_FAIL;
     }
-    const char* kent_env = getenv("HG_MERGE_KENT");  // "0": every entry by merge_prep (A/B runs)
-    if (kent_env && strcmp(kent_env, "0") == 0) {
-        kent_pieces = 0;
-        a.kp_pbase = nullptr;
+    // compaction mode: the entries come from the decode's workspace, one
+    // workgroup per pre-pass batch (hg_decode.hip, decode_entries_multi;
+    // kp[3 ntables] = the batched decode's device staging, kp[3 ntables + 1]
+    // its pre-pass grid) instead of merge_prep_kernel's per-record chains
+    const char* kent_env = getenv("HG_MERGE_KENT");  // "0": merge_prep_kernel (A/B runs)
+    if (kent_grid && !(kent_env && strcmp(kent_env, "0") == 0)) {
+        const int rk = hgk_decode_entries_launch(
+            reinterpret_cast<const void*>(kp[3 * (uint64_t)ntables]), ntables, kent_grid, a.run_off,
+            w.e0, w.err, stream);
+        if (rk != HG_OK) return rk;
+    } else {
+        const uint32_t g1 = (uint32_t)((n + THREADS * PREP_U - 1) / (THREADS * PREP_U));
+        hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, w.e0, w.err);
     }
-    if (kent_pieces)
-        hipLaunchKernelGGL(merge_kent_kernel, dim3((uint32_t)((kent_pieces + KENT_WAVES - 1) / KENT_WAVES)),
-                           dim3(THREADS), 0, stream, a, w.e0, w.err);
-    const uint32_t g1 = (uint32_t)((n + THREADS * PREP_U - 1) / (THREADS * PREP_U));
-    hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, w.e0, w.err);
     FinalArgs fa;
     fa.out = d_out;
     fa.cap = cap;
@@ -1354,7 +1272,6 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
     a.ntables = ntables;
     a.n = n;
     a.kp_scratch = a.kp_spiece = a.kp_ptag = nullptr;  // the entries exist (e0)
-    a.kp_pbase = a.kp_ctl = a.kp_poff = nullptr;
     a.kp_tag = 0;
     uint64_t* h = static_cast<uint64_t*>(staging);  // free: the stream is synchronized
     // 1. disorder points

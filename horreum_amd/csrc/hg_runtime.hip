@@ -1058,18 +1058,19 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
             r = batch_one_launch(c, ntables, dt.data(), lens, ds.data(), caps.data(), dr, kp_tag,
                                  &wso);
             if (r == HG_OK) {
-                kp.resize(6 * (size_t)ntables);
+                kp.resize(3 * (size_t)ntables + 2);
                 for (uint32_t t = 0; t < ntables; ++t) {
-                    uint64_t so, po, to, bo;
-                    hgk_decode_ws_layout(lens[t], &so, &po, &to, &bo);
+                    uint64_t so, po, to;
+                    hgk_decode_ws_layout(lens[t], &so, &po, &to);
                     const uint64_t b = reinterpret_cast<uint64_t>(c->bws.p) + wso[t];
                     kp[t] = b + so;
                     kp[ntables + t] = b + po;
                     kp[2 * (size_t)ntables + t] = b + to;
-                    kp[3 * (size_t)ntables + t] = b + bo;  // piece bases
-                    kp[4 * (size_t)ntables + t] = b;       // DecodeCtl (kp_count)
-                    kp[5 * (size_t)ntables + t] = (lens[t] + 16383) / 16384;  // pieces
                 }
+                // the decode's device staging (its DecodeArgs and pre-pass grid)
+                // for the per-batch entry builder (hgk_decode_entries_launch)
+                kp[3 * (size_t)ntables] = reinterpret_cast<uint64_t>(c->bstage_d.p);
+                kp[3 * (size_t)ntables + 1] = hgk_decode_multi_geometry(c->bstage.p, ntables);
             }
         } else {
             r = hg_decode_batch_dev_async(c, ntables, dt.data(), lens, ds.data(), caps.data(), dr);

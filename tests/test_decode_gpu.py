@@ -531,6 +531,24 @@ def test_zero_valued_records_resolved_fast(engine, shape):
     assert_same(engine, data[: data.size - 3])
 
 
+def test_one_lane_chunk_walk_errors(engine):
+    """Chunks of at most HG_LW_SER records (zero-valued 400-1200 B records)
+    are walked by one lane (lw_chunk_walk); a length it cannot follow -- past
+    the file, a high word set, past 2^32 -- falls back to the exact serial
+    walk: error kind and offset equal the oracle's, and the unbroken prefix
+    before each corruption decodes bit-exact."""
+    data = _zero_valued(60_000, (16, 17), (400, 1201), seed=11)
+    offs = oracle.decode(data)[0]["off"]
+    rng = np.random.default_rng(12)
+    for i in rng.integers(200, offs.size - 200, size=4):
+        o = int(offs[i])
+        for field, val in [(8, 1 << 33), (8, (1 << 32) - 1), (0, 1 << 40), (8, data.size)]:
+            bad = data.copy()
+            bad[o + field:o + field + 8] = np.frombuffer(int(val).to_bytes(8, "little"), np.uint8)
+            assert_same(engine, bad)
+        assert_same(engine, data[:o + 7])
+
+
 def _ctl_repairs(engine):
     import ctypes
     lib = engine.lib

@@ -7,7 +7,7 @@ for round in 1 2; do for n in "$@"; do
   unset HG_LIBRARY HG_MERGE_PAIRWISE HG_COMPACT_ENCODE HG_MERGE_KENT
   case $n in base) ;; pw) export HG_MERGE_PAIRWISE=1 ;; encpairs) export HG_COMPACT_ENCODE=pairs ;; nokent) export HG_MERGE_KENT=0 ;; *) export HG_LIBRARY=build_exp/$n/libhorreum_gpu.so ;; esac
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $d -- python3 tools/compact_leg.py > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
-  echo "== $n round $round: $(tail -1 $d.log | python3 -c "import json,sys; l=json.loads(sys.stdin.read()); print(l['ms'], l['status'], l.get('merged_records'))")"
+  echo "== $n round $round: $(grep "^{" $d.log | tail -1 | python3 -c "import json,sys; l=json.loads(sys.stdin.read()); print(l['ms'], l['status'], l.get('merged_records'))")"
   f=$(find $d -name "*kernel_stats.csv" | head -1)
   python3 - "$f" <<'PY'
 import csv, sys
