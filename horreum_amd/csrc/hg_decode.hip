@@ -3384,9 +3384,8 @@ __global__ __launch_bounds__(THREADS) void decode_entries_multi(const DecodeArgs
     }
     __syncthreads();
     const uint64_t r_lo = srange[0], total = srange[1] - r_lo, g0 = run_off[t] + r_lo;
-    // the entries of step r0 (records r0 + u THREADS + tid) into m; the next
-    // step's loads are issued before this step's checks and stores
-    auto load_step = [&](uint64_t r0, KEnt (&m)[KE_U]) {
+    for (uint64_t r0 = 0; r0 < total; r0 += THREADS * KE_U) {
+        KEnt m[KE_U];
 #pragma unroll
         for (uint32_t u = 0; u < KE_U; ++u) {
             const uint64_t r = r0 + u * THREADS + tid;
@@ -3410,15 +3409,9 @@ __global__ __launch_bounds__(THREADS) void decode_entries_multi(const DecodeArgs
                 m[u] = kent_of(a, r_lo + r, g0 + r);
             }
         }
-    };
-    KEnt m[KE_U];
-    load_step(0, m);
-    for (uint64_t r0 = 0; r0 < total; r0 += THREADS * KE_U) {
 #pragma unroll
         for (uint32_t u = 0; u < KE_U; ++u) st[u * THREADS + tid] = m[u];
         __syncthreads();
-        KEnt nm[KE_U];
-        load_step(r0 + THREADS * KE_U, nm);
         const uint32_t nv = (uint32_t)min((uint64_t)THREADS * KE_U, total - r0);
 #pragma unroll
         for (uint32_t u = 0; u < KE_U; ++u) {  // order check against the predecessor
@@ -3434,8 +3427,6 @@ __global__ __launch_bounds__(THREADS) void decode_entries_multi(const DecodeArgs
         __syncthreads();
         if (tid == 0) last = st[nv - 1];
         __syncthreads();
-#pragma unroll
-        for (uint32_t u = 0; u < KE_U; ++u) m[u] = nm[u];
     }
 }
 

@@ -21,10 +21,6 @@ struct SpecPiece {                // one per piece of an ok pre-pass batch
     uint32_t kl, vl, count, pad;  // pad: SP_STRIDE, or SP_HOP (count spans in scratch)
 };
 enum : uint32_t { SP_STRIDE = 0, SP_HOP = 1 };
-// Encode tiles (hg_encode.hip): records per tile and tiles per group sum; the
-// compaction's last merge round accumulates the record encode's sums in them.
-constexpr uint32_t ENC_TILE_RECS = 256;
-constexpr uint32_t ENC_GROUP_TILES = 16;
 
 // Key prefix of a record as merge entries compare it: bytes [0, 16) of the
 // key, big-endian, zero past klen; lo / hi = the key's first 16 bytes read

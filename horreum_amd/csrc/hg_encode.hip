@@ -78,7 +78,6 @@ __device__ __forceinline__ void st_stream16(uint8_t* p, uint4 v) {
 }
 constexpr uint32_t ENC_NW = ENC_THREADS / 64;
 constexpr uint32_t ENC_GROUP = 16;  // tiles per group sum (two-level output offsets)
-static_assert(ENC_TILE == ENC_TILE_RECS && ENC_GROUP == ENC_GROUP_TILES, "hg_device.hpp");
 
 struct EncodeArgs {
     const uint8_t* arena;
@@ -684,13 +683,11 @@ extern "C" uint64_t hgk_encode_workspace_bytes(uint64_t n) {
 namespace {
 // mode 0: streaming sources (a table's own pairs), 1: gathered pairs, 2:
 // whole records gathered (encode_records_kernel; rec_arena_len = arena bytes)
-// sums_ready: d_status already holds the tile and group sums (zeroed, then
-// accumulated by the compaction's last merge round): no encode_sums_kernel.
 int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
                        const uint64_t* d_n, int mode, uint64_t rec_arena_len, uint8_t* d_out,
                        uint64_t cap, uint64_t* d_rec_off, uint64_t rec_base,
                        uint32_t block_stride, hg_block* d_blocks, hg_encode_result* d_result,
-                       unsigned long long* d_status, hipStream_t stream, bool sums_ready = false) {
+                       unsigned long long* d_status, hipStream_t stream) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
@@ -701,12 +698,10 @@ int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t 
             return HG_HIP_FAIL;
         return HG_OK;
     }
-    if (!sums_ready) {
-        if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_HIP_FAIL;
-        hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
-                           d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum), d_n);
-        if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
-    }
+    if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_HIP_FAIL;
+    hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
+                       d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum), d_n);
+    if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng, cap,
                        d_result);
     if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
@@ -754,15 +749,14 @@ extern "C" int hgk_encode_launch_ex(const uint8_t* d_arena, const hg_pair* d_pai
 
 // Pairs that are whole source records in an arena of arena_len bytes (the
 // compaction's merged pairs): encode_records_kernel gathers the records.
-// sums_ready: d_status holds the tile / group sums already (see encode_launch_mode).
 extern "C" int hgk_encode_launch_records(const uint8_t* d_arena, uint64_t arena_len,
                                          const hg_pair* d_pairs, uint64_t n, const uint64_t* d_n,
                                          uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
                                          uint32_t block_stride, hg_block* d_blocks,
                                          hg_encode_result* d_result, unsigned long long* d_status,
-                                         hipStream_t stream, int sums_ready) {
+                                         hipStream_t stream) {
     return encode_launch_mode(d_arena, d_pairs, n, d_n, 2, arena_len, d_out, cap, d_rec_off, 0,
-                              block_stride, d_blocks, d_result, d_status, stream, sums_ready != 0);
+                              block_stride, d_blocks, d_result, d_status, stream);
 }
 
 extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,

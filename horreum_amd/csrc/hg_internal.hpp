@@ -34,7 +34,7 @@ extern "C" int hgk_encode_launch_ex(const uint8_t*, const hg_pair*, uint64_t, co
 extern "C" int hgk_encode_launch_records(const uint8_t*, uint64_t, const hg_pair*, uint64_t,
                                          const uint64_t*, uint8_t*, uint64_t, uint64_t*, uint32_t,
                                          hg_block*, hg_encode_result*, unsigned long long*,
-                                         hipStream_t, int sums_ready);
+                                         hipStream_t);
 extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
                                         hipStream_t);
 extern "C" int hgk_encode_size_launch(const hg_pair*, uint64_t, hg_encode_result*, unsigned long long*,
@@ -57,8 +57,7 @@ extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
                                 hg_merge_result*, void*, void*, hipStream_t, int defer,
-                                const uint64_t* kp, uint32_t kp_tag, unsigned long long* enc_sums,
-                                uint64_t enc_records, int* sums_fused);
+                                const uint64_t* kp, uint32_t kp_tag);
 extern "C" int hgk_merge_epochs(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
                                 hg_merge_result*, hg_merge_result*, void*, void*, hipStream_t);

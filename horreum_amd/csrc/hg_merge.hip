@@ -392,14 +392,7 @@ struct FinalArgs {
     uint64_t cap;
     hg_merge_result* result;
     uint32_t ntiles;
-    // compaction mode (or null): the record encode's tile sums (esum[0, enc_nt),
-    // output bytes of every hgk::ENC_TILE_RECS pairs) and group sums (esum[enc_nt
-    // ...), zeroed, accumulated here from the pairs (hg_encode.hip then skips
-    // encode_sums_kernel's pass over them)
-    unsigned long long* esum;
-    uint64_t enc_nt;
 };
-constexpr uint32_t FIN_SLOTS = TILE / hgk::ENC_TILE_RECS + 2;  // encode tiles a tile's pairs touch
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INCL = 2ull << 62;
 constexpr unsigned long long LB_VAL = (1ull << 62) - 1;
 
@@ -479,9 +472,7 @@ __global__ __launch_bounds__(THREADS, FINAL ? 6 : 5) void merge_level_kernel(Mer
     // HBM load after an LDS search instead of a chain of dependent loads
     __shared__ uint64_t fin_roff[FIN_LDS_TABLES + 1], fin_sp[FIN_LDS_TABLES],
         fin_toff[FIN_LDS_TABLES];
-    __shared__ unsigned long long fin_acc[FIN_SLOTS];
     const uint32_t tid = threadIdx.x;
-    if (FINAL && tid < FIN_SLOTS) fin_acc[tid] = 0;
     const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
     if (t0 >= a.n) return;
     const bool fin_lds = FINAL && a.ntables <= FIN_LDS_TABLES;
@@ -680,33 +671,6 @@ __global__ __launch_bounds__(THREADS, FINAL ? 6 : 5) void merge_level_kernel(Mer
                 uint64_t* o8 = reinterpret_cast<uint64_t*>(f.out);
                 for (uint32_t i = tid; i < 3 * ftot; i += THREADS)
                     if (w0 + i < wcap) o8[w0 + i] = s8[i];
-                if (f.esum) {
-                    // output bytes of this tile's pairs per encode tile: a thread's
-                    // <= EPT consecutive pairs touch at most two of them; per slot
-                    // a wave sum, an LDS add per wave, a device add per slot
-                    const uint64_t t0 = fin_base / hgk::ENC_TILE_RECS;
-                    const uint64_t q0 = fin_base + fpre;  // this thread's first pair
-                    const uint32_t sl = (uint32_t)(q0 / hgk::ENC_TILE_RECS - t0);
-                    uint64_t s_lo = 0, s_hi = 0;
-                    for (uint32_t k = 0; k < fcnt; ++k) {
-                        const hg_pair& p = lp[fpre + k];
-                        const uint64_t sz = 16ull + p.klen + p.vlen;
-                        if ((q0 + k) / hgk::ENC_TILE_RECS - t0 == sl) s_lo += sz;
-                        else s_hi += sz;
-                    }
-#pragma unroll
-                    for (uint32_t j = 0; j < FIN_SLOTS; ++j) {
-                        const uint64_t c = hgk::wave_sum<uint64_t>(
-                            (fcnt && sl == j ? s_lo : 0ull) + (fcnt && sl + 1 == j ? s_hi : 0ull));
-                        if ((tid & 63u) == 0 && c) atomicAdd(&fin_acc[j], (unsigned long long)c);
-                    }
-                    __syncthreads();
-                    if (tid < FIN_SLOTS && fin_acc[tid]) {
-                        const uint64_t et = t0 + tid;
-                        atomicAdd(&f.esum[et], fin_acc[tid]);
-                        atomicAdd(&f.esum[f.enc_nt + et / hgk::ENC_GROUP_TILES], fin_acc[tid]);
-                    }
-                }
             }
         }
         d0 = d1;
@@ -1192,8 +1156,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                                 const uint64_t* counts, hg_pair* d_out, uint64_t cap,
                                 hg_merge_result* d_result, void* d_ws, void* staging,
                                 hipStream_t stream, int defer, const uint64_t* kp,
-                                uint32_t kp_tag, unsigned long long* enc_sums,
-                                uint64_t enc_records, int* sums_fused) {
+                                uint32_t kp_tag) {
     using namespace hgm;
     if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
     uint64_t n = 0;
@@ -1265,20 +1228,6 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     fa.out = d_out;
     fa.cap = cap;
     fa.result = d_result;
-    // compaction: the last round (if there is one: >= 2 non-empty runs) also
-    // sums the record encode's tiles (enc_sums: hgk_encode_workspace_bytes(
-    // enc_records) bytes, the tile sums then the group sums), zeroed here
-    fa.esum = nullptr;
-    fa.enc_nt = 0;
-    if (sums_fused) *sums_fused = 0;
-    if (enc_sums && nruns0 >= 2) {
-        const uint64_t ent = (enc_records + hgk::ENC_TILE_RECS - 1) / hgk::ENC_TILE_RECS;
-        const uint64_t eng = (ent + hgk::ENC_GROUP_TILES - 1) / hgk::ENC_GROUP_TILES;
-        if (hipMemsetAsync(enc_sums, 0, (ent + eng) * 8, stream) != hipSuccess) return HG_HIP_FAIL;
-        fa.esum = enc_sums;
-        fa.enc_nt = ent;
-        if (sums_fused) *sums_fused = 1;
-    }
     // the rounds ping-pong between e1 and e2, so e0 keeps the entries for the
     // exact loop / the epochs (the first round reads e0)
     int rc = launch_rounds(a, a.run_off + ntables + 1, nruns0, w.e0, w.e1, w.e2, w, w.err, fa,
@@ -1417,8 +1366,6 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
         fa.out = d_out + std::min(N, cap);
         fa.cap = cap > N ? cap - N : 0;
         fa.result = w.ep_res;
-        fa.esum = nullptr;
-        fa.enc_nt = 0;
         if ((rc = launch_rounds(ae, w.ep_roff, nre, w.e1, w.e2, w.e1, w, ep_err, fa, stream)) !=
             HG_OK)
             return rc;

@@ -928,10 +928,7 @@ namespace {
 int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
                 const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
                 hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, int defer,
-                const uint64_t* kp = nullptr, uint32_t kp_tag = 0,
-                unsigned long long* enc_sums = nullptr, uint64_t enc_records = 0,
-                int* sums_fused = nullptr) {
-    if (sums_fused) *sums_fused = 0;
+                const uint64_t* kp = nullptr, uint32_t kp_tag = 0) {
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
@@ -958,8 +955,7 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
         if (ensure_pin(c->mstage, hgk_merge_staging_bytes(ntables) + 4096) != HG_OK)
             return HG_HIP_FAIL;
         r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
-                             d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag,
-                             enc_sums, enc_records, sums_fused);
+                             d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag);
         if (r != HG_OK) return r;
     }
     if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
@@ -1108,11 +1104,8 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     // tables that are not strictly increasing: the merge reports HG_ERR_UNSORTED
     // with no output (the encode then writes nothing) and the epochs below run
     // the reference loop; otherwise merge and encode run back to back
-    // the last merge round also sums the record encode's tiles (sums_fused)
-    int sums_fused = 0;
     r = merge_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm, dres_m,
-                    1, kp.empty() ? nullptr : kp.data(), kp_tag,
-                    reinterpret_cast<unsigned long long*>(c->ws.p), nm, &sums_fused);
+                    1, kp.empty() ? nullptr : kp.data(), kp_tag);
     if (r != HG_OK) return r;
     auto encode = [&]() -> int {
         if (nm == 0)
@@ -1130,8 +1123,7 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
         return hgk_encode_launch_records(arena, arena_len, pairs, nm, &dres_m->n_out, d_out, cap,
                                          d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr,
                                          block_stride, d_blk, dres_e,
-                                         reinterpret_cast<unsigned long long*>(c->ws.p), c->stream,
-                                         sums_fused);
+                                         reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
     };
     if ((r = encode()) != HG_OK) return r;
     char* h = static_cast<char*>(c->hres.p);
@@ -1141,7 +1133,6 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     *res = *reinterpret_cast<const hg_merge_result*>(h);
     if (res->kind == HG_ERR_UNSORTED) {
         hg_merge_result er2{};
-        sums_fused = 0;  // the epochs' rounds do not sum the encode's tiles
         if ((r = merge_epochs(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs,
                               nm, dres_m, &er2)) != HG_OK ||
             (r = encode()) != HG_OK)
