@@ -2258,6 +2258,9 @@ __device__ __forceinline__ void lw_wait_vm(uint32_t n) {
 // lane-linear, + the halo by lanes 0-3); near the end of the bytes present:
 // plain 16-byte loads with zero fill (returns after they landed).  Returns the
 // vector memory instructions left in flight.
+#ifndef HG_LW_DMA_AUX
+#define HG_LW_DMA_AUX 0  // cache policy of the chunk DMA (2: nontemporal)
+#endif
 __device__ __forceinline__ uint32_t lw_fetch_chunk(const DecodeArgs& a, uint64_t cb, uint8_t* dst) {
     const uint32_t lane = threadIdx.x & 63u;
     if (cb + LW_CHUNK + 64 <= a.rlen) {
@@ -2265,11 +2268,11 @@ __device__ __forceinline__ uint32_t lw_fetch_chunk(const DecodeArgs& a, uint64_t
         for (uint32_t q = 0; q < 4; ++q)
             __builtin_amdgcn_global_load_lds(
                 static_cast<const void*>(a.sst + cb + (uint64_t)(q * 64 + lane) * 16),
-                (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, 0);
+                (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, HG_LW_DMA_AUX);
         if (lane < 4)
             __builtin_amdgcn_global_load_lds(
                 static_cast<const void*>(a.sst + cb + LW_CHUNK + lane * 16),
-                (__attribute__((address_space(3))) void*)(dst + LW_CHUNK), 16, 0, 0);
+                (__attribute__((address_space(3))) void*)(dst + LW_CHUNK), 16, 0, HG_LW_DMA_AUX);
         return 5;
     }
 #pragma unroll 1

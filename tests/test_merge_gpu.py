@@ -347,6 +347,53 @@ def test_compact_dev(engine, stride, unsorted):
     assert c3.kind in (1, 2) and c3.status == c3.kind and c3.table == len(datas) - 1
 
 
+def _mixed_stride_table(keys, t, var_from, rng, dups_every=0):
+    """8-byte big-endian keys; records [0, var_from) fixed 8 B values (a
+    stride run), the rest 1-200 B values; with dups_every, the first record
+    starting at or after every multiple of dups_every bytes is followed by a
+    duplicate of itself (a disorder point at pre-pass batch edges)."""
+    keys = [int(k) for k in keys]
+    vl = [8 if i < var_from else int(rng.integers(1, 201)) for i in range(len(keys))]
+    if dups_every:
+        out_k, out_v, off, nxt = [], [], 0, dups_every
+        for k, v in zip(keys, vl):
+            out_k.append(k)
+            out_v.append(v)
+            off += 16 + 8 + v
+            if off >= nxt:
+                out_k.append(k)
+                out_v.append(v)
+                off += 16 + 8 + v
+                nxt += dups_every
+        keys, vl = out_k, out_v
+    pairs = [(k.to_bytes(8, "big"), bytes([t]) * v) for k, v in zip(keys, vl)]
+    arena, rec = oracle.pack_pairs(pairs)
+    return oracle.encode(arena, rec)[0]
+
+
+@pytest.mark.parametrize("dups", [False, True])
+def test_compact_entries_fast_and_searched_batches(engine, dups):
+    """Compaction-mode merge entries (hg_decode.hip decode_entries_multi):
+    tables whose stride part is emitted by the resolved prefix (entries from
+    the pre-pass prefixes) and whose variable-size part is not (entries found
+    by span search), in one compaction -- with dups, a duplicate key right
+    after every 64 KiB boundary, so the fused order check meets disorder at
+    batch edges of both kinds and the epochs take over.  Output == the
+    oracle's compact_inner output, serialized."""
+    rng = np.random.default_rng(41)
+    uni = np.unique(rng.integers(0, 1 << 40, size=900_000, dtype=np.uint64))
+    pick = [np.sort(rng.choice(uni, size=n, replace=False)) for n in (300_000, 220_000, 250_000)]
+    datas = [_mixed_stride_table(pick[0], 0, len(pick[0]), rng),
+             _mixed_stride_table(pick[1], 1, 110_000, rng, 65536 if dups else 0),
+             _mixed_stride_table(pick[2], 2, 200_000, rng)]
+    out = engine.compact_host([d.tobytes() for d in datas], block_stride=9)
+    want, wblocks, wn = oracle.compacted_table(datas, block_stride=9)
+    assert out.status == 0 and out.kind == 0 and out.n == wn
+    assert out.table == (2 if dups else 0)
+    assert np.array_equal(out.data, want)
+    assert np.array_equal(out.blocks, wblocks)
+
+
 # ---- epochs: the reference loop cut at the tables' disorder points -----------------------
 def _keyed_tables(sizes, seed, universe=None):
     """Sorted unique 8-byte big-endian keys per table (value = table id)."""

@@ -12,6 +12,6 @@ run() {  # run <name> <seconds> <args...>
   if [ $rc -ne 0 ]; then exit $rc; fi
 }
 rm -rf gpurun_out/${TAG}_ctrace gpurun_out/${TAG}_cfetch gpurun_out/${TAG}_cwrite
-run ${TAG}_ctrace 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_ctrace -- python3 tools/compact_leg.py
-run ${TAG}_cfetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_cfetch -- python3 tools/compact_leg.py
-run ${TAG}_cwrite 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_cwrite -- python3 tools/compact_leg.py
+run ${TAG}_ctrace ${T_TRACE:-200} rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_ctrace -- python3 tools/compact_leg.py
+run ${TAG}_cfetch ${T_PMC:-120} rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/${TAG}_cfetch -- python3 tools/compact_leg.py
+run ${TAG}_cwrite ${T_PMC:-120} rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/${TAG}_cwrite -- python3 tools/compact_leg.py

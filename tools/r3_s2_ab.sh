@@ -1,5 +1,5 @@
-# Round-3 session-2 GPU step: compaction A/B (merge entries from the decode
-# workspace vs merge_prep_kernel), then smoke + GPU tests + bench.
+# Round-3 session-2 GPU step: lane-walk chunk DMA cache policy A/B, then the
+# decode PMC evidence of the bench's variable-size shapes (r3_evidence_a.sh).
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 400 bash tools/ab_compact.sh base nokent > gpurun_out/ab_kent.log 2>&1; rc=$?; cat gpurun_out/ab_kent.log; [ $rc -eq 0 ] || exit $rc
-TAG=r3s2 bash tools/r3_full.sh
+ROUNDS=2 WL="small medium zsmall mixed4k" timeout -k 10 400 bash tools/ab_variants.sh base lwnt > gpurun_out/ab_lwnt.log 2>&1; rc=$?; cat gpurun_out/ab_lwnt.log; [ $rc -eq 0 ] || exit $rc
+bash tools/r3_evidence_a.sh
