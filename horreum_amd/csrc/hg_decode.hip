@@ -2258,8 +2258,12 @@ __device__ __forceinline__ void lw_wait_vm(uint32_t n) {
 // lane-linear, + the halo by lanes 0-3); near the end of the bytes present:
 // plain 16-byte loads with zero fill (returns after they landed).  Returns the
 // vector memory instructions left in flight.
+// Cache policy of the chunk DMA: nontemporal (aux 2) -- the table is read
+// once.  Same box, 2 rounds (tools/decode_variants.py): small 0.1517 ->
+// 0.1476 ms, medium 0.2065 -> 0.2009, 16 B / 8 B-4 KiB 0.0915 -> 0.0893,
+// zero-valued small unchanged.
 #ifndef HG_LW_DMA_AUX
-#define HG_LW_DMA_AUX 0  // cache policy of the chunk DMA (2: nontemporal)
+#define HG_LW_DMA_AUX 2
 #endif
 __device__ __forceinline__ uint32_t lw_fetch_chunk(const DecodeArgs& a, uint64_t cb, uint8_t* dst) {
     const uint32_t lane = threadIdx.x & 63u;
