@@ -17,6 +17,9 @@
 // first 16 bytes and are both longer fetch the rest from HBM.
 //   1. merge_prep_kernel: one entry per record (runs laid out table by table),
 //   2. and in the same pass: each table strictly increasing (else step 5).
+//      Compaction (hg_compact_*): both come from the decode's workspace
+//      instead, one workgroup per pre-pass batch (hg_decode.hip,
+//      decode_entries_multi: the pre-pass left the key prefixes).
 //   3. log2(k) rounds of merge_level_kernel: adjacent runs (A = higher
 //      priority, B = lower) merge by merge path: a workgroup owns TILE output
 //      positions, takes its A/B split from merge_split_kernel (an 8-ary
