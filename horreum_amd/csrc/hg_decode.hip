@@ -3719,11 +3719,25 @@ extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_
 // bytes, d_stage: device memory of the same size; the caller keeps h_stage
 // untouched until the stream has passed this call (the arguments are copied
 // from it asynchronously).
-extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t ntab) {
-    using namespace hgk;
-    return ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256 + ((uint64_t)ntab * 8 + 255) / 256 * 256 +
-           2 * (((uint64_t)ntab + 1) * 4 + 255) / 256 * 256;
+namespace {
+// The staging of a batched decode (host copy and device copy alike): the
+// tables' DecodeArgs, their control-region sizes, the prefix sums of their
+// pre-pass grids and of their decode grids.
+struct MultiStage {
+    uint64_t zb, pre_s, pre_d, bytes;  // byte offsets (DecodeArgs at 0) and size
+};
+MultiStage multi_stage(uint32_t ntab) {
+    auto al = [](uint64_t b) { return (b + 255) / 256 * 256; };
+    MultiStage m;
+    m.zb = al((uint64_t)ntab * sizeof(hgk::DecodeArgs));
+    m.pre_s = m.zb + al((uint64_t)ntab * 8);
+    m.pre_d = m.pre_s + al(((uint64_t)ntab + 1) * 4);
+    m.bytes = m.pre_d + al(((uint64_t)ntab + 1) * 4);
+    return m;
 }
+}  // namespace
+
+extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t ntab) { return multi_stage(ntab).bytes; }
 
 extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_tables,
                                        const uint64_t* lens, hg_span* const* d_spans,
@@ -3738,13 +3752,11 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
     const uint32_t bp = general_pieces(total_pieces, res_gen);
     const uint32_t sbp = spec_pieces(bp, total_pieces, device_cus());
     char* hs = static_cast<char*>(h_stage);
-    const uint64_t args_b = ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256;
-    const uint64_t zb_b = ((uint64_t)ntab * 8 + 255) / 256 * 256;
-    const uint64_t pre_b = (((uint64_t)ntab + 1) * 4 + 255) / 256 * 256;
+    const MultiStage ms = multi_stage(ntab);
     DecodeArgs* args = reinterpret_cast<DecodeArgs*>(hs);
-    uint64_t* zb = reinterpret_cast<uint64_t*>(hs + args_b);
-    uint32_t* pre_s = reinterpret_cast<uint32_t*>(hs + args_b + zb_b);
-    uint32_t* pre_d = reinterpret_cast<uint32_t*>(hs + args_b + zb_b + pre_b);
+    uint64_t* zb = reinterpret_cast<uint64_t*>(hs + ms.zb);
+    uint32_t* pre_s = reinterpret_cast<uint32_t*>(hs + ms.pre_s);
+    uint32_t* pre_d = reinterpret_cast<uint32_t*>(hs + ms.pre_d);
     pre_s[0] = pre_d[0] = 0;
     for (uint32_t i = 0; i < ntab; ++i) {
         args[i] = make_args(d_tables[i], lens[i], d_spans[i], caps[i], d_results + i,
@@ -3762,9 +3774,9 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
         return HG_HIP_FAIL;
     char* ds = static_cast<char*>(d_stage);
     const DecodeArgs* dargs = reinterpret_cast<const DecodeArgs*>(ds);
-    const uint64_t* dzb = reinterpret_cast<const uint64_t*>(ds + args_b);
-    const uint32_t* dpre_s = reinterpret_cast<const uint32_t*>(ds + args_b + zb_b);
-    const uint32_t* dpre_d = reinterpret_cast<const uint32_t*>(ds + args_b + zb_b + pre_b);
+    const uint64_t* dzb = reinterpret_cast<const uint64_t*>(ds + ms.zb);
+    const uint32_t* dpre_s = reinterpret_cast<const uint32_t*>(ds + ms.pre_s);
+    const uint32_t* dpre_d = reinterpret_cast<const uint32_t*>(ds + ms.pre_d);
     hipLaunchKernelGGL(decode_zero_multi, dim3(ntab), dim3(THREADS), 0, stream, dargs, dzb, ntab);
     if (pre_s[ntab]) {
         if (kpre_tag)
@@ -3794,11 +3806,9 @@ extern "C" int hgk_decode_entries_launch(const void* d_stage, uint32_t ntab, uin
     using namespace hgk;
     if (!nspec_total) return HG_OK;
     const char* ds = static_cast<const char*>(d_stage);
-    const uint64_t args_b = ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256;
-    const uint64_t zb_b = ((uint64_t)ntab * 8 + 255) / 256 * 256;
     hipLaunchKernelGGL(decode_entries_multi, dim3(nspec_total), dim3(THREADS), 0, stream,
                        reinterpret_cast<const DecodeArgs*>(ds), ntab,
-                       reinterpret_cast<const uint32_t*>(ds + args_b + zb_b), d_run_off,
+                       reinterpret_cast<const uint32_t*>(ds + multi_stage(ntab).pre_s), d_run_off,
                        static_cast<KEnt*>(d_ent), d_err);
     return HG_LAUNCH_STATUS();
 }
@@ -3807,8 +3817,6 @@ extern "C" int hgk_decode_entries_launch(const void* d_stage, uint32_t ntab, uin
 // h_stage (read back from it: the caller keeps it until the entries launch).
 extern "C" uint32_t hgk_decode_multi_geometry(const void* h_stage, uint32_t ntab) {
     using namespace hgk;
-    const char* hs = static_cast<const char*>(h_stage);
-    const uint64_t args_b = ((uint64_t)ntab * sizeof(DecodeArgs) + 255) / 256 * 256;
-    const uint64_t zb_b = ((uint64_t)ntab * 8 + 255) / 256 * 256;
-    return reinterpret_cast<const uint32_t*>(hs + args_b + zb_b)[ntab];
+    return reinterpret_cast<const uint32_t*>(static_cast<const char*>(h_stage) +
+                                             multi_stage(ntab).pre_s)[ntab];
 }
