@@ -23,13 +23,25 @@ def short(name):
     return name.split("(")[0].replace("void ", "")
 
 
+def newest_run(files):
+    """The files of the newest rocprofv3 run among `files` (gpurun_out/ keeps
+    earlier runs' <pid>_*.csv next to the new ones)."""
+    if not files:
+        return []
+    top = max(files, key=os.path.getmtime)
+    pid = os.path.basename(top).split("_")[0]
+    return [f for f in files if os.path.dirname(f) == os.path.dirname(top)
+            and os.path.basename(f).split("_")[0] == pid]
+
+
 def main():
     out, tag = sys.argv[1], sys.argv[2]
     dest = sys.argv[3] if len(sys.argv) > 3 else f"{tag}_pmc_compaction.json"
     sys.path.insert(0, os.path.join(ROOT, "tools"))
     from summarize_pmc import source_stamp
     res = {"tag": tag, "calls_per_run": CALLS, "kernels": {}, "_source": source_stamp()}
-    stats = glob.glob(os.path.join(out, f"{tag}_ctrace", "**", "*kernel_stats.csv"), recursive=True)
+    stats = newest_run(glob.glob(os.path.join(out, f"{tag}_ctrace", "**", "*kernel_stats.csv"),
+                                 recursive=True))
     for r in csv.DictReader(open(stats[0])):
         if not r["Name"].startswith(OURS):
             continue
@@ -39,8 +51,8 @@ def main():
     for cnt, sub, scale, key in (("FETCH_SIZE", "cfetch", 2.0, "hbm_read_bytes"),
                                  ("WRITE_SIZE", "cwrite", 1.0, "hbm_write_bytes")):
         tot = defaultdict(float)
-        for f in glob.glob(os.path.join(out, f"{tag}_{sub}", "**", "*counter_collection.csv"),
-                           recursive=True):
+        for f in newest_run(glob.glob(os.path.join(out, f"{tag}_{sub}", "**",
+                                                "*counter_collection.csv"), recursive=True)):
             for r in csv.DictReader(open(f)):
                 if r["Counter_Name"] == cnt and r["Kernel_Name"].startswith(OURS):
                     tot[short(r["Kernel_Name"])] += float(r["Counter_Value"]) * 1024 * scale
