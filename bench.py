@@ -739,6 +739,25 @@ def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32, ho
                                               "the generated record layout"}
 
 
+def cfg5_rank_keys(rank, ntab, per_table):
+    """Key ids (sorted, unique uint64; 16-byte big-endian keys) of key range
+    [rank * 2^40, (rank + 1) * 2^40) of each of the ntab cfg 5 tables: a
+    quarter of the keys shared by every table, the rest the table's own."""
+    rng = np.random.default_rng(5 + 1000 * rank)
+    lo = np.uint64(rank) << np.uint64(40)
+    shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64)) + lo
+    out = []
+    for _ in range(ntab):
+        own = rng.integers(0, 1 << 40, size=per_table - shared.size, dtype=np.uint64) + lo
+        out.append(np.unique(np.concatenate([shared, own])))
+    return out
+
+
+def cfg5_value_seed(rank, t):
+    """Seed of the value bytes of table t's slice on `rank`."""
+    return 50 + t + 1000 * rank
+
+
 def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000, host=False,
                    pmc_name="r3_pmc_compaction.json", exact=False):
     """BASELINE config 5 on this GPU's key range: 8 sorted tables of
@@ -760,16 +779,11 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     rate from host memory (hg_compact_host on pageable copies: H2D of every
     table, decode, merge, encode, D2H of the compacted table), median of 3."""
     from horreum_amd import synth
-    rng = np.random.default_rng(5 + 1000 * rank)
-    lo = np.uint64(rank) << np.uint64(40)
-    shared = np.unique(rng.integers(0, 1 << 40, size=per_table // 4, dtype=np.uint64)) + lo
     bufs, offs_b, total, n_in, allkeys = [], [], 0, 0, []
-    for t in range(ntab):
-        own = rng.integers(0, 1 << 40, size=per_table - shared.size, dtype=np.uint64) + lo
-        keys = np.unique(np.concatenate([shared, own]))
+    for t, keys in enumerate(cfg5_rank_keys(rank, ntab, per_table)):
         n_in += int(keys.size)
         allkeys.append(keys)
-        buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=50 + t + 1000 * rank,
+        buf, _ = synth.keyed_table(keys, np.full(keys.size, 100), seed=cfg5_value_seed(rank, t),
                                    device=device)
         bufs.append(buf)
     sizes = [b.numel() for b in bufs]
