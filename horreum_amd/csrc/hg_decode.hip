@@ -1886,6 +1886,26 @@ __global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_kernel(DecodeArg
 //      stride batch's, and the pre-pass links check the entries as usual.
 constexpr uint32_t HOP_SEG_PIECES = 4;                    // 64 KiB segments
 constexpr uint32_t HOP_SEGS = SPEC_BP / HOP_SEG_PIECES;   // per pre-pass batch, at most
+// Batches whose piece 0 shows at most HOP_WIDE_CAND candidate run ends walk
+// HOP_WIDE-piece (128 KiB) segments: half the guesses for chains twice as
+// long (a walk takes up to HOP_MAX_RECS records per 4 pieces).  Shorter
+// segments measured slower on every hop shape (cfg 4, 32 x 64 MiB: 32 KiB
+// 0.665 -> 0.75 ms, 16 KiB 1.27 ms); 128 KiB ones for every hop batch with the
+// record limit unscaled cost 400-1200 B records 3.7x (their walks gave up).
+// Thresholds, same box, 2 rounds (tools/multi_table.py, decode_variants.py):
+// 64 KiB always: cfg 4 0.662 ms, 8 B-4 KiB 0.091, 0-16 KiB 0.210, 0-64 KiB
+// 0.214, 400-1200 B 0.166; <= 12: 0.507-0.582 / 0.084 / 0.199 / 0.204 / 0.162;
+// <= 16: 0.501-0.523 / 0.084 / 0.198 / 0.201 / 0.165; <= 24: 0.489 / 0.085-
+// 0.088 / 0.198 / 0.202 / 0.156.
+#ifndef HG_HOP_WIDE_CAND
+#define HG_HOP_WIDE_CAND 24
+#endif
+#ifndef HG_HOP_WIDE
+#define HG_HOP_WIDE 8
+#endif
+constexpr uint32_t HOP_WIDE_CAND = HG_HOP_WIDE_CAND;
+constexpr uint32_t HOP_WIDE = HG_HOP_WIDE;
+static_assert(HOP_WIDE % HOP_SEG_PIECES == 0 && HOP_WIDE <= SPEC_BP, "hop segment geometry");
 constexpr uint32_t HOP_WIN = 4096;                        // guess window (bytes)
 constexpr uint32_t HOP_CHECK = 3;                         // hops a guess must survive
 #ifndef HG_HOP_MAX_CAND
@@ -1941,15 +1961,15 @@ __device__ uint64_t hop_check(const DecodeArgs& a, uint64_t p, uint64_t kl, uint
 
 // Exact walk of [x, end) through HBM headers: spans to out[0..), count,
 // exit (first start >= end) and whether a record cannot be read or the
-// segment holds more than HOP_MAX_RECS records (dead: the batch is left to
-// the general engine, which reads the table instead).
+// segment holds more than maxr records (dead: the batch is left to the
+// general engine, which reads the table instead).
 __device__ void hop_walk(const DecodeArgs& a, uint64_t x, uint64_t end, hg_span* out,
-                         uint32_t& cnt, uint64_t& exit, uint32_t& dead) {
+                         uint32_t maxr, uint32_t& cnt, uint64_t& exit, uint32_t& dead) {
     uint32_t n = 0;
     uint64_t cur = x;
     dead = 0;
     while (cur < end) {
-        if (n == HOP_MAX_RECS) {
+        if (n == maxr) {
             dead = 1;
             break;
         }
@@ -2028,7 +2048,6 @@ __device__ void hop_guess(const DecodeArgs& a, const uint8_t* w, uint64_t S, uin
 __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_t np,
                           SpecPiece* sp, uint64_t& X0, uint64_t& X, uint64_t& total) {
     const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
-    const uint32_t nseg = (np + HOP_SEG_PIECES - 1) / HOP_SEG_PIECES;
     const uint64_t bend = min((uint64_t)(p0 + np) * PIECE, a.stop);
     // Large records?  Piece 0 is still staged: count its header candidates
     // (a record start and its shifts pass the zero-byte filter, ~4 per record
@@ -2064,11 +2083,15 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
             return false;
         }
     }
+    // pieces per segment (uniform): wide segments for sparse candidates
+    const uint32_t hsp = uni(s.hcnt[0]) <= HOP_WIDE_CAND ? HOP_WIDE : HOP_SEG_PIECES;
+    const uint32_t maxr = HOP_MAX_RECS / HOP_SEG_PIECES * hsp;
+    const uint32_t nseg = (np + hsp - 1) / hsp;
     uint8_t* w = reinterpret_cast<uint8_t*>(s.data64) + wid * (HOP_WIN + 16);
     // A: guesses, four segments per round (one per wave)
     for (uint32_t r = 0; r * NW < nseg; ++r) {
         const uint32_t k = r * NW + wid;
-        const uint64_t S = (uint64_t)(p0 + k * HOP_SEG_PIECES) * PIECE;
+        const uint64_t S = (uint64_t)(p0 + k * hsp) * PIECE;
         __syncthreads();
         if (k < nseg) {
 #pragma unroll
@@ -2098,11 +2121,11 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
     }
     // B: one lane per segment walks it into scratch
     if (tid < nseg && s.hg[tid] != NO_HOP) {
-        const uint64_t S1 = (uint64_t)(p0 + (tid + 1) * HOP_SEG_PIECES) * PIECE;
+        const uint64_t S1 = (uint64_t)(p0 + (tid + 1) * hsp) * PIECE;
         uint32_t c, dd;
         uint64_t ex;
-        hop_walk(a, s.hg[tid], min(S1, bend),
-                 a.scratch + (size_t)(p0 + tid * HOP_SEG_PIECES) * MAX_REC_PIECE, c, ex, dd);
+        hop_walk(a, s.hg[tid], min(S1, bend), a.scratch + (size_t)(p0 + tid * hsp) * MAX_REC_PIECE,
+                 maxr, c, ex, dd);
         s.hcnt[tid] = c;
         s.hexit[tid] = ex;
         s.hdead[tid] = dd;
@@ -2119,11 +2142,11 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
                     why = 2;
                     break;
                 }
-                const uint64_t S1 = (uint64_t)(p0 + (k + 1) * HOP_SEG_PIECES) * PIECE;
+                const uint64_t S1 = (uint64_t)(p0 + (k + 1) * hsp) * PIECE;
                 uint32_t c, dd;
                 uint64_t ex;
-                hop_walk(a, x, min(S1, bend),
-                         a.scratch + (size_t)(p0 + k * HOP_SEG_PIECES) * MAX_REC_PIECE, c, ex, dd);
+                hop_walk(a, x, min(S1, bend), a.scratch + (size_t)(p0 + k * hsp) * MAX_REC_PIECE,
+                         maxr, c, ex, dd);
                 s.hg[k] = x;
                 s.hcnt[k] = c;
                 s.hexit[k] = ex;
@@ -2144,8 +2167,8 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
     __syncthreads();
     if (!s.hok) return false;
     if (tid < np) {
-        const uint32_t k = tid / HOP_SEG_PIECES;
-        const bool first = tid % HOP_SEG_PIECES == 0;
+        const uint32_t k = tid / hsp;
+        const bool first = tid % hsp == 0;
         SpecPiece o;
         o.x = first ? s.hg[k] : 0;
         o.R = 0;

@@ -379,6 +379,27 @@ def test_hop_mode_records_larger_than_window(engine, hop_batches):
     assert_same(engine, data[: data.size - 1000])
 
 
+def test_hop_wide_segments_meeting_small_records(engine):
+    """Tables past 64 MiB get pre-pass batches of >= 8 pieces; a batch whose
+    piece 0 holds a few KiB-sized records walks 128 KiB hop segments
+    (HOP_WIDE).  Islands of 100-byte records inside such segments pass a
+    walk's record limit and send their batches to the general engine: spans,
+    count and errors still equal the oracle's."""
+    parts, rng = [], np.random.default_rng(77)
+    for k in range(4):
+        parts.append(_shape_table(10_500, (16, 17), (3000, 4096), seed=70 + k))
+        if k < 3:
+            parts.append(_shape_table(int(rng.integers(300, 9000)), (8, 17), (60, 100), seed=80 + k))
+    data = np.concatenate(parts)
+    assert data.size > 130 * (1 << 20)
+    assert_same(engine, data)
+    offs = oracle.decode(data)[0]["off"]
+    bad = data.copy()
+    o = int(offs[offs.size // 2])
+    bad[o + 8:o + 16] = np.frombuffer(int(1 << 33).to_bytes(8, "little"), np.uint8)
+    assert_same(engine, bad)
+
+
 @pytest.mark.parametrize("shape", ["medium", "huge", "small_far"])
 def test_guess_rules_shapes(engine, shape):
     """Tables that exercise the guess rules over many general batches:

@@ -2,9 +2,9 @@
 # 16 KiB hop1) on the batched cfg 4 decode (tools/multi_table.py) and the
 # single-table large-record shapes (tools/decode_variants.py).
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
-for round in 1 2; do for name in base hop2 hop1; do
+for round in 1 2; do for name in base off w12 w24; do
   if [ "$name" = base ]; then unset HG_LIBRARY; else export HG_LIBRARY=$PWD/build_exp/$name/libhorreum_gpu.so; fi
   timeout -k 10 300 python3 tools/multi_table.py > gpurun_out/abh_mt_$name.log 2>&1 || { tail -5 gpurun_out/abh_mt_$name.log; exit 1; }
   echo "== $name round $round: cfg4 $(grep -o '"ms[^,]*' gpurun_out/abh_mt_$name.log | head -2 | tr '\n' ' ')"
 done; done
-ROUNDS=1 WL="mixed4k midlarge large huge" timeout -k 10 400 bash tools/ab_variants.sh base hop2 hop1
+ROUNDS=2 WL="mixed4k midlarge large huge" timeout -k 10 400 bash tools/ab_variants.sh base off w12 w24
