@@ -827,12 +827,21 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     in_bytes = sum(sizes)
     n_distinct = int(np.unique(np.concatenate(allkeys)).size)
     exact_ok = None
+    del arena  # the check needs the tables' rows and the output only
+    torch.cuda.empty_cache()
     if want_rows is not None:
         rows = torch.cat(bufs).view(-1, 132)
-        exact_ok = bool(out_len == want_rows.numel() * 132 and torch.equal(
-            out[:out_len], rows.index_select(0, want_rows).view(-1)))
-        del rows, bufs, want_rows
-    del arena, out
+        del bufs
+        exact_ok = out_len == want_rows.numel() * 132
+        step = 1 << 24  # rows per compared slice (no whole-output temporary)
+        for i in range(0, want_rows.numel(), step):
+            if not exact_ok:
+                break
+            j = min(i + step, want_rows.numel())
+            exact_ok = torch.equal(out[i * 132:j * 132], rows.index_select(0, want_rows[i:j]).view(-1))
+        exact_ok = bool(exact_ok)
+        del rows, want_rows
+    del out
     torch.cuda.empty_cache()
     line = {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
             "tables": ntab, "records_per_table": per_table, "input_bytes_per_gpu": in_bytes,
