@@ -394,6 +394,22 @@ def test_compact_entries_fast_and_searched_batches(engine, dups):
     assert np.array_equal(out.blocks, wblocks)
 
 
+def test_compact_many_tables(engine):
+    """70 tables in one compaction: the entry builder's table search over the
+    batched decode's grid, more tables than the last merge round keeps in LDS
+    (FIN_LDS_TABLES = 64), seven rounds; empty tables among them.  Output ==
+    the oracle's compact_inner output, serialized, with its index blocks."""
+    tables = sorted_tables(70, 6000, 0.05, 43, long_prefix=True)
+    tables[5] = []
+    tables[69] = []
+    datas = encode_tables(tables)
+    out = engine.compact_host([d.tobytes() for d in datas], block_stride=5)
+    want, wblocks, wn = oracle.compacted_table(datas, block_stride=5)
+    assert out.status == 0 and out.kind == 0 and out.n == wn
+    assert np.array_equal(out.data, want)
+    assert np.array_equal(out.blocks, wblocks)
+
+
 # ---- epochs: the reference loop cut at the tables' disorder points -----------------------
 def _keyed_tables(sizes, seed, universe=None):
     """Sorted unique 8-byte big-endian keys per table (value = table id)."""
