@@ -341,7 +341,8 @@ def main(argv=None):
         extra["multi_table_decode_cfg4"] = multi_table_leg(torch, eng, device, args, world, rank,
                                                            host=not args.no_host and world == 1)
         extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank,
-                                                         host=not args.no_host and world == 1)
+                                                         host=not args.no_host and world == 1,
+                                                         exact=True)
         extra["compaction_cfg5_share"] = compaction_leg(torch, eng, device, world, rank,
                                                         per_table=8_134_407, exact=True,
                                                         pmc_name="r3_pmc_compaction_share.json")
@@ -351,6 +352,25 @@ def main(argv=None):
         extra["lookups"] = lookup_leg(torch, eng, sst, n, k, v)
     if not args.no_host and world == 1:
         extra["host_inclusive"] = host_leg(torch, eng, sst, n, world)
+
+    if not args.no_extra:
+        # the split across GPUs (§8e) from rank 0 over contexts on devices
+        # 0..N-1 while the other ranks wait; on one GPU, HG_BENCH_MULTI_CTX=G
+        # rehearses it with G contexts sharing the card
+        ctx_env = int(os.environ.get("HG_BENCH_MULTI_CTX", "0"))
+        ndev = torch.cuda.device_count()
+        devices = (list(range(world)) if world > 1 and ndev >= world and
+                   os.environ.get("HG_BENCH_SHARE_GPU") != "1" else
+                   [local] * ctx_env if ctx_env > 1 else None)
+        barrier(world, device)
+        if devices is None:
+            extra["multi_gpu_split"] = {"skipped": "one GPU and HG_BENCH_MULTI_CTX unset"}
+        elif rank == 0:
+            try:
+                extra["multi_gpu_split"] = multi_split_leg(torch, eng, devices)
+            except Exception as e:  # noqa: BLE001 -- a failed leg must not lose the bench line
+                extra["multi_gpu_split"] = {"error": repr(e)}
+        barrier(world, device)
 
     cpu = (cpu_baseline(sst, n, args.cpu_sample_mb, args.cpu_seconds)
            if (rank == 0 and world == 1) else None)
@@ -737,6 +757,111 @@ def multi_table_leg(torch, eng, device, args, world, rank, tables_per_gpu=32, ho
                             "per ~2 KiB record, so this is not an HBM fraction",
             "parity_ok": bool(ok), "parity": "counts, kinds and every span of all tables vs "
                                               "the generated record layout"}
+
+
+def multi_split_leg(torch, eng, devices, ntab=8, per_table=1_000_000, decode_tables=16):
+    """SURVEY §8e's split across GPUs, run from ONE process over contexts on
+    `devices` (rank 0, while the other ranks wait at a barrier): the cfg 5
+    scaled compaction (8 tables x per_table records over the whole key space,
+    table t resident on devices[t % G]) by hg_multi_compact_dev -- splitter
+    keys sampled from every table, each table decoded in place on its owner,
+    every key range's slices gathered to its context by peer copies over
+    xGMI (device copies when two contexts share a GPU), merged and encoded
+    there -- against one context's hg_compact_dev of the same tables: the
+    slices concatenated must equal it byte for byte.  Then cfg 4-shaped
+    tables (64 MiB each, 8 B-4 KiB values) from host memory round-robin over
+    the contexts by hg_multi_decode_host (PCIe-inclusive), spans checked by
+    generator truth.  Wall clock, median of 3."""
+    from horreum_amd import synth
+    from horreum_amd.multi import MultiEngine
+    G = len(devices)
+    dev0 = torch.device("cuda", devices[0])
+    keys = cfg5_rank_keys(0, ntab, per_table)
+    tabs0, owner = [], []
+    for t, k in enumerate(keys):
+        buf, _ = synth.keyed_table(k, np.full(k.size, 100), seed=cfg5_value_seed(0, t), device=dev0)
+        tabs0.append(buf)
+        owner.append(t % G)
+    sizes = [b.numel() for b in tabs0]
+    total = sum(sizes)
+    # reference: one context (device 0), the tables in one arena
+    offs, acc = [], 0
+    for sz in sizes:
+        offs.append(acc)
+        acc += (sz + 7) & ~7
+    arena = torch.zeros(acc, dtype=torch.uint8, device=dev0)
+    for o, b in zip(offs, tabs0):
+        arena[o:o + b.numel()] = b
+    ref = eng.empty(acc)
+    c = eng.compact_dev(arena, offs, sizes, ref)
+    assert c.status == 0, c
+    ref_len = c.data.numel()
+
+    def sync_all():
+        for d in sorted(set(devices)):
+            torch.cuda.synchronize(d)
+
+    def med3(fn):
+        fn()
+        sync_all()
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            r = fn()
+            sync_all()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[1], r
+
+    t_single, _ = med3(lambda: eng.compact_dev(arena, offs, sizes, ref))
+    del arena
+    tabs = [b.to(torch.device("cuda", devices[o])) for b, o in zip(tabs0, owner)]
+    del tabs0
+    outs = [torch.zeros(total, dtype=torch.uint8, device=torch.device("cuda", d)) for d in devices]
+    m = MultiEngine(devices)
+    try:
+        t_multi, (rc, ol, orc, res) = med3(lambda: m.compact_dev(tabs, owner, outs))
+        got_len = sum(int(x) for x in ol)
+        ok = rc == 0 and got_len == ref_len
+        pos = 0
+        for g in range(G):
+            if not ok:
+                break
+            n = int(ol[g])
+            ok = torch.equal(outs[g][:n].to(dev0), ref[pos:pos + n])
+            pos += n
+        slices = [int(x) for x in ol]
+        del tabs, outs
+        torch.cuda.empty_cache()
+        # many tables from host memory, round-robin over the contexts
+        host, layouts = [], []
+        for t in range(decode_tables):
+            v = synth.mixed_table_vlens(64 << 20, 8, 4096, 0.05, seed=4 + t)
+            kk = np.arange(v.size, dtype=np.uint64) * 7 + t
+            buf, offs_t = synth.keyed_table(kk, v, seed=4 + t, device=dev0)
+            host.append(buf.cpu().numpy())
+            layouts.append(synth.span_rows(offs_t[:-1], np.full(v.size, 16), v))
+            del buf
+        hbytes = sum(h.size for h in host)
+        t_dec, douts = med3(lambda: m.decode_tables(host))
+        dec_ok = all(o.kind == 0 and o.n == w.shape[0] and
+                     np.array_equal(o.spans.view("<u8").reshape(-1, 2), w)
+                     for o, w in zip(douts, layouts))
+    finally:
+        m.close()
+    return {"contexts": G, "devices": list(devices),
+            "distinct_gpus": len(set(devices)),
+            "compact": {"api": "hg_multi_compact_dev", "tables": ntab,
+                        "records_per_table": per_table, "input_bytes": total,
+                        "ms": round(t_multi * 1e3, 3),
+                        "GiB_s": round(total / t_multi / GIB, 3),
+                        "single_context_ms": round(t_single * 1e3, 3),
+                        "slice_bytes": slices, "parity_bytes_ok": bool(ok),
+                        "parity": "slices concatenated == one context's hg_compact_dev"},
+            "decode_host": {"api": "hg_multi_decode_host", "tables": decode_tables,
+                            "bytes": hbytes, "ms": round(t_dec * 1e3, 3),
+                            "GiB_s": round(hbytes / t_dec / GIB, 3),
+                            "parity_ok": bool(dec_ok),
+                            "note": "pageable host tables: H2D-bound on each GPU's PCIe link"}}
 
 
 def cfg5_rank_keys(rank, ntab, per_table):

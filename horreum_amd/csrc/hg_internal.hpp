@@ -113,6 +113,20 @@ struct hg_ctx {
 };
 
 namespace hgi {
+// Restores the calling thread's current HIP device on scope exit: the
+// multi-context entry points switch devices on the caller's thread (set_dev,
+// peer enabling), and a caller that allocates next must stay on its own GPU.
+struct DeviceGuard {
+    int dev = -1;
+    DeviceGuard() {
+        if (hipGetDevice(&dev) != hipSuccess) dev = -1;
+    }
+    ~DeviceGuard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+    }
+    DeviceGuard(const DeviceGuard&) = delete;
+    DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
 int set_dev(hg_ctx* c);
 int ensure(hg_ctx* c, DevBuf& b, size_t bytes);
 int ensure_pin(PinBuf& b, size_t bytes);

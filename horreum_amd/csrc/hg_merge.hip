@@ -146,7 +146,10 @@ __device__ __forceinline__ MEnt make_ent(const MergeArgs& a, uint64_t g, uint32_
         const uint32_t tag = reinterpret_cast<const uint32_t*>(a.kp_ptag[t])[piece];
         const hgk::SpecPiece q = reinterpret_cast<const hgk::SpecPiece*>(a.kp_spiece[t])[piece];
         if (tag == a.kp_tag) {
-            if (q.pad == hgk::SP_STRIDE && sp.off >= q.x && q.R) {
+            // the prefix was masked with the piece's key length: it is this
+            // record's only if the record has that length (a piece past a
+            // header mismatch keeps its lattice but not its records)
+            if (q.pad == hgk::SP_STRIDE && sp.off >= q.x && q.R && sp.klen == q.kl) {
                 const uint64_t d = sp.off - q.x, j = d / q.R;
                 if (j * q.R == d && j < q.count) {
                     const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(
@@ -236,7 +239,8 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
         const uint64_t piece = sp[u].off / hgk::PIECE_BYTES;
         const uint32_t tag = reinterpret_cast<const uint32_t*>(a.kp_ptag[tt[u]])[piece];
         const hgk::SpecPiece q = reinterpret_cast<const hgk::SpecPiece*>(a.kp_spiece[tt[u]])[piece];
-        if (tag == a.kp_tag && q.pad == hgk::SP_STRIDE && sp[u].off >= q.x && q.R) {
+        if (tag == a.kp_tag && q.pad == hgk::SP_STRIDE && sp[u].off >= q.x && q.R &&
+            sp[u].klen == q.kl) {  // (a prefix masked with the piece's key length: make_ent)
             const uint64_t d = sp[u].off - q.x, j = d / q.R;
             if (j * q.R == d && j < q.count) pj[u] = (int64_t)(piece * hgk::PIECE_RECS + j);
         }
@@ -293,8 +297,9 @@ __global__ __launch_bounds__(THREADS) void merge_prep_kernel(MergeArgs a, MEnt* 
 
 // ---- 3. one merge round ---------------------------------------------------------------
 struct LevelArgs {
-    const uint64_t* roff;  // [nruns + 1] run offsets of this round's input
-    uint32_t nruns;
+    const uint64_t* roff;  // [nruns + 1] run offsets of this round's input; nullptr:
+    uint32_t nruns;        // runs of uw entries each (the last one short) over un entries
+    uint64_t uw, un;       // (the rank path's sort rounds, section 7)
 };
 
 struct LevelSmem {
@@ -321,6 +326,13 @@ __device__ __forceinline__ uint32_t lds_bound(const MergeArgs& a, const MEnt* s,
 // pair's start o, A/B boundary amid and end oend.
 __device__ __forceinline__ void pair_of(const LevelArgs& l, uint64_t d, uint32_t& pa, uint64_t& o,
                                         uint64_t& amid, uint64_t& oend) {
+    if (!l.roff) {  // uniform runs (scalar arithmetic, no search)
+        pa = (uint32_t)(d / l.uw) & ~1u;
+        o = (uint64_t)pa * l.uw;
+        amid = min(o + l.uw, l.un);
+        oend = min(o + 2 * l.uw, l.un);
+        return;
+    }
     uint32_t lo = 0, hi = l.nruns;
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -992,6 +1004,305 @@ __global__ void merge_flag_kernel(const unsigned long long* err, hg_merge_result
     *result = r;
 }
 
+// ---- 7. rank path: the reference loop on heavily disordered tables ------------------------
+// The loop's only operations on keys are "smallest head" and "equal to it"
+// (manager.rs:209-227), so any order-preserving integer image of the keys runs
+// it exactly.  Dense ranks (the number of distinct keys below a key) are built
+// in parallel -- every entry sorted (tiles of TILE in LDS, then merge-path
+// rounds over uniform runs), equal neighbours sharing a rank -- and the loop
+// itself then runs in ONE wave on 4-byte ranks: lane t holds table t's head
+// and next rank in registers, the smallest head is a DPP min over the lanes,
+// the first table holding it is the lowest set bit of a ballot (min_by_key keeps
+// the first minimum, :209-216), every lane whose head equals it advances
+// (:218-227).  Each table's next ranks stream through an LDS ring of two
+// halves refilled by LDS-DMA with counted waits, so no step waits on HBM; the
+// winners' entry indices go out 64 at a time and a parallel kernel turns them
+// into hg_pairs.  (The round-2 loop, merge_exact_kernel, compared 24-byte
+// entries and chased a global load per step: ~1-2 us per record.)
+constexpr uint32_t RANK_INF = 0xFFFFFFFFu;
+constexpr uint32_t RANK_MAX_TABLES = 64;  // one lane per table
+constexpr uint32_t RANK_LDS = 65536;      // the loop's LDS ring bytes
+constexpr uint32_t RANK_PAD = 4096;       // ranks readable past n (ring fills run up to 2 H + 2 past a table's end)
+
+__device__ __forceinline__ bool ent_is_pad(const MEnt& x) { return x.gd == 0xFFFFFFFFu; }
+
+// x < y in key order; the padding of a short last tile sorts after everything
+__device__ __forceinline__ bool sort_lt(const MergeArgs& a, const MEnt& x, const MEnt& y) {
+    if (ent_is_pad(y)) return !ent_is_pad(x);
+    if (ent_is_pad(x)) return false;
+    return key_cmp(a, x, y) < 0;
+}
+
+// Every TILE entries of `in` sorted by key (bitonic network in LDS; equal keys
+// in any order -- ranks do not depend on it) into `out`.
+__global__ __launch_bounds__(THREADS) void sort_tile_kernel(MergeArgs a, const MEnt* in, MEnt* out) {
+    __shared__ MEnt s[TILE];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+    for (uint32_t i = tid; i < TILE; i += THREADS) {
+        MEnt m;
+        if (t0 + i < a.n) {
+            m = in[t0 + i];
+        } else {
+            m.p0 = m.p1 = ~0ull;
+            m.klen = m.gd = 0xFFFFFFFFu;
+        }
+        s[i] = m;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= TILE; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t q = tid; q < TILE / 2; q += THREADS) {
+                const uint32_t i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i + j;
+                const MEnt x = s[i], y = s[l];
+                const bool up = (i & k) == 0;
+                if (up ? sort_lt(a, y, x) : sort_lt(a, x, y)) {
+                    s[i] = y;
+                    s[l] = x;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = tid; i < TILE && t0 + i < a.n; i += THREADS) out[t0 + i] = s[i];
+}
+
+// Key-change flags of the sorted entries: f = 1 where a key differs from the
+// one before it (the first entry: 1).  Thread tid of a tile owns 4
+// consecutive entries.
+__device__ __forceinline__ uint32_t rank_flags(const MergeArgs& a, const MEnt* srt, uint64_t i0,
+                                               uint32_t f[EPT]) {
+    uint32_t c = 0;
+    MEnt prev;
+    if (i0 > 0 && i0 < a.n) prev = srt[i0 - 1];
+#pragma unroll
+    for (uint32_t u = 0; u < EPT; ++u) {
+        const uint64_t i = i0 + u;
+        f[u] = 0;
+        if (i < a.n) {
+            const MEnt x = srt[i];
+            f[u] = (i == 0 || key_cmp(a, prev, x) != 0) ? 1u : 0u;
+            prev = x;
+        }
+        c += f[u];
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(THREADS) void rank_count_kernel(MergeArgs a, const MEnt* srt,
+                                                             uint32_t* tile_cnt) {
+    __shared__ uint32_t ws[THREADS / 64];
+    uint32_t f[EPT];
+    uint32_t c = rank_flags(a, srt, (uint64_t)blockIdx.x * TILE + threadIdx.x * EPT, f);
+    c = hgk::wave_sum<uint32_t>(c);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t s = 0;
+        for (uint32_t w = 0; w < THREADS / 64; ++w) s += ws[w];
+        tile_cnt[blockIdx.x] = s;
+    }
+}
+
+// rank[g] = distinct keys below entry g's key (g = the entry's index in the
+// tables' layout), from the flags' prefix sums (tile bases from merge_scan_kernel).
+__global__ __launch_bounds__(THREADS) void rank_scatter_kernel(MergeArgs a, const MEnt* srt,
+                                                               const uint64_t* tile_base,
+                                                               uint32_t* rank) {
+    __shared__ uint32_t tmp[THREADS / 64];
+    const uint64_t i0 = (uint64_t)blockIdx.x * TILE + threadIdx.x * EPT;
+    uint32_t f[EPT];
+    const uint32_t c = rank_flags(a, srt, i0, f);
+    uint32_t tot;
+    uint64_t r = tile_base[blockIdx.x] + hgk::block_excl_scan<THREADS / 64>(c, tmp, tot);
+#pragma unroll
+    for (uint32_t u = 0; u < EPT; ++u) {
+        if (i0 + u >= a.n) break;
+        r += f[u];
+        rank[srt[i0 + u].gd & ~DEAD] = (uint32_t)(r - 1);
+    }
+}
+
+// Wave-wide inclusive min by DPP (lane 63 holds the wave's minimum); lanes
+// without a source keep ~0 as the identity.
+__device__ __forceinline__ uint32_t dpp_min_incl(uint32_t v) {
+#define HG_DPP_MIN(ctrl, rmask) \
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)RANK_INF, (int)v, ctrl, rmask, 0xf, false))
+    HG_DPP_MIN(0x111, 0xf);
+    HG_DPP_MIN(0x112, 0xf);
+    HG_DPP_MIN(0x114, 0xf);
+    HG_DPP_MIN(0x118, 0xf);
+    HG_DPP_MIN(0x142, 0xa);
+    HG_DPP_MIN(0x143, 0xc);
+#undef HG_DPP_MIN
+    return v;
+}
+
+// s_waitcnt vmcnt(min(n, 8)): this wave's vector memory operations retire in
+// issue order, so "at most n outstanding" covers every one issued n or more
+// operations ago (fewer allowed is merely conservative).
+__device__ __forceinline__ void rank_wait_vm(uint32_t n) {
+    switch (n) {
+        case 0: __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: __asm__ volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
+        case 2: __asm__ volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
+        case 3: __asm__ volatile("s_waitcnt vmcnt(3)" ::: "memory"); break;
+        case 4: __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
+        case 5: __asm__ volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
+        case 6: __asm__ volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+        case 7: __asm__ volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
+        default: __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    }
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+    return ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), l) << 32) |
+           __builtin_amdgcn_readlane((uint32_t)v, l);
+}
+
+struct RankArgs {
+    const uint32_t* rank;     // dense rank per entry (tables' layout), RANK_PAD readable past n
+    const uint64_t* run_off;  // [ntables + 1]
+    uint32_t ntables;         // <= RANK_MAX_TABLES
+    uint32_t H;               // ranks per ring half: a power of two >= 128, 2 H ntables 4 B <= RANK_LDS
+    const uint64_t* start;    // [ntables] heads to start from (table-local)
+    uint32_t* win_idx;        // out: the winners' entry indices, in output order
+    uint64_t* steps;          // out: the number of winners
+};
+
+// One half of table t's ring (ranks [q, q + H) of the table) by LDS-DMA; the
+// whole wave issues it (wave-uniform LDS base, one 16-byte piece per lane).
+// Returns the vector memory instructions issued.
+__device__ __forceinline__ uint32_t rank_fill(const RankArgs& r, uint32_t* ring_half,
+                                              const uint32_t* src) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lanes = min(64u, r.H / 4), nins = max(1u, r.H / 256);
+    for (uint32_t q = 0; q < nins; ++q)
+        if (lane < lanes)
+            __builtin_amdgcn_global_load_lds(static_cast<const void*>(src + q * 256 + lane * 4),
+                                             (__attribute__((address_space(3))) void*)(ring_half + q * 256),
+                                             16, 0, 0);
+    return nins;
+}
+
+__global__ __launch_bounds__(64) void rank_merge_kernel(RankArgs r) {
+    extern __shared__ uint32_t ring[];  // [ntables][2][H]
+    const uint32_t lane = threadIdx.x;
+    const uint32_t H = r.H, hs = (uint32_t)__builtin_ctz(H), RM = 2 * H - 1;
+    const bool mine = lane < r.ntables;
+    // positions are table-local u32 (a merge holds < 2^31 entries)
+    const uint32_t base = mine ? (uint32_t)r.run_off[lane] : 0u;
+    const uint32_t cnt = mine ? (uint32_t)r.run_off[lane + 1] - base : 0u;
+    uint32_t idx = mine ? (uint32_t)min(r.start[lane], (uint64_t)cnt) : 0u;
+    uint32_t hr = idx < cnt ? r.rank[base + idx] : RANK_INF;
+    uint32_t hn = idx + 1 < cnt ? r.rank[base + idx + 1] : RANK_INF;
+    const uint32_t* my = ring + lane * 2 * H;
+    // the ring holds the table's ranks [b H, (b + 2) H) around the next read
+    // position idx + 2 (slot = position mod 2H); both halves now, waited for
+    for (uint32_t t = 0; t < r.ntables; ++t) {
+        const uint32_t bt = __builtin_amdgcn_readlane(base, t), it = __builtin_amdgcn_readlane(idx, t);
+        const uint32_t b = (it + 2) >> hs;
+        uint32_t* rt = ring + t * 2 * H;
+        rank_fill(r, rt + (b & 1u) * H, r.rank + bt + ((uint64_t)b << hs));
+        rank_fill(r, rt + ((b + 1) & 1u) * H, r.rank + bt + ((uint64_t)(b + 1) << hs));
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t vm = 0;            // vector memory instructions issued since (wave-uniform)
+    uint32_t tk0 = 0, tk1 = 0;  // per half: vm right after its last refill was issued
+    uint32_t gidx = base + idx;
+    uint32_t ob = 0, pv = 0, ps = 0;
+    bool pf = false;
+    uint64_t j = 0;
+    for (;;) {
+        const uint32_t minr = __builtin_amdgcn_readlane(dpp_min_incl(hr), 63);
+        if (minr == RANK_INF) break;  // every table exhausted (:228-230)
+        const uint64_t m = __ballot(hr == minr);
+        const uint32_t w = (uint32_t)__builtin_ctzll(m);  // first table holding it
+        const uint32_t gw = __builtin_amdgcn_readlane(gidx, w);
+        const uint32_t jl = (uint32_t)j & 63u;
+        ob = lane == jl ? gw : ob;
+        if (jl == 63) {
+            r.win_idx[j - 63 + lane] = ob;
+            ++vm;
+        }
+        ++j;
+        // every table whose head equals the winner's key advances
+        // (the next rank is pv when pf -- an LDS read issued last step, first
+        // used here, so its latency hides behind this step's reduction -- else hn)
+        const bool adv = (m >> lane) & 1ull;
+        if (adv) {
+            ++idx;
+            ++gidx;
+            hr = pf ? pv : hn;
+        }
+        const uint32_t p = idx + 1;  // the next rank to read
+        const bool need = adv && p < cnt;
+        const uint64_t cm = __ballot(need && (p & (H - 1)) == 0);
+        if (cm) {  // lanes entering a new half: it must have landed; refill the one left
+            const uint32_t h = (p >> hs) & 1u;
+            const uint32_t tkh = h ? tk1 : tk0;
+            uint32_t allowed = RANK_INF;
+            for (uint64_t c = cm; c; c &= c - 1)
+                allowed = min(allowed, vm - __builtin_amdgcn_readlane(tkh, (uint32_t)__builtin_ctzll(c)));
+            rank_wait_vm(allowed);
+            for (uint64_t c = cm; c; c &= c - 1) {
+                const uint32_t t = (uint32_t)__builtin_ctzll(c);
+                const uint32_t bt = __builtin_amdgcn_readlane(base, t), pt = __builtin_amdgcn_readlane(p, t);
+                const uint32_t th = (pt >> hs) & 1u;
+                vm += rank_fill(r, ring + t * 2 * H + (th ^ 1u) * H, r.rank + bt + pt + H);
+                if (lane == t) {
+                    if (th) tk0 = vm;
+                    else tk1 = vm;
+                }
+            }
+        }
+        if (need) {
+            ps = p & RM;
+            pf = true;
+        } else if (adv) {
+            hn = RANK_INF;
+            pf = false;
+        }
+        // every lane reads its pending slot (a lane that did not advance gets
+        // the same rank again: its half is refilled only once it has left it),
+        // so the read lands in pv's own register and is first waited for at the
+        // next step's advance, not here
+        pv = my[ps];
+    }
+    const uint32_t jl = (uint32_t)j & 63u;
+    if (jl && lane < jl) r.win_idx[j - jl + lane] = ob;
+    if (lane == 0) *r.steps = j;
+}
+
+// The winners (entry indices in output order) -> hg_pairs at out[i], i <
+// *steps and i < cap; the last thread of the grid's first workgroup writes the result.
+__global__ __launch_bounds__(THREADS) void rank_emit_kernel(MergeArgs a, const uint32_t* win_idx,
+                                                            const uint64_t* steps, hg_pair* out,
+                                                            uint64_t cap, uint64_t n0,
+                                                            hg_merge_result* result) {
+    const uint64_t ns = *steps;
+    const uint64_t i = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
+    if (i == 0) {
+        hg_merge_result res;
+        res.n_out = n0 + ns;
+        res.kind = HG_OK;
+        res.table = 1;  // on success: 1 = the serial reference loop produced the output
+        res.index = 0;
+        *result = res;
+    }
+    if (i >= ns || n0 + i >= cap) return;
+    MEnt e;
+    e.gd = win_idx[i];
+    uint32_t t;
+    const hg_span sp = ent_span(a, e, t);
+    hg_pair p;
+    p.key_off = a.table_off[t] + sp.off + 16;
+    p.val_off = p.key_off + sp.klen;
+    p.klen = sp.klen;
+    p.vlen = sp.vlen;
+    out[n0 + i] = p;
+}
+
 }  // namespace hgm
 
 // ---- launcher ----------------------------------------------------------------------------
@@ -1020,6 +1331,9 @@ struct MergeWs {
     uint64_t* ep;                   // 4 * ntables: candidates, lo, hi, u
     uint64_t* ep_roff;              // an epoch's round offsets
     hg_merge_result* ep_res;
+    uint32_t* rank;                 // the rank path: a dense rank per entry (+ RANK_PAD)
+    uint32_t* win_idx;              // its winners' entry indices
+    uint64_t* rank_steps;           // its winner count
     uint64_t bytes;
 };
 MergeWs merge_ws(void* d_ws, uint32_t ntables, uint64_t n) {
@@ -1056,6 +1370,12 @@ MergeWs merge_ws(void* d_ws, uint32_t ntables, uint64_t n) {
     w.ep_roff = reinterpret_cast<uint64_t*>(p);
     p += al256(stage);
     w.ep_res = reinterpret_cast<hg_merge_result*>(p);
+    p += 256;
+    w.rank = reinterpret_cast<uint32_t*>(p);
+    p += al256((n + RANK_PAD) * 4);
+    w.win_idx = reinterpret_cast<uint32_t*>(p);
+    p += al256(n * 4 + 256);
+    w.rank_steps = reinterpret_cast<uint64_t*>(p);
     p += 256;
     w.bytes = (uint64_t)(p - base);
     return w;
@@ -1097,6 +1417,7 @@ int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hg
             LevelArgs l;
             l.roff = roff;
             l.nruns = (uint32_t)nr;
+            l.uw = l.un = 0;
             // tile_base is free in the rounds: the round's splits
             const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
             hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
@@ -1132,6 +1453,79 @@ int sync_copy(void* dst, const void* src, size_t n, hipMemcpyKind k, hipStream_t
     if (hipMemcpyAsync(dst, src, n, k, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess)
         return HG_HIP_FAIL;
     return HG_OK;
+}
+
+// The rank path (section 7) over the entries in w.e0: dense ranks (tiles
+// sorted in LDS, merge rounds over uniform runs, key-change flags scanned),
+// then the reference loop in one wave from the heads `start` (host,
+// table-local; nullptr: every table from its first record) with n0 records
+// already emitted, the pairs to d_out[n0, cap).  ntables <= RANK_MAX_TABLES.
+// Synchronous; the result goes to d_result and *h_result.
+int rank_path(const hgm::MergeArgs& a, const MergeWs& w, const uint64_t* start, uint64_t n0,
+              hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, hg_merge_result* h_result,
+              uint64_t* h, hipStream_t stream) {
+    using namespace hgm;
+    const uint32_t k = a.ntables;
+    const uint64_t n = a.n;
+    if (k > RANK_MAX_TABLES || n == 0) return HG_ERR_INTERNAL;
+    const uint64_t ntiles = (n + TILE - 1) / TILE;
+    unsigned long long* serr = w.dis_count + 1;  // the sort rounds' order word (sorted runs: stays ~0)
+    if (hipMemsetAsync(serr, 0xFF, 8, stream) != hipSuccess) return HG_HIP_FAIL;
+    hipLaunchKernelGGL(sort_tile_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)w.e0, w.e1);
+    MEnt* cur = w.e1;
+    MEnt* nxt = w.e2;
+    FinalArgs fa{};
+    for (uint64_t uw = TILE; uw < n; uw *= 2) {
+        LevelArgs l;
+        l.roff = nullptr;
+        l.nruns = (uint32_t)((n + uw - 1) / uw);
+        l.uw = uw;
+        l.un = n;
+        const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
+        hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
+                           (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)serr);
+        hipLaunchKernelGGL(merge_level_kernel<false>, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream,
+                           a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base, serr, fa);
+        std::swap(cur, nxt);
+    }
+    hipLaunchKernelGGL(rank_count_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)cur, w.tile_live);
+    hipLaunchKernelGGL(merge_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)w.tile_live,
+                       (uint32_t)ntiles, w.tile_base, w.ep_res);
+    hipLaunchKernelGGL(rank_scatter_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
+                       (const MEnt*)cur, (const uint64_t*)w.tile_base, w.rank);
+    int rc = HG_LAUNCH_STATUS();
+    if (rc != HG_OK) return rc;
+    uint64_t done = 0;
+    for (uint32_t t = 0; t < k; ++t) {
+        h[t] = start ? start[t] : 0;
+        done += h[t];
+    }
+    if (hipMemcpyAsync(w.ep, h, (uint64_t)k * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
+        return HG_HIP_FAIL;
+    uint32_t H = 1024;  // ranks per ring half: both halves of every table in RANK_LDS
+    while (H > 128 && (uint64_t)k * 2 * H * 4 > RANK_LDS) H >>= 1;
+    RankArgs ra;
+    ra.rank = w.rank;
+    ra.run_off = a.run_off;
+    ra.ntables = k;
+    ra.H = H;
+    ra.start = w.ep;
+    ra.win_idx = w.win_idx;
+    ra.steps = w.rank_steps;
+    hipLaunchKernelGGL(rank_merge_kernel, dim3(1), dim3(64), (size_t)k * 2 * H * 4, stream, ra);
+    const uint64_t left = n > done ? n - done : 1;
+    hipLaunchKernelGGL(rank_emit_kernel, dim3((uint32_t)((left + THREADS - 1) / THREADS)), dim3(THREADS),
+                       0, stream, a, (const uint32_t*)w.win_idx, (const uint64_t*)w.rank_steps, d_out,
+                       cap, n0, d_result);
+    if ((rc = HG_LAUNCH_STATUS()) != HG_OK) return rc;
+    unsigned long long e = 0;
+    if ((rc = sync_copy(&e, serr, 8, hipMemcpyDeviceToHost, stream)) != HG_OK ||
+        (rc = sync_copy(h_result, d_result, sizeof(hg_merge_result), hipMemcpyDeviceToHost, stream)) !=
+            HG_OK)
+        return rc;
+    return e == ~0ull ? HG_OK : HG_ERR_INTERNAL;
 }
 }  // namespace
 
@@ -1290,18 +1684,40 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
         *h_result = res;
         return sync_copy(d_result, h_result, sizeof res, hipMemcpyHostToDevice, stream);
     };
+    // The reference loop itself from heads hd (host, table-local; nullptr:
+    // the tables' first records) with n0 records emitted: the rank path (one
+    // wave over dense ranks) for up to RANK_MAX_TABLES tables, else the
+    // round-2 loop over entries.  HG_MERGE_SERIAL=exact forces the latter (A/B).
+    const char* serial_env = getenv("HG_MERGE_SERIAL");
+    const bool exact_loop = serial_env && strcmp(serial_env, "exact") == 0;
+    auto serial = [&](const uint64_t* hd0, uint64_t n0) -> int {
+        if (ntables <= RANK_MAX_TABLES && !exact_loop)
+            return rank_path(a, w, hd0, n0, d_out, cap, d_result, h_result, h, stream);
+        const uint64_t* dstart = nullptr;
+        if (hd0) {
+            for (uint32_t t = 0; t < ntables; ++t) h[t] = hd0[t];
+            if (hipMemcpyAsync(w.ep, h, (uint64_t)ntables * 8, hipMemcpyHostToDevice, stream) !=
+                hipSuccess)
+                return HG_HIP_FAIL;
+            dstart = w.ep;
+        }
+        hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)w.e0,
+                           (const unsigned long long*)w.err, w.heads, d_out, cap, d_result, dstart, n0);
+        int r2 = HG_LAUNCH_STATUS();
+        if (r2 != HG_OK) return r2;
+        return sync_copy(h_result, d_result, sizeof(hg_merge_result), hipMemcpyDeviceToHost, stream);
+    };
     // D == 0: the tables are strictly increasing after all -- the error word
     // came from a look-back wait over its budget (contention), not from the
     // order check -- and the one epoch below is the whole merge again.
-    // an epoch costs a few launches and host round trips (~0.1-0.2 ms), the
-    // serial loop ~1-2 us per record: many disorder points -> the serial loop
-    if (D > EPOCH_MAX_DISORDER || D > n / 128 + 1 || getenv("HG_MERGE_SERIAL")) {  // (A/B: serial)
-        hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)w.e0,
-                           (const unsigned long long*)w.err, w.heads, d_out, cap, d_result,
-                           (const uint64_t*)nullptr, (uint64_t)0);
-        if ((rc = HG_LAUNCH_STATUS()) != HG_OK) return rc;
-        return sync_copy(h_result, d_result, sizeof(hg_merge_result), hipMemcpyDeviceToHost, stream);
-    }
+    // an epoch costs a few launches and host round trips (~0.1-0.2 ms): many
+    // disorder points -> the serial loop
+    if (D > EPOCH_MAX_DISORDER || D > n / 128 + 1 || serial_env) return serial(nullptr, 0);
+    // test hook: epoch number HG_MERGE_TEST_EPOCH_FAIL reports a failure after
+    // it ran (as a look-back wait over its budget would), so the hand-over to
+    // the serial loop from the epochs' heads is exercised
+    const char* fail_env = getenv("HG_MERGE_TEST_EPOCH_FAIL");
+    const long fail_at = fail_env ? strtol(fail_env, nullptr, 10) : -1;
     std::vector<uint64_t> dl(D);
     if ((rc = sync_copy(dl.data(), w.dis_list, D * 8, hipMemcpyDeviceToHost, stream)) != HG_OK)
         return rc;
@@ -1349,7 +1765,7 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
         h[0] = 0;
         for (uint32_t t = 0; t < ntables; ++t) {
             const uint64_t len = u[t] - hd[t];
-            if (u[t] < hd[t] || u[t] > f[t]) return HG_ERR_INTERNAL;
+            if (u[t] < hd[t] || u[t] > f[t]) return serial(hd.data(), N);  // (never on a sound bound)
             if (!len) continue;
             if (hipMemcpyAsync(w.e1 + ne, w.e0 + ro[t] + hd[t], len * sizeof(MEnt),
                                hipMemcpyDeviceToDevice, stream) != hipSuccess)
@@ -1357,7 +1773,7 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
             ne += len;
             h[++nre] = ne;
         }
-        if (!ne) return HG_ERR_INTERNAL;  // every epoch consumes a disorder point
+        if (!ne) return serial(hd.data(), N);  // every epoch consumes a disorder point
         const uint64_t words = round_offsets(h, nre);
         if (words * 8 > hgk_merge_staging_bytes(ntables)) return HG_ERR_INTERNAL;
         if (hipMemcpyAsync(w.ep_roff, h, words * 8, hipMemcpyHostToDevice, stream) != hipSuccess ||
@@ -1379,7 +1795,10 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
         if ((rc = sync_copy(&er.r, w.ep_res, sizeof er.r, hipMemcpyDeviceToHost, stream)) != HG_OK ||
             (rc = sync_copy(&er.e, ep_err, 8, hipMemcpyDeviceToHost, stream)) != HG_OK)
             return rc;
-        if (er.e != ~0ull || er.r.kind != HG_OK) return HG_ERR_INTERNAL;
+        // a look-back wait over its budget (a stalled or shared GPU) or any
+        // other failure of the epoch: the serial loop takes over from its
+        // heads, overwriting whatever pairs the epoch left past N
+        if (er.e != ~0ull || er.r.kind != HG_OK || (long)epochs == fail_at) return serial(hd.data(), N);
         N += er.r.n_out;
         for (uint32_t t = 0; t < ntables; ++t) hd[t] = u[t];
         ++epochs;

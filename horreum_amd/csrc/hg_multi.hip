@@ -263,6 +263,7 @@ int hg_multi_decode_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
                          const uint8_t* const* h_tables, const uint64_t* lens,
                          hg_span* const* h_spans, const uint64_t* caps, uint64_t* n_out,
                          hg_err* errs) {
+    DeviceGuard keep;  // every device switch below is undone on return
     if (!ctxs || !nctx || (ntables && (!h_tables || !lens || !h_spans || !caps || !n_out)))
         return HG_ERR_INVALID_ARG;
     for (uint32_t i = 0; i < nctx; ++i)
@@ -303,6 +304,7 @@ int hg_multi_decode_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
 int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx, const uint8_t* h_sst,
                               uint64_t len, hg_span* h_spans, uint64_t cap, uint64_t* n_out,
                               hg_err* err) {
+    DeviceGuard keep;  // every device switch below is undone on return
     if (!ctxs || !nctx || (len && !h_sst) || (cap && !h_spans)) return HG_ERR_INVALID_ARG;
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
     for (uint32_t i = 0; i < nctx; ++i)
@@ -427,6 +429,8 @@ int copy_dev(hg_ctx* c, void* dst, int src_dev, const void* src, size_t n) {
 // Direct peer access between every pair of the contexts' devices where the
 // hardware allows it (xGMI); copies work without it too (staged by the runtime).
 void enable_peers(hg_ctx* const* ctxs, uint32_t nctx) {
+    // hipSetDevice below is per thread: the caller's device comes back on return
+    DeviceGuard keep;
     for (uint32_t i = 0; i < nctx; ++i)
         for (uint32_t j = 0; j < nctx; ++j) {
             const int a = ctxs[i]->device, b = ctxs[j]->device;
@@ -653,9 +657,9 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
         uint64_t enc = 0;
         rr = rt_encode_dev(c, arena, static_cast<const hg_pair*>(c->mpairs.p), mr.n_out, dst, cap,
                            static_cast<uint64_t*>(c->d_aux.p), 0, nullptr, &enc, true);
-        if (rr != HG_OK) return rr;
+        // the slice's size also on HG_ERR_CAPACITY, so the caller can resize and retry
         O[g].bytes = enc;
-        return (int)HG_OK;
+        return rr;
     });
     if (r != HG_OK) return r;
     for (const RangeOut& o : O)
@@ -671,6 +675,7 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
                           const uint8_t* const* h_tables, const uint64_t* lens, uint8_t* h_out,
                           uint64_t cap, uint64_t* out_len, uint32_t block_stride,
                           hg_block* h_blocks, hg_merge_result* result) {
+    DeviceGuard keep;  // every device switch below is undone on return
     if (!ctxs || !nctx || (ntables && (!h_tables || !lens)) || (cap && !h_out))
         return HG_ERR_INVALID_ARG;
     if (h_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;
@@ -749,6 +754,7 @@ int hg_multi_compact_dev(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
                          const uint32_t* owner, const uint8_t* const* d_tables,
                          const uint64_t* lens, uint8_t* const* d_outs, const uint64_t* caps,
                          uint64_t* out_lens, uint64_t* out_recs, hg_merge_result* result) {
+    DeviceGuard keep;  // every device switch below is undone on return
     if (!ctxs || !nctx || !d_outs || !caps || !out_lens || !out_recs ||
         (ntables && (!owner || !d_tables || !lens)))
         return HG_ERR_INVALID_ARG;

@@ -161,23 +161,37 @@ class _ResidentLRU:
         self.items = OrderedDict()  # id(table) -> (weakref(table), bytes)
         self.total = 0
 
+    def _forget(self, key, ref):
+        """Weakref callback: a table collected without release() leaves."""
+        item = self.items.get(key)
+        if item is not None and item[0] is ref:
+            del self.items[key]
+            self.total -= item[1]
+
     def touch(self, table, nbytes):
         key = id(table)
-        if key in self.items:
+        item = self.items.get(key)
+        if item is not None and item[0]() is table:
             self.items.move_to_end(key)
             return
-        self.items[key] = (weakref.ref(table), nbytes)
+        if item is not None:  # a dead table's id reused: its entry is stale
+            del self.items[key]
+            self.total -= item[1]
+        self.items[key] = (weakref.ref(table, lambda r, k=key: self._forget(k, r)), nbytes)
         self.total += nbytes
         while self.total > self.budget and len(self.items) > 1:
             _, (ref, b) = self.items.popitem(last=False)
             self.total -= b
             old = ref()
-            if old is not None:
+            # only the state this engine holds: a table that moved to another
+            # engine keeps that engine's resident copy
+            if old is not None and old._resident is not None and _LRUS.get(old._resident[0]) is self:
                 old._resident = None
 
     def drop(self, table):
-        item = self.items.pop(id(table), None)
-        if item is not None:
+        item = self.items.get(id(table))
+        if item is not None and item[0]() is table:
+            del self.items[id(table)]
             self.total -= item[1]
 
 
@@ -251,6 +265,9 @@ class SSTable:
         from .engine import default_engine
         eng = engine or default_engine()
         if self._resident is None or self._resident[0] is not eng:
+            if self._resident is not None:  # an engine switch: leave the old engine's LRU
+                _lru(self._resident[0]).drop(self)
+                self._resident = None
             data = self.file.read_bytes(eng)
             rt = eng.resident_table(data)
             if rt.kind != 0:

@@ -497,3 +497,106 @@ def test_merge_epochs_then_compact(engine):
     assert out.status == 0 and out.n == wn and out.table == 2
     assert np.array_equal(out.data, want)
     assert np.array_equal(out.blocks, wblocks)
+
+
+# ---- the rank path: the reference loop in one wave over dense key ranks ------------------
+def _shuffled_keyed(sizes, seed, dup_frac=0.0, modes=None, universe=None):
+    """Keyed tables (8-byte big-endian keys, value = table id), each shuffled,
+    reversed or left sorted per `modes`, with a fraction of its keys repeated
+    inside the table (duplicates the loop advances together)."""
+    keys = _keyed_tables(sizes, seed, universe=universe)
+    rng = np.random.default_rng(seed + 1000)
+    out = []
+    for t, k in enumerate(keys):
+        k = list(k)
+        if dup_frac and k:
+            k += [k[i] for i in rng.integers(0, len(k), int(len(k) * dup_frac))]
+        mode = (modes or ["shuffle"] * len(keys))[t]
+        if mode == "shuffle":
+            rng.shuffle(k)
+        elif mode == "reverse":
+            k = k[::-1]
+        elif mode == "sorted":
+            k = sorted(k)
+        out.append(_encode_keyed(np.array(k, dtype=np.uint64), t))
+    return out
+
+
+def _rank_case(engine, datas, table=1):
+    res, got, _, offs = device_merge(engine, datas)
+    want, rc = oracle_merge_pairs(datas, offs)
+    assert rc == 0 and res.status == 0 and res.n == want.size
+    assert np.array_equal(got, want)
+    assert res.table == table
+    return res
+
+
+@pytest.mark.parametrize("sizes,dup,seed", [
+    ([20_000] * 8, 0.0, 61),                    # cfg 5's shape, shuffled, 8 lanes, H 1024
+    ([5_000, 1, 0, 2, 7_000, 1_023, 1_024, 1_025], 0.1, 62),  # ring edges, empty and tiny tables
+    ([300] * 64, 0.2, 63),                      # 64 tables: one per lane, H 128 (32-lane fills)
+    ([70_000, 3], 0.3, 64),                     # one long table against a short one
+])
+def test_rank_path_shuffled(engine, sizes, dup, seed):
+    """Tables far from sorted (every other record a disorder point): the
+    reference loop (manager.rs:199-234) over dense ranks in one wave, record
+    for record the oracle's."""
+    _rank_case(engine, _shuffled_keyed(sizes, seed, dup_frac=dup))
+
+
+def test_rank_path_mixed_and_long_prefixes(engine):
+    """Sorted, shuffled and reversed tables together, keys sharing their
+    first 16+ bytes (the sort and the rank flags compare key tails in HBM),
+    tombstones, within-table duplicates."""
+    rng = np.random.default_rng(65)
+    tables = sorted_tables(6, 9000, 0.5, 65, long_prefix=True)
+    for t in (1, 3):
+        rng.shuffle(tables[t])
+    tables[4] = tables[4][::-1] + tables[4][:200]
+    _exact_case(engine, tables)
+
+
+def test_rank_path_equals_exact_loop(engine, monkeypatch):
+    """HG_MERGE_SERIAL=exact runs the round-2 loop over 24-byte entries:
+    both loops give the oracle's output on the same input."""
+    datas = _shuffled_keyed([3_000, 2_000, 2_500], 66, dup_frac=0.2)
+    _rank_case(engine, datas)
+    monkeypatch.setenv("HG_MERGE_SERIAL", "exact")
+    _rank_case(engine, datas)
+
+
+@pytest.mark.parametrize("fail_at", [0, 1, 3])
+def test_epoch_failure_hands_over_to_the_loop(engine, monkeypatch, fail_at):
+    """an epoch that fails (a look-back wait over its budget on a
+    shared card, forced here by HG_MERGE_TEST_EPOCH_FAIL) no longer fails the
+    merge: the serial loop resumes from the epochs' heads and record count."""
+    sizes = [120_000, 50_000, 80_000, 20_000, 60_000, 90_000]
+    keys = _keyed_tables(sizes, seed=52, universe=400_000)
+    rng = np.random.default_rng(53)
+    datas = [_encode_keyed(k, t, swap_at=int(rng.integers(1, k.size - 2)))
+             for t, k in enumerate(keys)]
+    monkeypatch.setenv("HG_MERGE_TEST_EPOCH_FAIL", str(fail_at))
+    _rank_case(engine, datas, table=1)
+
+
+def test_rank_path_over_64_tables_uses_the_entry_loop(engine):
+    """More tables than lanes: the round-2 loop over entries (still exact)."""
+    datas = _shuffled_keyed([40] * 70, 67, dup_frac=0.2)
+    _rank_case(engine, datas)
+
+
+def test_rank_path_8x250k_shuffled_timed(engine):
+    """8 x 250 k fully shuffled records, 25 % of the keys in every table:
+    exact, and far below the round-2 loop's ~1-2 us per record."""
+    import time
+    import torch
+    datas = _shuffled_keyed([250_000] * 8, 68, universe=1_000_000)
+    device_merge(engine, datas)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res, got, _, offs = device_merge(engine, datas)
+    dt = time.perf_counter() - t0
+    want, rc = oracle_merge_pairs(datas, offs)
+    assert rc == 0 and res.status == 0 and res.table == 1
+    assert res.n == want.size and np.array_equal(got, want)
+    assert dt < 0.5, dt  # the round-2 loop: ~2-4 s

@@ -271,3 +271,88 @@ def test_two_contexts_two_threads():
     for t in th:
         t.join()
     assert not errors, errors
+
+
+def test_compact_dev_capacity_reports_slice_sizes(engine, multi2):
+    """A slice that does not fit its caller buffer: HG_ERR_CAPACITY with every
+    slice's size in out_lens (the overflowing one included), so the caller can
+    resize and call again; the retry is byte-identical to one context's
+    compaction."""
+    import torch
+    from horreum_amd.abi import Status
+    tables = sorted_tables(4, 8000, 0.4, 47)
+    datas = [d for d in encode_tables(tables)]
+    dev = [torch.from_numpy(d.copy()).to("cuda:0") for d in datas]
+    small = [torch.zeros(64, dtype=torch.uint8, device="cuda:0") for _ in range(2)]
+    torch.cuda.synchronize()
+    rc, ol, _, _ = multi2.compact_dev(dev, [0, 1, 0, 1], small)
+    assert rc == Status.CAPACITY
+    assert all(x > 64 for x in ol), ol  # both slices report what they need
+    outs = [torch.zeros(int(x), dtype=torch.uint8, device="cuda:0") for x in ol]
+    rc, ol2, orc, _ = multi2.compact_dev(dev, [0, 1, 0, 1], outs)
+    torch.cuda.synchronize()
+    assert rc == 0 and list(ol2) == list(ol)
+    single = engine.compact_host([d.tobytes() for d in datas])
+    got = np.concatenate([outs[g][:ol2[g]].cpu().numpy() for g in range(2)])
+    assert np.array_equal(got, single.data) and sum(orc) == single.n
+
+
+# ---- contexts on distinct devices (skipped on a one-GPU box) -----------------------------
+@pytest.mark.skipif("not __import__('torch').cuda.device_count() >= 2",
+                    reason="needs two GPUs: the peer-copy branch of the split")
+@pytest.mark.parametrize("seed", [51, 52])
+def test_compact_dev_across_devices(engine, seed):
+    """hg_multi_compact_dev with contexts on devices 0 and 1: each table
+    resident on its owner's GPU, key-range slices gathered by peer copies
+    (hipMemcpyPeerAsync over xGMI), slice g written on device g; byte-identical
+    to one context's compaction.  The caller's current device is unchanged."""
+    import torch
+    from horreum_amd.multi import MultiEngine
+    m = MultiEngine([0, 1])
+    try:
+        tables = sorted_tables(6, 20000, 0.3, seed)
+        datas = [d for d in encode_tables(tables)]
+        owner = [t % 2 for t in range(len(datas))]
+        dev = [torch.from_numpy(d.copy()).to("cuda:%d" % o) for d, o in zip(datas, owner)]
+        total = sum(d.size for d in datas)
+        outs = [torch.zeros(total, dtype=torch.uint8, device="cuda:%d" % g) for g in range(2)]
+        torch.cuda.set_device(0)
+        for g in range(2):
+            torch.cuda.synchronize(g)
+        rc, ol, orc, res = m.compact_dev(dev, owner, outs)
+        assert torch.cuda.current_device() == 0
+        for g in range(2):
+            torch.cuda.synchronize(g)
+        single = engine.compact_host([d.tobytes() for d in datas])
+        got = np.concatenate([outs[g][:ol[g]].cpu().numpy() for g in range(2)])
+        assert rc == 0 and np.array_equal(got, single.data) and sum(orc) == single.n
+        assert all(ol)  # really split across the two GPUs
+        split = m.compact([d.tobytes() for d in datas], block_stride=7)
+        ref = engine.compact_host([d.tobytes() for d in datas], block_stride=7)
+        assert split.status == 0 and np.array_equal(split.data, ref.data)
+        assert np.array_equal(split.blocks, ref.blocks)
+    finally:
+        m.close()
+
+
+@pytest.mark.skipif("not __import__('torch').cuda.device_count() >= 2",
+                    reason="needs two GPUs")
+def test_decode_tables_across_devices_keeps_caller_device():
+    """Tables round-robin over contexts on devices 0 and 1 (cfg 4's split):
+    every table's spans equal the oracle's, and the calling thread is left on
+    the device it was on (the driver switches devices on the caller's thread)."""
+    import torch
+    from horreum_amd.multi import MultiEngine
+    m = MultiEngine([1, 0])
+    try:
+        names = ["fixed_16_100", "mixed_small", "mixed_4k", "tiny"]
+        datas = [corpus.make(nm)[2] for nm in names]
+        torch.cuda.set_device(1)
+        outs = m.decode_tables(datas)
+        assert torch.cuda.current_device() == 1
+        for d, o in zip(datas, outs):
+            want, wn, wk, _, _ = oracle.decode(d)
+            assert (o.n, o.kind) == (wn, wk) and np.array_equal(o.spans, want)
+    finally:
+        torch.cuda.set_device(0)
+        m.close()
