@@ -11,6 +11,7 @@ namespace hgk {
 
 constexpr uint64_t V40 = (1ull << 40) - 1;  // 40-bit positions/counts in status words
 
+
 // Decode pieces and their pre-pass records (hg_decode.hip), shared with the
 // merge's entry builder (hg_merge.hip), which takes key prefixes the decode
 // pre-pass left in the span scratch of stride pieces (compaction mode).

@@ -283,8 +283,8 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
     constexpr uint32_t U = NTL ? ENC_U : ENC_U_GATHER;
     __shared__ EncodeSmem s;
     const uint32_t tid = threadIdx.x;
-    const uint32_t t = blockIdx.x;
     a.n = enc_count(a.n, a.n_dev);
+    const uint32_t t = blockIdx.x;
     if ((uint64_t)t * ENC_TILE >= a.n) return;  // grid sized for the upper bound
     const uint64_t r0 = (uint64_t)t * ENC_TILE + (uint64_t)tid * ENC_RPT;  // this thread's records
 
@@ -482,8 +482,8 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_records_kernel(EncodeArgs 
                                                                      uint64_t arena_len) {
     __shared__ RecSmem s;
     const uint32_t tid = threadIdx.x;
-    const uint32_t t = blockIdx.x;
     a.n = enc_count(a.n, a.n_dev);
+    const uint32_t t = blockIdx.x;
     if ((uint64_t)t * ENC_TILE >= a.n) return;  // grid sized for the upper bound
     const uint64_t r0 = (uint64_t)t * ENC_TILE;
     const uint32_t nrec = (uint32_t)min((uint64_t)ENC_TILE, a.n - r0);

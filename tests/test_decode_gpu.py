@@ -613,3 +613,50 @@ def test_splice_repair_of_wrong_batch_entries(engine, fake_every):
     assert planted > 10
     assert_same(engine, data)
     assert _ctl_repairs(engine) > 0
+
+
+def _prepass_links(engine, sst):
+    """Decode `sst` (device) and read back the pre-pass batch records
+    (tools/spec_diag.py's view): (spans result, first_bad, link mismatches,
+    splice repairs, pre-pass codes)."""
+    import ctypes
+    lib = engine.lib
+    lib.hgk_ctx_workspace.restype = ctypes.c_void_p
+    lib.hgk_ctx_workspace.argtypes = [ctypes.c_void_p]
+    lib.hgk_debug_d2h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
+    out = engine.decode_dev(sst, sst.numel())
+    lay = (ctypes.c_uint64 * 8)()
+    lib.hgk_decode_last_layout(lay)
+    sb_off, _, nspec = list(lay)[:3]
+    ws = lib.hgk_ctx_workspace(engine.ctx)
+    sbd = np.dtype([("x0", "<u8"), ("exit", "<u8"), ("count", "<u4"), ("ok", "<u4"), ("pad", "<u8")])
+    sb = np.zeros(nspec, sbd)
+    lib.hgk_debug_d2h(sb.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws + sb_off), sb.nbytes)
+    ctl = np.zeros(4, np.uint32)
+    lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws), 16)
+    links = int(np.sum(sb["x0"][1:] != sb["exit"][:-1]))
+    return out, nspec - int(ctl[1]), links, int(ctl[3]), sb["pad"] & 0xFF, nspec
+
+
+@pytest.mark.parametrize("seed", [4, 6])
+def test_hop_entries_keep_tombstones(engine, monkeypatch, seed):
+    """Round-3 regression (cfg 4's batched decode 0.27 -> 0.48 ms): a hop
+    segment's entry guess skipped a tombstone whose 16-byte key starts with
+    zero bytes (header, zeros and key merged into one run of candidates whose
+    end reads as an all-zero header), so the batch began one record late and
+    every such batch was spliced behind a look-back chain.  At the batched
+    geometry of cfg 4 (64-piece batches) every pre-pass batch of a cfg 4
+    table must now link to its predecessor's exit: no repairs, nothing left
+    to the general engine -- and the spans equal the generated layout."""
+    from horreum_amd import synth
+    monkeypatch.setenv("HG_DECODE_BP", "64")
+    monkeypatch.setenv("HG_DECODE_SBP", "64")
+    v = synth.mixed_table_vlens(64 << 20, 8, 4096, 0.05, seed=seed)
+    keys = np.arange(v.size, dtype=np.uint64) * 7 + seed
+    buf, offs = synth.keyed_table(keys, v, seed=seed, device=engine.device)
+    out, first_bad, links, repairs, codes, nspec = _prepass_links(engine, buf)
+    want = synth.span_rows(offs[:-1], np.full(v.size, 16), v)
+    got = engine.spans_to_numpy(out.spans, out.n).view("<u8").reshape(-1, 2)
+    assert out.kind == 0 and out.n == v.size and np.array_equal(got, want)
+    assert (codes == 5).all(), codes  # every batch in hop mode
+    assert (first_bad, links, repairs) == (nspec, 0, 0)

@@ -2,9 +2,11 @@
 """Compaction of 8 tables x 1 M records (cfg 5's shape: 16 B keys / 100 B
 values, 25 % shared keys) through hg_compact_dev: sorted tables (the parallel
 merge), one duplicate key late in table 3 and one inversion in every table
-(the epochs of the reference loop), and -- with --serial -- the same one-
-duplicate input through the serial loop on the device (HG_MERGE_SERIAL: the
-round-2 path).  Prints one JSON line per case (median of 3 wall ms)."""
+(the epochs of the reference loop), every table fully shuffled and half of
+them shuffled (the rank path: dense key ranks, the loop in one wave), each
+checked byte for byte against the oracle's compaction with --check; with
+--serial the one-duplicate input also through the round-2 loop over entries
+(HG_MERGE_SERIAL=exact).  Prints one JSON line per case (median of 3 wall ms)."""
 import json
 import os
 import sys
@@ -34,11 +36,13 @@ def tables(per_table, mode, rng_seed=5):
             j = int(rng.integers(1, k.size - 2))
             k = k.copy()
             k[j], k[j + 1] = k[j + 1], k[j]
+        elif mode == "shuffle" or (mode == "half" and t % 2 == 1):
+            k = rng.permutation(k)
         out.append(k)
     return out
 
 
-def run(eng, keys, label, reps=3):
+def run(eng, keys, label, reps=3, check=False):
     dev = eng.device
     bufs = [synth.keyed_table(k, np.full(k.size, 100), seed=50 + t, device=dev)[0]
             for t, k in enumerate(keys)]
@@ -50,6 +54,7 @@ def run(eng, keys, label, reps=3):
     arena = torch.zeros(total, dtype=torch.uint8, device=dev)
     for o, b in zip(offs, bufs):
         arena[o:o + b.numel()] = b
+    hosts = [b.cpu().numpy() for b in bufs] if check else None
     del bufs
     out = eng.empty(total)
     c = eng.compact_dev(arena, offs, sizes, out)
@@ -60,7 +65,14 @@ def run(eng, keys, label, reps=3):
         c = eng.compact_dev(arena, offs, sizes, out)
         torch.cuda.synchronize(dev)
         ts.append((time.perf_counter() - t0) * 1e3)
+    parity = None
+    if check:
+        from oracle import oracle
+        want, _, wn = oracle.compacted_table(hosts)
+        got = out[:c.data.numel()].cpu().numpy()
+        parity = bool(wn == c.n and np.array_equal(got, want))
     print(json.dumps({"case": label, "records_in": int(sum(k.size for k in keys)),
+                      "parity_vs_oracle": parity,
                       "records_out": int(c.n), "status": int(c.status), "table": int(c.table),
                       "epochs": int(c.index) if c.table == 2 else None,
                       "ms": round(sorted(ts)[reps // 2], 3),
@@ -75,8 +87,11 @@ def main():
     run(eng, tables(per, "sorted"), "sorted (parallel merge)")
     run(eng, tables(per, "dup"), "one duplicate key at 0.9 of table 3 (epochs)")
     run(eng, tables(per, "every"), "one inversion in every table (epochs)")
+    chk = "--check" in sys.argv
+    run(eng, tables(per, "shuffle"), "every table shuffled (rank path)", check=chk)
+    run(eng, tables(per, "half"), "tables 1, 3, 5, 7 shuffled (rank path)", check=chk)
     if "--serial" in sys.argv:
-        os.environ["HG_MERGE_SERIAL"] = "1"
+        os.environ["HG_MERGE_SERIAL"] = "exact"
         run(eng, tables(per, "dup"), "one duplicate key, serial reference loop (round-2 path)",
             reps=1)
 

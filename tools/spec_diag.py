@@ -21,7 +21,10 @@ from horreum_amd.engine import Engine  # noqa: E402
 
 def workloads(dev):
     yield from _workloads(dev)
-    for t in (0, 1):  # two BASELINE cfg-4 tables (64 MiB, keyed, 8..4096 B values)
+    # BASELINE cfg-4 tables (64 MiB, keyed, 8..4096 B values): two, or
+    # CFG4_TABLES of them (with HG_DECODE_BP=64 HG_DECODE_SBP=64 each single-table
+    # decode has the batched decode's geometry for cfg 4's 32 tables per GPU)
+    for t in range(int(os.environ.get("CFG4_TABLES", "2"))):
         v = synth.mixed_table_vlens(64 << 20, 8, 4096, 0.05, seed=4 + t)
         keys = np.arange(v.size, dtype=np.uint64) * 7 + t
         buf, _ = synth.keyed_table(keys, v, seed=4 + t, device=dev)
