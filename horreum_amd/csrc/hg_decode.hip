@@ -2379,12 +2379,15 @@ __device__ __forceinline__ void lw_chunk_masks(const uint8_t* buf, uint16_t* zm)
 #define HG_LW_LEAN 1
 #endif
 __device__ __forceinline__ void lw_masks4(const uint16_t* zm, uint32_t seg0, uint32_t clen,
-                                          uint64_t rem, uint64_t& cm0, uint64_t& nextbit) {
+                                          uint64_t rem, uint64_t& cm0, uint64_t& nextbit,
+                                          uint64_t& zb) {
     cm0 = 0;
     nextbit = 0;
+    zb = 0;
     if (seg0 >= clen || rem < 16) return;
     const uint32_t gi = seg0 / 16;  // zero-byte bits of bytes seg0 .. seg0 + 79: d0, d1, d2 (16)
     const uint2 z = *reinterpret_cast<const uint2*>(&zm[gi]);
+    zb = ((uint64_t)z.y << 32) | z.x;  // the segment's zero bytes (lw_guess)
     uint32_t d0 = z.x, d1 = z.y, d2 = zm[gi + 4];
     d0 &= __builtin_amdgcn_alignbit(d1, d0, 1);  // bit j: bytes j, j+1 zero
     d1 &= __builtin_amdgcn_alignbit(d2, d1, 1);
@@ -2411,16 +2414,18 @@ __device__ __forceinline__ void lw_masks4(const uint16_t* zm, uint32_t seg0, uin
 
 __device__ __forceinline__ void lw_masks(const uint16_t* zm, uint32_t seg0, uint32_t clen,
                                          uint64_t rem, uint32_t hz, uint64_t& cm0,
-                                         uint64_t& nextbit) {
+                                         uint64_t& nextbit, uint64_t& zb) {
     if (HG_LW_LEAN) {
-        lw_masks4(zm, seg0, clen, rem, cm0, nextbit);
+        lw_masks4(zm, seg0, clen, rem, cm0, nextbit, zb);
         return;
     }
     cm0 = 0;
     nextbit = 0;
+    zb = 0;
     if (seg0 >= clen || rem < 16) return;
     const uint32_t gi = seg0 / 16;
     const uint64_t z0 = *reinterpret_cast<const uint64_t*>(&zm[gi]);
+    zb = z0;
     const uint32_t z1 = zm[gi + 4];
     uint64_t c, c64;
     if (hz == 0) {
@@ -2511,13 +2516,27 @@ __device__ __noinline__ uint32_t lw_guess_nz(const uint8_t* data, const uint16_t
     return NO_GUESS;
 }
 
+#ifndef HG_LW_NZ1
+#define HG_LW_NZ1 1  // 0: run ends in position order (round-3 rule, A/B)
+#endif
 // This lane's guess in [seg0, segend) (piece-relative) or NO_GUESS; cm0 / the
 // next lane's first candidate bit as in lean_prepare.
 __device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, const uint16_t* zm,
                                              uint32_t seg0, uint32_t segend, uint32_t clen,
                                              uint64_t rem, uint32_t hz, uint64_t cm0,
-                                             uint64_t nextbit) {
-    const uint64_t runend = cm0 & ~((cm0 >> 1) | (nextbit << 63));
+                                             uint64_t nextbit, uint64_t zb) {
+    uint64_t runend = cm0 & ~((cm0 >> 1) | (nextbit << 63));
+    // Inside zero-byte values a run of candidates ends 8 bytes before the true
+    // header (that position reads as the header (0, klen): klen's low byte
+    // lands in its vlen) -- a shifted read whose record lands inside the next
+    // one.  So a run end whose first byte is zero is passed over when another
+    // run end, with a non-zero first byte, follows 8 bytes later; a true
+    // header of an empty key (first byte zero too) has no such partner
+    // (always passing such run ends over cost small records 5 %).
+    if (HG_LW_NZ1) {  // (zb: the segment's zero-byte bits, from lw_masks)
+        const uint64_t drop = runend & zb & ((runend & ~zb) >> 8);
+        runend &= ~drop;
+    }
     uint64_t cm = runend;
     uint32_t tries = 0;  // a lane left without a guess is entered by the relaxation
 #pragma nounroll
@@ -2676,8 +2695,8 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     const uint32_t seg0 = lane * SEG, segend = min(seg0 + SEG, clen);
     const uint32_t je = guess ? 0u : (uint32_t)((X - cb) / SEG);
     const bool in_chunk = seg0 < clen && lane >= je;
-    uint64_t cm0, nb;
-    lw_masks(zm, seg0, clen, rem, a.hz, cm0, nb);
+    uint64_t cm0, nb, zb;
+    lw_masks(zm, seg0, clen, rem, a.hz, cm0, nb, zb);
     const uint32_t lim = (uint32_t)min(rem, (uint64_t)1 << 31);
     uint32_t g = NO_GUESS;
     LWalk w;
@@ -2686,7 +2705,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     w.cnt = 0;
     w.p01 = w.p23 = 0;
     if (!guess && lane == je) g = (uint32_t)(X - cb);
-    else if (in_chunk) g = lw_guess(data, zm, seg0, segend, clen, rem, a.hz, cm0, nb);
+    else if (in_chunk) g = lw_guess(data, zm, seg0, segend, clen, rem, a.hz, cm0, nb, zb);
     if (HG_LW_ZERO && g != NO_GUESS && (g & LW_ZERO_HDR))  // rare: a lane inside zero bytes
         g = lw_guess_nz(data, zm, seg0, clen, rem, cm0, nb);
     if (in_chunk && g != NO_GUESS) lw_walk(data, lim, g, segend, seg0, cm0, w);

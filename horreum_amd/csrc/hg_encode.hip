@@ -443,7 +443,7 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_kernel(EncodeArgs a) {
 // cfg 5 leg, a VALU-bound gather.  A tile owns the pieces that START in its
 // byte range; the last one may finish with the next tile's first record.
 #ifndef HG_ENC_REC_U
-#define HG_ENC_REC_U 2
+#define HG_ENC_REC_U 1  // cfg 5 leg, round 4 same box: 1 -> 1.254-1.257 ms, 2: 1.268-1.279, 4: 1.285-1.336
 #endif
 constexpr uint32_t REC_U = HG_ENC_REC_U;  // pieces per lane per step (their loads overlap)
 

@@ -1110,9 +1110,11 @@ __global__ __launch_bounds__(THREADS) void rank_count_kernel(MergeArgs a, const 
 
 // rank[g] = distinct keys below entry g's key (g = the entry's index in the
 // tables' layout), from the flags' prefix sums (tile bases from merge_scan_kernel).
+// pack (every rank < 2^26, <= 64 tables): the value stored is rank << 6 |
+// the entry's table, the loop's reduction key (rank_loop).
 __global__ __launch_bounds__(THREADS) void rank_scatter_kernel(MergeArgs a, const MEnt* srt,
                                                                const uint64_t* tile_base,
-                                                               uint32_t* rank) {
+                                                               uint32_t* rank, uint32_t pack) {
     __shared__ uint32_t tmp[THREADS / 64];
     const uint64_t i0 = (uint64_t)blockIdx.x * TILE + threadIdx.x * EPT;
     uint32_t f[EPT];
@@ -1123,7 +1125,8 @@ __global__ __launch_bounds__(THREADS) void rank_scatter_kernel(MergeArgs a, cons
     for (uint32_t u = 0; u < EPT; ++u) {
         if (i0 + u >= a.n) break;
         r += f[u];
-        rank[srt[i0 + u].gd & ~DEAD] = (uint32_t)(r - 1);
+        const uint32_t g = srt[i0 + u].gd & ~DEAD;
+        rank[g] = pack ? ((uint32_t)(r - 1) << 6) | run_of(a, g) : (uint32_t)(r - 1);
     }
 }
 
@@ -1172,6 +1175,7 @@ struct RankArgs {
     const uint64_t* start;    // [ntables] heads to start from (table-local)
     uint32_t* win_idx;        // out: the winners' entry indices, in output order
     uint64_t* steps;          // out: the number of winners
+    uint32_t pack;            // rank entries are rank << 6 | table (rank_scatter_kernel)
 };
 
 // One half of table t's ring (ranks [q, q + H) of the table) by LDS-DMA; the
@@ -1189,59 +1193,59 @@ __device__ __forceinline__ uint32_t rank_fill(const RankArgs& r, uint32_t* ring_
     return nins;
 }
 
-__global__ __launch_bounds__(64) void rank_merge_kernel(RankArgs r) {
-    extern __shared__ uint32_t ring[];  // [ntables][2][H]
+// Wave-wide min over the first 8 << (NL - 3) lanes by NL DPP steps (lanes
+// without a source keep ~0): lane (8 << (NL - 3)) - 1 holds it.
+template <int NL>
+__device__ __forceinline__ uint32_t dpp_min_lanes(uint32_t v) {
+#define HG_DPP_MIN(ctrl, rmask) \
+    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)RANK_INF, (int)v, ctrl, rmask, 0xf, false))
+    HG_DPP_MIN(0x111, 0xf);
+    HG_DPP_MIN(0x112, 0xf);
+    HG_DPP_MIN(0x114, 0xf);
+    if (NL > 3) HG_DPP_MIN(0x118, 0xf);
+    if (NL > 4) HG_DPP_MIN(0x142, 0xa);
+    if (NL > 5) HG_DPP_MIN(0x143, 0xc);
+#undef HG_DPP_MIN
+    return __builtin_amdgcn_readlane(v, (8u << (NL - 3)) - 1u);
+}
+
+struct RankState {
+    uint32_t idx, gidx, hk, pv, ob, tk0, tk1, vm;
+};
+
+// The loop proper (manager.rs:205-231), NL DPP steps over the tables' lanes.
+// Lane t holds its head's key hk (PACK: rank << 6 | t, so the min also names
+// the winner -- the lowest table holding the smallest key, min_by_key's first
+// minimum -- without a ballot and a bit scan; else the rank) and pv, the ring
+// slot of its next record, read one step ahead.
+template <int NL, bool PACK>
+__device__ __forceinline__ uint32_t rank_loop(const RankArgs& r, uint32_t* ring, const uint32_t* my,
+                                              uint32_t base, uint32_t cnt, RankState& st) {
     const uint32_t lane = threadIdx.x;
     const uint32_t H = r.H, hs = (uint32_t)__builtin_ctz(H), RM = 2 * H - 1;
-    const bool mine = lane < r.ntables;
-    // positions are table-local u32 (a merge holds < 2^31 entries)
-    const uint32_t base = mine ? (uint32_t)r.run_off[lane] : 0u;
-    const uint32_t cnt = mine ? (uint32_t)r.run_off[lane + 1] - base : 0u;
-    uint32_t idx = mine ? (uint32_t)min(r.start[lane], (uint64_t)cnt) : 0u;
-    uint32_t hr = idx < cnt ? r.rank[base + idx] : RANK_INF;
-    uint32_t hn = idx + 1 < cnt ? r.rank[base + idx + 1] : RANK_INF;
-    const uint32_t* my = ring + lane * 2 * H;
-    // the ring holds the table's ranks [b H, (b + 2) H) around the next read
-    // position idx + 2 (slot = position mod 2H); both halves now, waited for
-    for (uint32_t t = 0; t < r.ntables; ++t) {
-        const uint32_t bt = __builtin_amdgcn_readlane(base, t), it = __builtin_amdgcn_readlane(idx, t);
-        const uint32_t b = (it + 2) >> hs;
-        uint32_t* rt = ring + t * 2 * H;
-        rank_fill(r, rt + (b & 1u) * H, r.rank + bt + ((uint64_t)b << hs));
-        rank_fill(r, rt + ((b + 1) & 1u) * H, r.rank + bt + ((uint64_t)(b + 1) << hs));
-    }
-    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t vm = 0;            // vector memory instructions issued since (wave-uniform)
-    uint32_t tk0 = 0, tk1 = 0;  // per half: vm right after its last refill was issued
-    uint32_t gidx = base + idx;
-    uint32_t ob = 0, pv = 0, ps = 0;
-    bool pf = false;
-    uint64_t j = 0;
+    uint32_t idx = st.idx, gidx = st.gidx, hk = st.hk, pv = st.pv;
+    uint32_t ob = st.ob, tk0 = st.tk0, tk1 = st.tk1, vm = st.vm;
+    uint32_t j = 0;
     for (;;) {
-        const uint32_t minr = __builtin_amdgcn_readlane(dpp_min_incl(hr), 63);
-        if (minr == RANK_INF) break;  // every table exhausted (:228-230)
-        const uint64_t m = __ballot(hr == minr);
-        const uint32_t w = (uint32_t)__builtin_ctzll(m);  // first table holding it
+        const uint32_t key = dpp_min_lanes<NL>(hk);
+        if (key == RANK_INF) break;  // every table exhausted (:228-230)
+        const uint32_t w = PACK ? (key & 63u) : (uint32_t)__builtin_ctzll(__ballot(hk == key));
         const uint32_t gw = __builtin_amdgcn_readlane(gidx, w);
-        const uint32_t jl = (uint32_t)j & 63u;
-        ob = lane == jl ? gw : ob;
-        if (jl == 63) {
+        ob = lane == (j & 63u) ? gw : ob;
+        if ((j & 63u) == 63u) {
             r.win_idx[j - 63 + lane] = ob;
             ++vm;
         }
         ++j;
-        // every table whose head equals the winner's key advances
-        // (the next rank is pv when pf -- an LDS read issued last step, first
-        // used here, so its latency hides behind this step's reduction -- else hn)
-        const bool adv = (m >> lane) & 1ull;
+        // every table whose head equals the winner's key advances (:218-227)
+        const bool adv = PACK ? (hk ^ key) < 64u : hk == key;
         if (adv) {
             ++idx;
             ++gidx;
-            hr = pf ? pv : hn;
+            hk = idx < cnt ? pv : RANK_INF;
         }
-        const uint32_t p = idx + 1;  // the next rank to read
-        const bool need = adv && p < cnt;
-        const uint64_t cm = __ballot(need && (p & (H - 1)) == 0);
+        const uint32_t p = idx + 1;  // the next record's position
+        const uint64_t cm = __ballot(adv && (p & (H - 1)) == 0);
         if (cm) {  // lanes entering a new half: it must have landed; refill the one left
             const uint32_t h = (p >> hs) & 1u;
             const uint32_t tkh = h ? tk1 : tk0;
@@ -1260,21 +1264,58 @@ __global__ __launch_bounds__(64) void rank_merge_kernel(RankArgs r) {
                 }
             }
         }
-        if (need) {
-            ps = p & RM;
-            pf = true;
-        } else if (adv) {
-            hn = RANK_INF;
-            pf = false;
-        }
-        // every lane reads its pending slot (a lane that did not advance gets
-        // the same rank again: its half is refilled only once it has left it),
-        // so the read lands in pv's own register and is first waited for at the
-        // next step's advance, not here
-        pv = my[ps];
+        // every lane reads its next record's slot (a lane that did not advance
+        // reads the same one again: its half is refilled only once it has left
+        // it), so the read lands in pv's own register, waited for one step later
+        pv = my[p & RM];
     }
-    const uint32_t jl = (uint32_t)j & 63u;
-    if (jl && lane < jl) r.win_idx[j - jl + lane] = ob;
+    st.ob = ob;
+    st.vm = vm;
+    return j;
+}
+
+__global__ __launch_bounds__(64) void rank_merge_kernel(RankArgs r) {
+    extern __shared__ uint32_t ring[];  // [ntables][2][H]
+    const uint32_t lane = threadIdx.x;
+    const uint32_t H = r.H, hs = (uint32_t)__builtin_ctz(H), RM = 2 * H - 1;
+    const bool mine = lane < r.ntables;
+    // positions are table-local u32 (a merge holds < 2^31 entries)
+    const uint32_t base = mine ? (uint32_t)r.run_off[lane] : 0u;
+    const uint32_t cnt = mine ? (uint32_t)r.run_off[lane + 1] - base : 0u;
+    RankState st;
+    st.idx = mine ? (uint32_t)min(r.start[lane], (uint64_t)cnt) : 0u;
+    st.hk = st.idx < cnt ? r.rank[base + st.idx] : RANK_INF;
+    // the ring holds the table's ranks [b H, (b + 2) H) around the next
+    // record's position idx + 1 (slot = position mod 2H); both halves now,
+    // waited for
+    for (uint32_t t = 0; t < r.ntables; ++t) {
+        const uint32_t bt = __builtin_amdgcn_readlane(base, t), it = __builtin_amdgcn_readlane(st.idx, t);
+        const uint32_t b = (it + 1) >> hs;
+        uint32_t* rt = ring + t * 2 * H;
+        rank_fill(r, rt + (b & 1u) * H, r.rank + bt + ((uint64_t)b << hs));
+        rank_fill(r, rt + ((b + 1) & 1u) * H, r.rank + bt + ((uint64_t)(b + 1) << hs));
+    }
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t* my = ring + lane * 2 * H;
+    st.pv = my[(st.idx + 1) & RM];
+    st.vm = 0;            // vector memory instructions issued since (wave-uniform)
+    st.tk0 = st.tk1 = 0;  // per half: vm right after its last refill was issued
+    st.gidx = base + st.idx;
+    st.ob = 0;
+    uint32_t j;
+    if (r.pack) {
+        if (r.ntables <= 8) j = rank_loop<3, true>(r, ring, my, base, cnt, st);
+        else if (r.ntables <= 16) j = rank_loop<4, true>(r, ring, my, base, cnt, st);
+        else if (r.ntables <= 32) j = rank_loop<5, true>(r, ring, my, base, cnt, st);
+        else j = rank_loop<6, true>(r, ring, my, base, cnt, st);
+    } else {
+        if (r.ntables <= 8) j = rank_loop<3, false>(r, ring, my, base, cnt, st);
+        else if (r.ntables <= 16) j = rank_loop<4, false>(r, ring, my, base, cnt, st);
+        else if (r.ntables <= 32) j = rank_loop<5, false>(r, ring, my, base, cnt, st);
+        else j = rank_loop<6, false>(r, ring, my, base, cnt, st);
+    }
+    const uint32_t jl = j & 63u;
+    if (jl && lane < jl) r.win_idx[j - jl + lane] = st.ob;
     if (lane == 0) *r.steps = j;
 }
 
@@ -1497,8 +1538,10 @@ int rank_path(const hgm::MergeArgs& a, const MergeWs& w, const uint64_t* start, 
                        (const MEnt*)cur, w.tile_live);
     hipLaunchKernelGGL(merge_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)w.tile_live,
                        (uint32_t)ntiles, w.tile_base, w.ep_res);
+    // ranks < n; HG_RANK_NOPACK: plain ranks at any size (tests the > 2^26 form)
+    const uint32_t pack = n < (1ull << 26) && !getenv("HG_RANK_NOPACK") ? 1u : 0u;
     hipLaunchKernelGGL(rank_scatter_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
-                       (const MEnt*)cur, (const uint64_t*)w.tile_base, w.rank);
+                       (const MEnt*)cur, (const uint64_t*)w.tile_base, w.rank, pack);
     int rc = HG_LAUNCH_STATUS();
     if (rc != HG_OK) return rc;
     uint64_t done = 0;
@@ -1518,6 +1561,7 @@ int rank_path(const hgm::MergeArgs& a, const MergeWs& w, const uint64_t* start, 
     ra.start = w.ep;
     ra.win_idx = w.win_idx;
     ra.steps = w.rank_steps;
+    ra.pack = pack;
     hipLaunchKernelGGL(rank_merge_kernel, dim3(1), dim3(64), (size_t)k * 2 * H * 4, stream, ra);
     const uint64_t left = n > done ? n - done : 1;
     hipLaunchKernelGGL(rank_emit_kernel, dim3((uint32_t)((left + THREADS - 1) / THREADS)), dim3(THREADS),

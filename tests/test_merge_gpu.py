@@ -533,6 +533,8 @@ def _rank_case(engine, datas, table=1):
 
 @pytest.mark.parametrize("sizes,dup,seed", [
     ([20_000] * 8, 0.0, 61),                    # cfg 5's shape, shuffled, 8 lanes, H 1024
+    ([2_000] * 13, 0.1, 65),                    # 16-lane reduction
+    ([1_000] * 27, 0.1, 66),                    # 32-lane reduction, H 256
     ([5_000, 1, 0, 2, 7_000, 1_023, 1_024, 1_025], 0.1, 62),  # ring edges, empty and tiny tables
     ([300] * 64, 0.2, 63),                      # 64 tables: one per lane, H 128 (32-lane fills)
     ([70_000, 3], 0.3, 64),                     # one long table against a short one
@@ -554,6 +556,15 @@ def test_rank_path_mixed_and_long_prefixes(engine):
         rng.shuffle(tables[t])
     tables[4] = tables[4][::-1] + tables[4][:200]
     _exact_case(engine, tables)
+
+
+def test_rank_path_plain_ranks(engine, monkeypatch):
+    """HG_RANK_NOPACK: the loop over plain ranks (winner by ballot and bit
+    scan), the form used past 2^26 entries, on shuffled tables of 3, 12, 20
+    and 40 tables (every DPP depth)."""
+    monkeypatch.setenv("HG_RANK_NOPACK", "1")
+    for k, seed in ((3, 71), (12, 72), (20, 73), (40, 74)):
+        _rank_case(engine, _shuffled_keyed([1500] * k, seed, dup_frac=0.2))
 
 
 def test_rank_path_equals_exact_loop(engine, monkeypatch):

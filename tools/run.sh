@@ -57,7 +57,7 @@ for step in "$@"; do
       WL="${WL:-small medium mixed4k zsmall midlarge}" timeout -k 10 900 bash tools/ab_variants.sh base ${VARIANTS:?} ||
         exit 1 ;;
     merge)
-      timeout -k 10 600 python3 tools/merge_epochs.py > gpurun_out/${T}_merge.log 2>&1 || fail merge 5 gpurun_out/${T}_merge.log
+      timeout -k 10 600 python3 tools/merge_epochs.py ${MERGE_ARGS:-} > gpurun_out/${T}_merge.log 2>&1 || fail merge 5 gpurun_out/${T}_merge.log
       grep -v amdgpu.ids gpurun_out/${T}_merge.log ;;
     compact)
       timeout -k 10 300 python3 tools/compact_leg.py > gpurun_out/${T}_compact.log 2>&1 ||
