@@ -2526,16 +2526,17 @@ __device__ __forceinline__ uint32_t lw_guess(const uint8_t* data, const uint16_t
                                              uint64_t rem, uint32_t hz, uint64_t cm0,
                                              uint64_t nextbit, uint64_t zb) {
     uint64_t runend = cm0 & ~((cm0 >> 1) | (nextbit << 63));
-    // Inside zero-byte values a run of candidates ends 8 bytes before the true
-    // header (that position reads as the header (0, klen): klen's low byte
-    // lands in its vlen) -- a shifted read whose record lands inside the next
-    // one.  So a run end whose first byte is zero is passed over when another
-    // run end, with a non-zero first byte, follows 8 bytes later; a true
-    // header of an empty key (first byte zero too) has no such partner
-    // (always passing such run ends over cost small records 5 %).
+    // Inside zero-byte values runs of candidates end 16 and 8 bytes before
+    // the true header (those positions read as the headers (0, 0) and
+    // (0, klen): klen's low byte lands in the vlen) -- reads inside the value
+    // that chain into the next record.  So a run end whose first byte is zero
+    // is passed over when a run end with a non-zero first byte follows 8 or 16
+    // bytes later; a true header of an empty key (first byte zero too) has no
+    // such partner (passing every zero-first-byte run end over cost small
+    // records 5 %).
     if (HG_LW_NZ1) {  // (zb: the segment's zero-byte bits, from lw_masks)
-        const uint64_t drop = runend & zb & ((runend & ~zb) >> 8);
-        runend &= ~drop;
+        const uint64_t nzr = runend & ~zb;
+        runend &= ~(zb & ((nzr >> 8) | (nzr >> 16)));
     }
     uint64_t cm = runend;
     uint32_t tries = 0;  // a lane left without a guess is entered by the relaxation
