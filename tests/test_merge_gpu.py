@@ -611,3 +611,34 @@ def test_rank_path_8x250k_shuffled_timed(engine):
     assert rc == 0 and res.status == 0 and res.table == 1
     assert res.n == want.size and np.array_equal(got, want)
     assert dt < 0.5, dt  # the round-2 loop: ~2-4 s
+
+
+@pytest.mark.parametrize("kent", ["1", "0"])
+def test_compaction_key_length_change_on_the_stride_lattice(engine, monkeypatch, kent):
+    """a stride piece of 16 B keys / 100 B values holding one
+    record of a 10 B key and a 106 B value -- the same 132-byte size, so it
+    sits exactly on the piece's stride lattice but its header differs.  The
+    decode pre-pass masks a piece's key prefixes with the piece's key length;
+    a prefix taken for this record would carry 6 value bytes.  Both entry
+    builders (HG_MERGE_KENT=1: per pre-pass batch; 0: merge_prep_kernel) must
+    give the oracle's compaction byte for byte."""
+    monkeypatch.setenv("HG_MERGE_KENT", kent)
+    rng = np.random.default_rng(81)
+    tables = []
+    for t in range(3):
+        ids = np.unique(rng.integers(1, 1 << 63, size=20_000, dtype=np.uint64))
+        pairs = []
+        for i, k in enumerate(ids):
+            key = int(k).to_bytes(16, "big")
+            if t == 1 and i in (777, 5000, 12345):  # on the lattice: 10 + 106 == 16 + 100
+                # a prefix of this key: sorts just before it, mid-table
+                pairs.append((key[:10], rng.integers(0, 256, 106, dtype=np.uint8).tobytes()))
+            else:
+                pairs.append((key, rng.integers(0, 256, 100, dtype=np.uint8).tobytes()))
+        pairs.sort(key=lambda kv: kv[0])
+        tables.append(pairs)
+    datas = encode_tables(tables)
+    out = engine.compact_host([d.tobytes() for d in datas], block_stride=5)
+    want, wblocks, wn = oracle.compacted_table(datas, block_stride=5)
+    assert out.status == 0 and out.n == wn
+    assert np.array_equal(out.data, want) and np.array_equal(out.blocks, wblocks)
