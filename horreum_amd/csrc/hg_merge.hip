@@ -356,10 +356,13 @@ __device__ __forceinline__ void pair_of(const LevelArgs& l, uint64_t d, uint32_t
 #define HG_SPLIT_G 8  // cfg5 leg: 8-ary 21 us per round, 4-ary 25, 16-ary 29
 #endif
 constexpr uint32_t SPLIT_G = HG_SPLIT_G;
+// zst (nullable): the FINAL round's look-back status words, zeroed here by
+// a merge's first round (one launch fewer than a memset: ~10 us of gap).
 __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, LevelArgs l,
                                                               const MEnt* in, uint64_t* split,
                                                               uint64_t nb_tiles,
-                                                              const unsigned long long* err) {
+                                                              const unsigned long long* err,
+                                                              unsigned long long* zst) {
     const uint32_t lane = threadIdx.x & 63u, j = lane % SPLIT_G, gsh = lane - j;
     const uint64_t t = ((uint64_t)blockIdx.x * THREADS + threadIdx.x) / SPLIT_G;
     if (t > nb_tiles) return;  // the whole group
@@ -394,7 +397,10 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
             i = lo;
         }
     }
-    if (j == 0) split[t] = i;
+    if (j == 0) {
+        split[t] = i;
+        if (zst && t < nb_tiles) zst[t] = 0;
+    }
 }
 
 // The last round (two runs -> one) emits the hg_pairs itself (step 4 fused):
@@ -1455,7 +1461,7 @@ int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hg
     fa.st = w.lb_status;
     fa.ntiles = (uint32_t)ntiles;
     if (nr >= 2) {
-        if (hipMemsetAsync(w.lb_status, 0, ntiles * 8, stream) != hipSuccess) return HG_HIP_FAIL;
+        bool first = true;  // the first round's split kernel zeroes the look-back statuses
         MEnt* cur = in;
         MEnt* nxt = b1;
         while (nr > 1) {
@@ -1466,7 +1472,9 @@ int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hg
             // tile_base is free in the rounds: the round's splits
             const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
             hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
-                               (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)err);
+                               (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)err,
+                               first ? w.lb_status : (unsigned long long*)nullptr);
+            first = false;
             if (nr == 2)  // the last round emits the pairs
                 hipLaunchKernelGGL(merge_level_kernel<true>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
                                    stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
@@ -1529,7 +1537,8 @@ int rank_path(const hgm::MergeArgs& a, const MergeWs& w, const uint64_t* start, 
         l.un = n;
         const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
         hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
-                           (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)serr);
+                           (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)serr,
+                           (unsigned long long*)nullptr);
         hipLaunchKernelGGL(merge_level_kernel<false>, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream,
                            a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base, serr, fa);
         std::swap(cur, nxt);
@@ -1633,9 +1642,12 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     if (kp)
         for (uint64_t i = 0; i < 3 * (uint64_t)ntables; ++i) h[rwords + i] = kp[i];
     const MergeWs w = merge_ws(d_ws, ntables, n);
-    if (hipMemcpyAsync(w.d_stage, h, stage_words * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
+    // the error word (~0: no order violation yet) follows the staging in the
+    // workspace: one copy sets both (a memset launch fewer)
+    const uint64_t err_word = (uint64_t)(reinterpret_cast<uint64_t*>(w.err) - w.d_stage);
+    h[err_word] = ~0ull;
+    if (hipMemcpyAsync(w.d_stage, h, (err_word + 1) * 8, hipMemcpyHostToDevice, stream) != hipSuccess)
         return HG_HIP_FAIL;
-    if (hipMemsetAsync(w.err, 0xFF, 8, stream) != hipSuccess) return HG_HIP_FAIL;
     MergeArgs a;
     a.arena = d_arena;
     a.arena_len = arena_len;
