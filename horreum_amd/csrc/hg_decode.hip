@@ -2516,6 +2516,9 @@ __device__ __noinline__ uint32_t lw_guess_nz(const uint8_t* data, const uint16_t
     return NO_GUESS;
 }
 
+#ifndef HG_LW_WSHR
+#define HG_LW_WSHR 1  // 0: the relaxation's lane shift by __shfl_up (A/B)
+#endif
 #ifndef HG_LW_NZ1
 #define HG_LW_NZ1 1  // 0: run ends in position order (round-3 rule, A/B)
 #endif
@@ -2748,8 +2751,15 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     for (uint32_t r = 0; r < LW_WROUNDS; ++r) {
         if (a.sdiag && threadIdx.x == 0) ++s.lw_prof[7];
         const uint32_t m = dpp_max_incl(ev);
-        uint32_t excl = __shfl_up(m, 1, 64);
-        if (lane == 0) excl = 0;
+        // the previous lane's inclusive max: a DPP wave shift (gfx9 wave_shr:1,
+        // lane 0 gets 0) instead of __shfl_up's LDS permute round trip
+        uint32_t excl;
+        if (HG_LW_WSHR) {
+            excl = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xf, 0xf, false);
+        } else {
+            excl = __shfl_up(m, 1, 64);
+            if (lane == 0) excl = 0;
+        }
         const uint32_t seed = lane == jl ? xw : excl;
         uint32_t nev = ev;
         if (act) {
