@@ -606,9 +606,29 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
     //    table's owner (bytes and decoded spans, device to device: each byte
     //    crosses once, nothing is uploaded or decoded again), merged, encoded
     O.assign(nrange, RangeOut{});
+    // every owner's decode (and sample / cut work) is ordered before the copies
+    // out of it by an event on its stream -- not only by the host having
+    // synchronised it (decode_share's D2H), which an asynchronous decode would drop
+    struct Events {
+        std::vector<hipEvent_t> ev;
+        ~Events() {
+            for (hipEvent_t e : ev)
+                if (e) (void)hipEventDestroy(e);
+        }
+    } evs;
+    evs.ev.assign(nctx, nullptr);
+    for (uint32_t ci = 0; ci < nctx; ++ci) {
+        if (set_dev(ctxs[ci]) != HG_OK ||
+            hipEventCreateWithFlags(&evs.ev[ci], hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(evs.ev[ci], ctxs[ci]->stream) != hipSuccess)
+            return HG_HIP_FAIL;
+    }
     r = fan_out(nrange, [&](uint32_t g) {
         hg_ctx* c = ctxs[g];
         if (set_dev(c) != HG_OK) return (int)HG_HIP_FAIL;
+        for (uint32_t ci = 0; ci < nctx; ++ci)
+            if (ci != g && hipStreamWaitEvent(c->stream, evs.ev[ci], 0) != hipSuccess)
+                return (int)HG_HIP_FAIL;
         std::vector<uint64_t> pos(ntables), toff(ntables), cnt(ntables), sps(ntables);
         uint64_t ab = 0, nb = 0;
         for (uint32_t t = 0; t < ntables; ++t) {
