@@ -58,6 +58,75 @@ __global__ __launch_bounds__(256) void sweep_kernel(const uint8_t* src, uint32_t
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// LDS-DMA form of the contiguous sweep (round 4): each workgroup streams its
+// pieces with global_load_lds (16 B per lane, 1 KiB per wave instruction, 4 per
+// wave per 16 KiB piece) into NBUF LDS buffers, NBUF - 1 pieces in flight,
+// counted vmcnt + raw s_barrier (a __syncthreads() would drain every DMA),
+// nontemporal (aux 2) or default policy.
+template <int NBUF, int AUX>
+__global__ __launch_bounds__(256) void glds_sweep_kernel(const uint8_t* src, uint32_t ppb,
+                                                         unsigned long long* out) {
+    extern __shared__ u32x4 buf[];  // NBUF * PIECE bytes
+    const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
+    const uint64_t base = (uint64_t)blockIdx.x * ppb * PIECE;
+    auto issue = [&](uint32_t k) {
+        const uint8_t* s = src + base + (uint64_t)k * PIECE;
+        uint8_t* d = reinterpret_cast<uint8_t*>(buf) + (k % NBUF) * PIECE;
+#pragma unroll
+        for (uint32_t q = 0; q < GPT; ++q) {
+            const uint32_t g0 = q * 256 + wid * 64;
+            __builtin_amdgcn_global_load_lds(static_cast<const void*>(s + (uint64_t)(g0 + lane) * 16),
+                                             (__attribute__((address_space(3))) void*)(d + g0 * 16), 16, 0,
+                                             AUX);
+        }
+    };
+    for (uint32_t k = 0; k + 1 < NBUF && k < ppb; ++k) issue(k);
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < ppb; ++k) {
+        if (k + NBUF - 1 < ppb) {
+            issue(k + NBUF - 1);
+            // piece k landed: at most (NBUF - 1) pieces' DMAs younger than it
+            if (NBUF == 2) __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (NBUF == 3) __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory");
+            else __asm__ volatile("s_waitcnt vmcnt(12)" ::: "memory");
+        } else {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const u32x4 a = buf[(k % NBUF) * (PIECE / 16) + (tid * 7 + k) % (PIECE / 16)];
+        acc ^= a.x ^ a.w;
+        // every wave is done reading buffer k % NBUF before it is refilled
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int NBUF, int AUX>
+void run_glds(const uint8_t* d, uint64_t len, uint32_t ppb, unsigned long long* out, const char* name) {
+    const uint32_t npieces = (uint32_t)(len / PIECE);
+    const uint32_t grid = npieces / ppb;
+    const size_t lds = (size_t)NBUF * PIECE;
+    CHECK(hipFuncSetAttribute((const void*)glds_sweep_kernel<NBUF, AUX>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int occ = 0;
+    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, glds_sweep_kernel<NBUF, AUX>, 256, lds));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    float best = 1e9f;
+    for (int r = 0; r < 8; ++r) {
+        CHECK(hipEventRecord(e0));
+        glds_sweep_kernel<NBUF, AUX><<<grid, 256, lds>>>(d, ppb, out);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0 && ms < best) best = ms;
+    }
+    printf("%-26s ppb=%3u grid=%6u occ/CU=%2d  %.4f ms  %.0f GB/s\n", name, ppb, grid, occ, best,
+           (double)grid * ppb * PIECE / best / 1e6);
+}
+
 // Register-only grid-stride sweep (the 'float4 copy' shape without the write).
 __global__ __launch_bounds__(256) void flat_kernel(const u32x4* src, uint64_t n, unsigned long long* out) {
     uint32_t acc = 0;
@@ -119,6 +188,13 @@ int main() {
         }
         printf("flat grid-stride           grid=%6d  %.4f ms  %.0f GB/s\n", g, best, len / best / 1e6);
     }
+    for (uint32_t ppb : {16u, 32u, 64u}) {
+        run_glds<2, 2>(d, len, ppb, out, "glds x2 nt");
+        run_glds<3, 2>(d, len, ppb, out, "glds x3 nt");
+        run_glds<4, 2>(d, len, ppb, out, "glds x4 nt");
+        run_glds<3, 0>(d, len, ppb, out, "glds x3");
+    }
+    if (getenv("SWEEP_GLDS_ONLY")) return 0;
     for (uint32_t ppb : {4u, 16u, 64u}) {
         run<0, 0>(d, len, ppb, ticket, out, "contiguous pad0");
         run<1, 0>(d, len, ppb, ticket, out, "interleave pad0");
