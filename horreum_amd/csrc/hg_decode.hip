@@ -2313,18 +2313,39 @@ __device__ __forceinline__ void lw_wait_vm(uint32_t n) {
 #ifndef HG_LW_DMA_AUX
 #define HG_LW_DMA_AUX 2
 #endif
+// The DMA as inline asm (HG_DMA_ASM): the compiler's wait insertion treats
+// every LDS access behind a global_load_lds builtin as possibly reading the
+// bytes in flight and puts an s_waitcnt vmcnt(0) before it, so the chunk /
+// piece prefetched for the next iteration was waited for at the first LDS
+// read of the current one (no overlap at all).  Issued from asm the DMA is
+// invisible to it: the kernels' own counted waits (lw_wait_vm) order every
+// read of a DMA'd buffer after its DMA, and the compiler's waits for its own
+// loads only become stricter (it does not count these).  s_nop 0: the M0
+// write -> LDS-DMA hazard (one wait state).
+#ifndef HG_DMA_ASM
+#define HG_DMA_ASM 1
+#endif
+__device__ __forceinline__ void dma16(const void* src, uint8_t* dst) {
+    if (HG_DMA_ASM) {
+        // the low half of a flat LDS address is the LDS offset (the aperture
+        // is the high half): no null check as in an address-space cast
+        const uint32_t l = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)dst);
+        if (HG_LW_DMA_AUX == 2)
+            __asm__ volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" :: "v"(src), "{m0}"(l) : "memory");
+        else
+            __asm__ volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(src), "{m0}"(l) : "memory");
+    } else {
+        __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)dst, 16, 0,
+                                         HG_LW_DMA_AUX);
+    }
+}
 __device__ __forceinline__ uint32_t lw_fetch_chunk(const DecodeArgs& a, uint64_t cb, uint8_t* dst) {
     const uint32_t lane = threadIdx.x & 63u;
     if (cb + LW_CHUNK + 64 <= a.rlen) {
 #pragma unroll
         for (uint32_t q = 0; q < 4; ++q)
-            __builtin_amdgcn_global_load_lds(
-                static_cast<const void*>(a.sst + cb + (uint64_t)(q * 64 + lane) * 16),
-                (__attribute__((address_space(3))) void*)(dst + q * 1024), 16, 0, HG_LW_DMA_AUX);
-        if (lane < 4)
-            __builtin_amdgcn_global_load_lds(
-                static_cast<const void*>(a.sst + cb + LW_CHUNK + lane * 16),
-                (__attribute__((address_space(3))) void*)(dst + LW_CHUNK), 16, 0, HG_LW_DMA_AUX);
+            dma16(static_cast<const void*>(a.sst + cb + (uint64_t)(q * 64 + lane) * 16), dst + q * 1024);
+        if (lane < 4) dma16(static_cast<const void*>(a.sst + cb + LW_CHUNK + lane * 16), dst + LW_CHUNK);
         return 5;
     }
 #pragma unroll 1
@@ -3127,6 +3148,44 @@ __device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb,
 // behind the loads would make the wait for those loads (vmcnt counts both, in
 // order) wait for the stores too (measured: the pre-pass 173 -> 221 us with
 // the stores right after the verification).
+//
+// Piece staging (HG_SPEC_GLDS): the pieces stream into two LDS buffers by
+// global_load_lds (nontemporal, 4 x 1 KiB per wave per piece), piece i + 1 in
+// flight while piece i is checked, with counted vmcnt waits and raw
+// s_barriers (a __syncthreads() would wait for the DMA in flight too).  The
+// register-staged form (loads into v, ds_write after barrier (A)) streams at
+// ~6.4 TB/s, the LDS-DMA form at ~7.0 (tools/probes/sweep_probe.hip,
+// profiles/r4_sweep_glds.log).  The table's tail piece is staged from
+// registers (load16 zero-fills past the bytes present).
+#ifndef HG_SPEC_GLDS
+#define HG_SPEC_GLDS 1
+#endif
+// HG_LW_FUSE: the lane walks of SB_HOP_SMALL batches run in the pre-pass
+// workgroup itself (no decode_lw_kernel launch); the second piece buffer is
+// then also lw_batch's chunk buffer of waves 2 and 3.
+#ifndef HG_LW_FUSE
+#define HG_LW_FUSE 0
+#endif
+#if HG_LW_FUSE && !HG_SPEC_GLDS
+#error "HG_LW_FUSE needs HG_SPEC_GLDS (the second buffer)"
+#endif
+constexpr uint32_t SPEC_ALT_BYTES = HG_LW_FUSE ? PIECE + 512 : PIECE + 64;  // a piece + halo and zeros
+
+__device__ __forceinline__ bool spec_dma(const DecodeArgs& a, uint32_t p, uint8_t* dst) {
+    const uint64_t base = (uint64_t)p * PIECE;
+    if (base + PIECE > a.rlen) return false;
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+#pragma unroll
+    for (uint32_t q = 0; q < GPT; ++q) {
+        const uint32_t g0 = q * THREADS + wid * 64;  // granule layout as spec_stage's
+        dma16(static_cast<const void*>(a.sst + base + (uint64_t)(g0 + lane) * 16), dst + g0 * 16);
+    }
+    return true;
+}
+__device__ __forceinline__ void raw_barrier() {
+    __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 template <bool KPRE>
 __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
     __shared__ SpecSmem s;
@@ -3135,8 +3194,15 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     const uint32_t b = blk;
     const uint32_t p0 = b * a.sbp;
     const uint32_t np = min(a.sbp, a.npieces - p0);
+#if HG_SPEC_GLDS
+    __shared__ uint64_t spec_alt[SPEC_ALT_BYTES / 8];
+    uint8_t* const buf0 = reinterpret_cast<uint8_t*>(s.data64);
+    uint8_t* const buf1 = reinterpret_cast<uint8_t*>(spec_alt);
+    bool dma_cur = spec_dma(a, p0, buf0);
+#else
     uint4 v[GPT];
     load_piece(a, p0, v);
+#endif
     uint4 h = make_uint4(0, 0, 0, 0);
     if (tid < np) h = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
     uint64_t X = 0, X0 = 0, total = 0;
@@ -3161,12 +3227,35 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         const uint64_t base = (uint64_t)p * PIECE;
         const uint64_t rem = a.len - base;
         const uint32_t clen = piece_clen(a, base);
+#if HG_SPEC_GLDS
+        uint8_t* const cur = (i & 1) ? buf1 : buf0;
+        data = cur;
+        raw_barrier();  // (A) every wave is done with the other buffer (piece i - 1)
+        const bool dma_next = i + 1 < np && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
+        lw_wait_vm(dma_next ? GPT : 0);  // this wave's part of piece i landed
+        if (!dma_cur) {                  // the tail piece
+#pragma unroll
+            for (uint32_t q = 0; q < GPT; ++q)
+                *reinterpret_cast<uint4*>(cur + (q * THREADS + tid) * 16) =
+                    load16(a, base + (q * THREADS + tid) * 16);
+        }
+        if (i == 0 && tid < np) s.halo[tid] = h;
+        if (tid < 4)  // thread 0 reads back its own halo write when i == 0
+            *reinterpret_cast<uint4*>(cur + PIECE + tid * 16) = tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
+        flush_prefixes();  // the previous piece's prefixes (behind the wait: stores count in vmcnt)
+        raw_barrier();     // (B)
+        dma_cur = dma_next;
+#else
         __syncthreads();  // (A)
         if (i == 0 && tid < np) s.halo[tid] = h;
         spec_stage(s, v, i);
         flush_prefixes();  // the previous piece's prefixes, ahead of the next loads
         if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
         __syncthreads();  // (B)
+#endif
+#ifdef HG_SPEC_STREAM_ONLY  // timing experiment: staging only after piece 0 (results invalid)
+        if (i > 0) continue;
+#endif
         if (i == 0 && b == 0) {
             X = X0 = a.entry;  // the first batch's entry is known exactly
         } else if (i == 0) {
@@ -3224,6 +3313,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         total += ps.count;
         X = ps.kind == PK_EMPTY ? X : X + (uint64_t)ps.count * ps.R;
     }
+#if HG_SPEC_GLDS
+    lw_wait_vm(0);  // a break leaves the next piece's DMA in flight
+#endif
     flush_prefixes();
     if (hop) {
         bad = 0;
@@ -3231,9 +3323,17 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     }
     if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
 
+#if HG_LW_FUSE
+    if (HG_LW && !ok && hop && __builtin_amdgcn_readfirstlane(s.hcode) == SB_HOP_SMALL) {
+        uint32_t why = 0;
+        const bool lok = lw_batch(s, spec_alt, a, p0, np, sp, X0, X, total, why);
+        if (tid == 0) spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
+        return;
+    }
+#endif
     if (tid == 0) {
         const uint32_t code = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
-        if (HG_LW && !ok && code == SB_HOP_SMALL) {
+        if (HG_LW && !HG_LW_FUSE && !ok && code == SB_HOP_SMALL) {
             // small records: left to decode_lw_kernel, which publishes the
             // batch (its counts and links) once its lane walks are done
             SpecBatch o;
@@ -3732,7 +3832,7 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
                           : (size_t)env_or("HG_DECODE_SPEC_PAD", 0);
     hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), spec_pad, stream, a,
                        a.sbatch, const_cast<SpecPiece*>(a.spiece));
-    if (HG_LW)
+    if (HG_LW && !HG_LW_FUSE)
         hipLaunchKernelGGL(decode_lw_kernel, dim3(a.nspec), dim3(THREADS), 0, stream, a, a.sbatch,
                            const_cast<SpecPiece*>(a.spiece));
     const uint32_t grid = a.nbatches > a.nspec ? a.nbatches : a.nspec;
@@ -3863,7 +3963,7 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
         else
             hipLaunchKernelGGL(decode_spec_multi<false>, dim3(pre_s[ntab]), dim3(THREADS), 0, stream,
                                dargs, dpre_s, ntab);
-        if (HG_LW)
+        if (HG_LW && !HG_LW_FUSE)
             hipLaunchKernelGGL(decode_lw_multi, dim3(pre_s[ntab]), dim3(THREADS), 0, stream, dargs,
                                dpre_s, ntab);
     }

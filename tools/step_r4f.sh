@@ -1,6 +1,8 @@
-# Round 4: rank loop (single pending read, packed keys), lane-guess rule
-# with the zero bits from the masks, then the merge and decode GPU tests.
+# Round 4: LDS-DMA pre-pass staging + DMA issued from asm (no compiler
+# vmcnt(0) before LDS reads): decode GPU tests on the new library, then a
+# same-box A/B against the register-staged / builtin-DMA build (old) and the
+# asm DMA for the lane walks only (lwasm).
 set -e
-TAG=r4f tools/run.sh merge
-WL="cfg2 small medium midlarge zero" VARIANTS="nonz1" TAG=r4f tools/run.sh ab
-TAG=r4f PYT="tests/test_merge_gpu.py tests/test_decode_gpu.py" tools/run.sh tests
+TAG=r4f PYT="tests/test_decode_gpu.py" tools/run.sh tests
+WL="cfg2 small medium mixed4k zsmall midlarge zmidlarge" VARIANTS="old lwasm fuse" TAG=r4f tools/run.sh ab
+HG_LIBRARY=$PWD/build_exp/fuse/libhorreum_gpu.so TAG=r4f_fuse PYT="tests/test_decode_gpu.py" tools/run.sh tests
