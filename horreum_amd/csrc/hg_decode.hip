@@ -155,6 +155,15 @@ struct SpecBatch {                // one per pre-pass batch
     uint64_t pad;
 };
 
+// HG_SPEC_EMIT: the pre-pass writes the spans of stride batches at their
+// speculated positions (spec_body; decode_body then has nothing to write
+// when every batch was such a batch).  Off: measured on cfg 2 the pre-pass
+// went 170 -> 267 us with the span stores among its reads (0.213 -> 0.274 ms
+// per decode, same box, profiles/r4_ab_spec_emit.log), far more than the 25
+// us decode_kernel takes to write them on its own.
+#ifndef HG_SPEC_EMIT
+#define HG_SPEC_EMIT 0
+#endif
 // Control words of a decode call (zeroed with the statuses before launch).
 struct DecodeCtl {
     uint32_t ticket;              // decode_kernel batch tickets
@@ -162,6 +171,13 @@ struct DecodeCtl {
     uint32_t progress;            // general batches published (INCL / ERR): the look-back's
                                   // waits restart their budget whenever it moves
     uint32_t repairs;             // pre-pass batches spliced onto their predecessor's exit
+    // speculative spans (HG_SPEC_EMIT): stride batches that wrote their spans
+    // at (x0 - entry) / R, their records, and the largest R and ~R among them
+    // (spec_done: pre-pass batches finished; spec_all: all of them such
+    // batches, the result written)
+    uint32_t spec_cnt, spec_done;
+    unsigned long long spec_total, spec_rmax, spec_rnmax;
+    uint32_t spec_all, spec_pad;
 };
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
@@ -1465,12 +1481,15 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         if (DIAG && tid == 0) dg[slot] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start); \
     } while (0)
 
+    // every span already written by the pre-pass (HG_SPEC_EMIT; spec_body's
+    // last batch checked it and wrote the result)
+    const bool sd = HG_SPEC_EMIT && a.ctl->spec_all == 1u;
     // ---- spans of the pre-pass's resolved prefix (workgroup e = batch e) ----------
     const uint32_t fb = first_bad(a.ctl, a.nspec);
     // Only batches whose whole general batch is resolved: the general engine
     // redoes a general batch that holds an unresolved pre-pass batch (and
     // reuses the scratch spans of its pieces meanwhile).
-    if (blk < fb && min((blk / a.q + 1) * a.q, a.nspec) <= fb) {
+    if (!sd && blk < fb && min((blk / a.q + 1) * a.q, a.nspec) <= fb) {
         const uint32_t e = blk;
         const uint32_t ep0 = e * a.sbp;
         const uint32_t enp = min(a.sbp, a.npieces - ep0);
@@ -1489,7 +1508,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             *a.result = r;
         }
     }
-    if (fb >= a.nspec || blk >= a.nbatches) return;  // nothing left for the general engine
+    if (sd || fb >= a.nspec || blk >= a.nbatches) return;  // nothing left for the general engine
     if (tid == 0) s.batch = atomicAdd(a.ticket, 1u);
     __syncthreads();
     if (min((s.batch + 1) * a.q, a.nspec) <= fb) {
@@ -2284,7 +2303,7 @@ __device__ __forceinline__ void lw_wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// s_waitcnt vmcnt(min(n, 8)): the wave's vector memory operations complete in
+// s_waitcnt vmcnt(min(n, 12)): the wave's vector memory operations complete in
 // issue order, so with the chunk DMA issued before n span stores this waits
 // for the DMA only (fewer than n allowed outstanding is merely conservative).
 __device__ __forceinline__ void lw_wait_vm(uint32_t n) {
@@ -2297,7 +2316,11 @@ __device__ __forceinline__ void lw_wait_vm(uint32_t n) {
         case 5: __asm__ volatile("s_waitcnt vmcnt(5)" ::: "memory"); break;
         case 6: __asm__ volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
         case 7: __asm__ volatile("s_waitcnt vmcnt(7)" ::: "memory"); break;
-        default: __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 8: __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+        case 9: __asm__ volatile("s_waitcnt vmcnt(9)" ::: "memory"); break;
+        case 10: __asm__ volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
+        case 11: __asm__ volatile("s_waitcnt vmcnt(11)" ::: "memory"); break;
+        default: __asm__ volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     }
 }
 
@@ -3160,11 +3183,24 @@ __device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb,
 #ifndef HG_SPEC_GLDS
 #define HG_SPEC_GLDS 1
 #endif
+// HG_SPEC_ST_AFTER: a piece's stores issued behind the next piece's DMA with
+// counted waits that skip them (1), or behind the wait for the DMA (0).
+// Measured 0 faster: cfg 2 0.2034 -> 0.2128 ms with 1 (same box, 3 rounds,
+// profiles/r4_ab_fuse.log) -- waiting for the record stores paces the stream.
+#ifndef HG_SPEC_ST_AFTER
+#define HG_SPEC_ST_AFTER 0
+#endif
 // HG_LW_FUSE: the lane walks of SB_HOP_SMALL batches run in the pre-pass
 // workgroup itself (no decode_lw_kernel launch); the second piece buffer is
-// then also lw_batch's chunk buffer of waves 2 and 3.
+// then also lw_batch's chunk buffer of waves 2 and 3.  With the pieces
+// staged by LDS-DMA the pre-pass already needs the lane walks' LDS (4
+// workgroups per CU either way), so the fused kernel costs the stride path
+// nothing: same box, 3 rounds (profiles/r4_ab_fuse.log): cfg 2 0.2034 ->
+// 0.2028 ms, small 0.1471 -> 0.1407, medium 0.191 -> 0.185, zero-valued
+// small 0.1565 -> 0.1505, zero-valued 400-1200 B 0.276 -> 0.271, 400-1200 B
+// 0.150 -> 0.152.
 #ifndef HG_LW_FUSE
-#define HG_LW_FUSE 0
+#define HG_LW_FUSE 1
 #endif
 #if HG_LW_FUSE && !HG_SPEC_GLDS
 #error "HG_LW_FUSE needs HG_SPEC_GLDS (the second buffer)"
@@ -3184,6 +3220,34 @@ __device__ __forceinline__ bool spec_dma(const DecodeArgs& a, uint32_t p, uint8_
 }
 __device__ __forceinline__ void raw_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Thread 0 of every pre-pass batch, after its publication: the last batch
+// to finish checks whether every batch wrote its spans at their final
+// positions (speculative spans, spec_body: none bad -- so each links to its
+// predecessor's exit and the first enters at the entry -- all of them such
+// batches, one R, room for all) and then writes the result and sets
+// spec_all, so decode_kernel has nothing left to do.  A batch the lane walks
+// publish later is not such a batch, so its count never completes the set.
+__device__ __forceinline__ void spec_last_check(const DecodeArgs& a, const SpecBatch* sb) {
+    __threadfence();
+    if (atomicAdd(&a.ctl->spec_done, 1u) != a.nspec - 1) return;
+    __threadfence();
+    DecodeCtl* c = a.ctl;
+    const uint32_t bad = __hip_atomic_load(&c->bad_rev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t cnt = __hip_atomic_load(&c->spec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long n = ld_agent(&c->spec_total);
+    const unsigned long long rmax = ld_agent(&c->spec_rmax), rnmax = ld_agent(&c->spec_rnmax);
+    if (bad != 0 || cnt != a.nspec || rmax != ~rnmax || n > a.cap) return;
+    hg_decode_result r;
+    r.n_records = n;
+    r.kind = HG_OK;
+    r.reserved = 0;
+    r.err_offset = a.range ? a.obase + __hip_atomic_load(&sb[a.nspec - 1].exit, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT)
+                           : 0;
+    *a.result = r;
+    c->spec_all = 1u;
 }
 
 template <bool KPRE>
@@ -3211,15 +3275,45 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     constexpr uint32_t KPT = KPRE ? MAX_REC_PIECE / THREADS : 1;  // prefixes per thread
     uint4 pf[KPT];
     uint32_t pf_n = 0, pf_piece = 0;  // the pending prefixes (KPRE)
-    auto flush_prefixes = [&]() {
-        if (!KPRE || !pf_n) return;
+    // The flushes return a lower bound of the store instructions this wave
+    // issued (one per 16-byte store; a wave issues one when its first lane
+    // does), for the counted waits of the LDS-DMA staging.
+    const uint32_t w64 = tid & ~63u;  // the wave's first thread
+    auto flush_prefixes = [&]() -> uint32_t {
+        if (!KPRE || !pf_n) return 0u;
         hg_span* slot = a.scratch + (size_t)pf_piece * MAX_REC_PIECE;
+        uint32_t n = 0;
 #pragma unroll
-        for (uint32_t k = 0; k < KPT; ++k)
+        for (uint32_t k = 0; k < KPT; ++k) {
             if (tid + k * THREADS < pf_n) *reinterpret_cast<uint4*>(slot + tid + k * THREADS) = pf[k];
+            n += w64 + k * THREADS < pf_n ? 1u : 0u;
+        }
         if (tid == 0) piece_tags(a)[pf_piece] = a.kpre_tag;
         pf_n = 0;
+        return n + (w64 == 0 ? 1u : 0u);
     };
+    // Speculative spans (HG_SPEC_EMIT): a stride batch entered at X0 with
+    // (X0 - entry) % R == 0 whose pieces all have that R writes its records'
+    // spans at (x - entry) / R -- their final positions if every batch before
+    // it is such a batch with the same R and the chain links up.  decode_kernel
+    // checks exactly that (DecodeCtl: no batch bad, spec_cnt == nspec, one R)
+    // and then has nothing left to write; otherwise it writes every span as
+    // before.  A piece's spans are written during the next piece, behind its
+    // staging wait (stores count in vmcnt, as the prefixes above).
+    bool spec = HG_SPEC_EMIT != 0;
+    uint64_t spec_R = 0, spec_idx = 0;            // the batch's R, the next record's position
+    uint64_t sw_x = 0, sw_idx = 0;                // the pending piece: first record, position
+    uint32_t sw_n = 0, sw_kl = 0, sw_vl = 0;
+    auto flush_spans = [&]() -> uint32_t {
+        if (!HG_SPEC_EMIT || !sw_n) return 0u;
+        for (uint32_t t = tid; t < sw_n; t += THREADS)
+            if (sw_idx + t < a.cap) write_span(a.spans, sw_idx + t, a.obase + sw_x + t * spec_R, sw_kl, sw_vl);
+        // (past the capacity some stores are skipped: count none)
+        const uint32_t n = sw_idx + sw_n <= a.cap && w64 < sw_n ? (sw_n - w64 + THREADS - 1) / THREADS : 0u;
+        sw_n = 0;
+        return n;
+    };
+    uint32_t nst_prev = 0;  // stores this wave issued after the DMA of the piece being staged
     // Two barriers per piece: (A) the previous piece is done with LDS; stage
     // v and the halo and put the next piece's loads in flight before (B).
     for (uint32_t i = 0; i < np; ++i) {
@@ -3232,7 +3326,19 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         data = cur;
         raw_barrier();  // (A) every wave is done with the other buffer (piece i - 1)
         const bool dma_next = i + 1 < np && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
-        lw_wait_vm(dma_next ? GPT : 0);  // this wave's part of piece i landed
+        if (HG_SPEC_ST_AFTER) {
+            // the previous piece's prefixes and spans go out behind the next
+            // piece's DMA; the wait for this piece's DMA allows every younger
+            // operation (vector memory operations complete in issue order),
+            // so it never waits for a store
+            const uint32_t nst = flush_prefixes() + flush_spans();
+            lw_wait_vm(nst_prev + (dma_next ? GPT : 0) + nst);  // this wave's part of piece i landed
+            nst_prev = nst;
+        } else {
+            lw_wait_vm(dma_next ? GPT : 0);  // (and every store before the DMA)
+            flush_prefixes();
+            flush_spans();
+        }
         if (!dma_cur) {                  // the tail piece
 #pragma unroll
             for (uint32_t q = 0; q < GPT; ++q)
@@ -3242,7 +3348,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         if (i == 0 && tid < np) s.halo[tid] = h;
         if (tid < 4)  // thread 0 reads back its own halo write when i == 0
             *reinterpret_cast<uint4*>(cur + PIECE + tid * 16) = tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
-        flush_prefixes();  // the previous piece's prefixes (behind the wait: stores count in vmcnt)
         raw_barrier();     // (B)
         dma_cur = dma_next;
 #else
@@ -3250,6 +3355,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         if (i == 0 && tid < np) s.halo[tid] = h;
         spec_stage(s, v, i);
         flush_prefixes();  // the previous piece's prefixes, ahead of the next loads
+        flush_spans();
         if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
         __syncthreads();  // (B)
 #endif
@@ -3280,6 +3386,24 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             hop = true;
             break;
         }
+        if (HG_SPEC_EMIT && spec) {
+            if (i == 0) {
+                spec = ps.kind == PK_STRIDE && X0 >= a.entry && (X0 - a.entry) % ps.R == 0;
+                if (spec) {
+                    spec_R = ps.R;
+                    spec_idx = (X0 - a.entry) / ps.R;
+                }
+            }
+            if (spec && ps.kind == PK_STRIDE) {
+                spec = ps.R == spec_R;
+                sw_x = ps.x;
+                sw_idx = spec_idx;
+                sw_n = spec ? ps.count : 0u;
+                sw_kl = ps.kl;
+                sw_vl = ps.vl;
+                spec_idx += ps.count;
+            }
+        }
         if (tid == 0) {
             SpecPiece o;
             o.x = ps.x;
@@ -3290,6 +3414,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             o.pad = 0;
             sp[p] = o;
         }
+        nst_prev += w64 == 0 ? 2u : 0u;  // the 32-byte record: two stores at least
         if (KPRE && ps.kind == PK_STRIDE) {  // compaction mode: key prefixes from LDS
             const uint32_t xr = (uint32_t)(X - base), R = (uint32_t)ps.R;
 #pragma unroll
@@ -3317,6 +3442,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     lw_wait_vm(0);  // a break leaves the next piece's DMA in flight
 #endif
     flush_prefixes();
+    flush_spans();
     if (hop) {
         bad = 0;
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
@@ -3331,6 +3457,12 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         return;
     }
 #endif
+    if (HG_SPEC_EMIT && tid == 0 && spec && !hop && ok) {
+        atomicAdd(&a.ctl->spec_cnt, 1u);
+        atomicAdd(&a.ctl->spec_total, (unsigned long long)total);
+        atomicMax(&a.ctl->spec_rmax, (unsigned long long)spec_R);
+        atomicMax(&a.ctl->spec_rnmax, ~(unsigned long long)spec_R);
+    }
     if (tid == 0) {
         const uint32_t code = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
         if (HG_LW && !HG_LW_FUSE && !ok && code == SB_HOP_SMALL) {
@@ -3345,6 +3477,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         } else {
             spec_publish(a, sb, b, X0, X, total, ok, code);
         }
+        if (HG_SPEC_EMIT) spec_last_check(a, sb);
     }
 }
 

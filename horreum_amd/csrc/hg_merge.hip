@@ -703,6 +703,336 @@ __global__ __launch_bounds__(THREADS, FINAL ? 6 : 5) void merge_level_kernel(Mer
     }
 }
 
+// ---- 3b. one-pass k-way merge (K <= KW_MAX runs) -----------------------------------------
+// The 3 rounds of 2-way merges above move every entry through HBM three times
+// (8 runs: 2 x 86 + 156 us, plus 3 x 23 us of split searches on the cfg 5
+// leg).  Here one pass does it: tiles are cut at sampled splitters instead of
+// fixed output positions, so a tile's share of every run is known from K
+// searches and the tile merges its K segments inside LDS.
+//   kw_sample_kernel: every KW_S-th entry of each run (a sample), in run
+//     order, into a compact array (L2-resident for the searches below).
+//   kw_split_kernel: each sample's rank among all samples in the strict total
+//     order (key, run) -- K - 1 searches over the other runs' samples, one
+//     lane each -- and for every KW_M-th rank (a splitter) its exact position
+//     in every run: the search narrowed to the KW_S entries between two
+//     samples.  Tile k = the entries from splitter k to splitter k + 1: in run
+//     i at most KW_S x (samples of run i in between + 1) - 1 entries, so
+//     <= KW_S KW_M + K (KW_S - 1) <= KW_CAP in all.
+//   kw_merge_kernel: a tile's K segments into LDS, log2(K) pairwise merge
+//     passes in place (merge path per thread, ties: the lower run first; a
+//     B element equal to the last A element before it is dead -- newest
+//     wins, as the rounds), then the FINAL round's emission (look-back over
+//     the tiles' live counts, pairs).  An entry equal to one of a higher
+//     priority run in an earlier tile can only be its segment's first and
+//     that run's entry just before the tile: checked when staging.
+// Measured (cfg 5 leg, 8 x 1 M, same box, profiles/r4_ab_spec_emit.log): one
+// pass is slower than the rounds -- kw_merge_kernel 425 us + 43 us of splits
+// against 2 x 93 + 161 us + 3 x 22 us; without its LDS passes it still takes
+// 258 us (the FINAL emission's span lookups and look-back dominate, at 4
+// workgroups per CU), and the three in-LDS passes cost another 167 us of
+// dependent LDS compares.  Kept behind HG_MERGE_KWAY=1 (tests compare it with
+// the oracle and the rounds), not the default.
+constexpr uint32_t KW_S = 64;
+constexpr uint32_t KW_M = 16;
+constexpr uint32_t KW_MAX = 8;
+constexpr uint32_t KW_CAP = 1536;  // >= KW_S KW_M + KW_MAX (KW_S - 1) = 1528
+constexpr uint32_t KW_THREADS = 384;
+constexpr uint32_t KW_EPT = KW_CAP / KW_THREADS;  // 4
+constexpr uint32_t KW_WPT = 3 * KW_EPT;           // 8-byte words per thread when staging
+static_assert(KW_S * KW_M + KW_MAX * (KW_S - 1) <= KW_CAP, "tile bound");
+
+struct KwArgs {
+    uint64_t roff[KW_MAX + 1];  // the runs' entry offsets in `in`
+    uint32_t soff[KW_MAX + 1];  // their samples' offsets (ceil(len / KW_S) each)
+    uint32_t K, ns, ntiles;     // runs, samples, tiles (ceil(ns / KW_M))
+};
+
+__device__ __forceinline__ uint32_t kw_run_of_sample(const KwArgs& k, uint32_t s) {
+    uint32_t j = 0;
+#pragma unroll
+    for (uint32_t i = 1; i < KW_MAX; ++i)
+        if (i < k.K && k.soff[i] <= s) j = i;
+    return j;
+}
+
+// Samples, and the FINAL look-back statuses zeroed (one launch fewer).
+__global__ __launch_bounds__(THREADS) void kw_sample_kernel(KwArgs k, const MEnt* in, MEnt* samp,
+                                                            unsigned long long* zst) {
+    const uint32_t s = blockIdx.x * THREADS + threadIdx.x;
+    if (s < k.ntiles) zst[s] = 0;
+    if (s >= k.ns) return;
+    const uint32_t j = kw_run_of_sample(k, s);
+    samp[s] = in[k.roff[j] + (uint64_t)(s - k.soff[j]) * KW_S];
+}
+
+// y (run i) before x (run j) in the order (key, run).
+__device__ __forceinline__ bool kw_before(const MergeArgs& a, const MEnt& y, uint32_t i, const MEnt& x,
+                                          uint32_t j) {
+    const int c = key_cmp(a, y, x);
+    return c < 0 || (c == 0 && i < j);
+}
+
+// Eight lanes per sample (lane i: run i).  split[t * K + i] = tile t's first
+// entry of run i (run-relative), t = 0 .. ntiles (the last row: the run ends).
+__global__ __launch_bounds__(THREADS) void kw_split_kernel(MergeArgs a, KwArgs k, const MEnt* in,
+                                                           const MEnt* samp, uint64_t* split,
+                                                           const unsigned long long* err) {
+    const uint32_t gt = blockIdx.x * THREADS + threadIdx.x;
+    const uint32_t s = gt / KW_MAX, i = gt % KW_MAX;
+    if (s >= k.ns || *err != ~0ull) return;  // (the merge kernel aborts on err)
+    const uint32_t j = kw_run_of_sample(k, s);
+    const uint32_t u = s - k.soff[j];
+    const MEnt x = samp[s];
+    // q: samples of run i before x
+    uint32_t q = 0;
+    if (i == j) {
+        q = u;
+    } else if (i < k.K) {
+        uint32_t lo = 0, hi = k.soff[i + 1] - k.soff[i];
+        const MEnt* si = samp + k.soff[i];
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (kw_before(a, si[mid], i, x, j)) lo = mid + 1;
+            else hi = mid;
+        }
+        q = lo;
+    }
+    uint32_t rank = q;  // sum over the sample's eight lanes
+#pragma unroll
+    for (uint32_t d = 1; d < KW_MAX; d <<= 1) rank += __shfl_xor(rank, d, 64);
+    if (s == 0 && i < k.K) split[(uint64_t)k.ntiles * k.K + i] = k.roff[i + 1] - k.roff[i];
+    if (rank % KW_M || i >= k.K) return;
+    const uint64_t t = rank / KW_M;
+    uint64_t pos;
+    if (i == j) {
+        pos = (uint64_t)u * KW_S;
+    } else {
+        // entries of run i before x: in [KW_S (q - 1) + 1, KW_S q] (q > 0), else 0
+        const uint64_t len = k.roff[i + 1] - k.roff[i];
+        uint64_t lo = q ? (uint64_t)KW_S * (q - 1) + 1 : 0, hi = min((uint64_t)KW_S * q, len);
+        const MEnt* ri = in + k.roff[i];
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;  // entry mid before x <=> more than mid entries are
+            if (kw_before(a, ri[mid], i, x, j)) lo = mid + 1;
+            else hi = mid;
+        }
+        pos = lo;
+    }
+    split[t * k.K + i] = pos;
+}
+
+struct KwSmem {
+    alignas(16) MEnt seg[KW_CAP];
+    MEnt prev[KW_MAX];
+    uint32_t so[KW_MAX + 1];  // segment offsets in seg (so[i] = N for i >= K)
+    uint64_t c0[KW_MAX];      // the tile's first entry of each run (run-relative)
+    uint32_t has_prev[KW_MAX];
+    uint32_t bad;
+};
+
+__global__ __launch_bounds__(KW_THREADS, 2) void kw_merge_kernel(MergeArgs a, KwArgs k, const MEnt* in,
+                                                                  const uint64_t* split,
+                                                                  unsigned long long* err, FinalArgs f) {
+    __shared__ KwSmem s;
+    __shared__ uint32_t fin_tmp[KW_THREADS / 64];
+    __shared__ uint64_t fin_base;
+    __shared__ uint64_t fin_roff[FIN_LDS_TABLES + 1], fin_sp[FIN_LDS_TABLES], fin_toff[FIN_LDS_TABLES];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t bx = blockIdx.x;
+    const uint32_t K = k.K;
+    const bool fin_lds = a.ntables <= FIN_LDS_TABLES;
+    if (fin_lds) {
+        if (tid <= a.ntables) fin_roff[tid] = a.run_off[tid];
+        if (tid < a.ntables) {
+            fin_sp[tid] = reinterpret_cast<uint64_t>(a.spans[tid]);
+            fin_toff[tid] = a.table_off[tid];
+        }
+    }
+    if (tid == 0) s.bad = 0;
+    if (tid < KW_MAX) {
+        // once the order check failed the split kernel wrote nothing: no
+        // split is read then, and none is used unless it lies in its run
+        const bool errset = *err != ~0ull;
+        uint64_t c0 = 0, c1 = 0;
+        if (tid < K && !errset) {
+            c0 = split[(uint64_t)bx * K + tid];
+            c1 = split[(uint64_t)(bx + 1) * K + tid];
+        }
+        const uint64_t rl = tid < K ? k.roff[tid + 1] - k.roff[tid] : 0;
+        const bool okc = c0 <= c1 && c1 <= rl && c1 - c0 <= KW_CAP;
+        if (!okc) c0 = c1 = 0;
+        s.c0[tid] = c0;
+        // segment lengths -> offsets (eight lanes of wave 0)
+        const uint32_t len = okc ? (uint32_t)(c1 - c0) : KW_CAP + 1;
+        uint32_t incl = len;
+#pragma unroll
+        for (uint32_t d = 1; d < KW_MAX; d <<= 1) {
+            const uint32_t o = __shfl_up(incl, d, 64);
+            if (tid >= d) incl += o;
+        }
+        s.so[tid + 1] = incl;
+        if (tid == 0) s.so[0] = 0;
+        s.has_prev[tid] = tid < K && c0 > 0;
+        if (tid < K && c0 > 0) s.prev[tid] = in[k.roff[tid] + c0 - 1];
+        if (tid == KW_MAX - 1 && (incl > KW_CAP || errset)) s.bad = 1;
+    }
+    __syncthreads();
+    if (s.bad) {  // unsorted input (err) or splits no sorted input gives
+        if (*err == ~0ull && tid == 0) atomicMin(err, 0ull);
+        if (tid < 64) final_lookback(f, bx, 0, err);
+        return;
+    }
+    const uint32_t N = s.so[KW_MAX];
+    {  // the segments as 8-byte words, every load before the first LDS write
+        uint64_t v[KW_WPT];
+        uint64_t* ws = reinterpret_cast<uint64_t*>(s.seg);
+#pragma unroll
+        for (uint32_t r = 0; r < KW_WPT; ++r) {
+            const uint32_t w = tid + r * KW_THREADS;
+            v[r] = 0;
+            if (w < 3 * N) {
+                const uint32_t e = w / 3;
+                uint32_t i = 0;
+#pragma unroll
+                for (uint32_t q = 1; q < KW_MAX; ++q)
+                    if (s.so[q] <= e) i = q;
+                const uint64_t* src = reinterpret_cast<const uint64_t*>(in + k.roff[i] + s.c0[i]);
+                v[r] = src[w - 3 * s.so[i]];
+            }
+        }
+#pragma unroll
+        for (uint32_t r = 0; r < KW_WPT; ++r) {
+            const uint32_t w = tid + r * KW_THREADS;
+            if (w < 3 * N) ws[w] = v[r];
+        }
+    }
+    __syncthreads();
+    // a segment's first entry equal to a higher-priority run's entry just
+    // before the tile: dead (newest wins across the tile edge)
+    if (tid < K && s.so[tid + 1] > s.so[tid]) {
+        MEnt& x = s.seg[s.so[tid]];
+        bool eq = false;
+        for (uint32_t i = 0; i < tid; ++i)
+            if (s.has_prev[i] && key_cmp(a, s.prev[i], x) == 0) eq = true;
+        if (eq) x.gd |= DEAD;
+    }
+    __syncthreads();
+    MEnt fx[KW_EPT];
+    const uint32_t d0 = tid * KW_EPT;
+#ifdef HG_KW_NOPASS  // timing experiment: no merge passes (results invalid)
+    for (uint32_t e = 0; e < KW_EPT; ++e) fx[e] = s.seg[min(d0 + e, N - 1)];
+    for (uint32_t w = K; w < K; w <<= 1) {
+#else
+    for (uint32_t w = 1; w < K; w <<= 1) {
+#endif
+        // pass: runs [2 p w, (2 p + 1) w) (A) and [(2 p + 1) w, (2 p + 2) w) (B) merge
+        uint32_t pend = 0, ai = 0, bj = 0, A0 = 0, Am = 0, B1 = 0;
+#pragma unroll
+        for (uint32_t e = 0; e < KW_EPT; ++e) {
+            const uint32_t pos = d0 + e;
+            if (pos >= N) break;
+            if (pos >= pend) {  // the pair holding pos, and its merge-path split there
+                uint32_t p = 0;
+                for (uint32_t q = 2 * w; q < KW_MAX; q += 2 * w)
+                    if (s.so[q] <= pos) p = q;
+                A0 = s.so[p];
+                Am = s.so[p + w];
+                B1 = s.so[min(p + 2 * w, KW_MAX)];
+                pend = B1;
+                const uint32_t na = Am - A0, nb = B1 - Am, dd = pos - A0;
+                uint32_t lo = dd > nb ? dd - nb : 0, hi = dd < na ? dd : na;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (key_cmp(a, s.seg[A0 + mid], s.seg[Am + dd - 1 - mid]) <= 0) lo = mid + 1;
+                    else hi = mid;
+                }
+                ai = lo;
+                bj = dd - lo;
+            }
+            const uint32_t na = Am - A0, nb = B1 - Am;
+            const MEnt* SA = s.seg + A0;
+            const MEnt* SB = s.seg + Am;
+            MEnt x;
+            if (bj >= nb || (ai < na && key_cmp(a, SA[ai], SB[bj]) <= 0)) {
+                x = SA[ai++];
+            } else {
+                x = SB[bj++];
+                if (ai > 0 && key_cmp(a, SA[ai - 1], x) == 0) x.gd |= DEAD;
+            }
+            fx[e] = x;
+        }
+        __syncthreads();  // every thread is done reading this pass's input
+        if (2 * w < K) {  // another pass follows
+#pragma unroll
+            for (uint32_t e = 0; e < KW_EPT; ++e)
+                if (d0 + e < N) s.seg[d0 + e] = fx[e];
+            __syncthreads();
+        }
+    }
+    // FINAL emission (as merge_level_kernel<true>)
+    const uint32_t ne = d0 < N ? min(KW_EPT, N - d0) : 0u;
+    uint32_t fcnt = 0;
+#pragma unroll
+    for (uint32_t e = 0; e < KW_EPT; ++e) fcnt += e < ne && !(fx[e].gd & DEAD) ? 1u : 0u;
+    uint32_t ftot;
+    const uint32_t fpre = hgk::block_excl_scan<KW_THREADS / 64>(fcnt, fin_tmp, ftot);
+    if (tid < 64) {
+        const uint64_t b = final_lookback(f, bx, ftot, err);
+        if (tid == 0) {
+            fin_base = b;
+            if (bx + 1 == f.ntiles) {
+                hg_merge_result r;
+                r.n_out = b + ftot;
+                r.kind = HG_OK;
+                r.table = 0;
+                r.index = 0;
+                *f.result = r;
+            }
+        }
+    }
+    hg_pair* lp = reinterpret_cast<hg_pair*>(s.seg);
+    uint32_t r = fpre;
+    uint32_t tk[KW_EPT];
+    hg_span spk[KW_EPT];
+    uint64_t tof[KW_EPT];
+#pragma unroll
+    for (uint32_t e = 0; e < KW_EPT; ++e) {
+        const uint64_t g = e < ne ? (uint64_t)(fx[e].gd & ~DEAD) : 0ull;
+        if (fin_lds) {
+            uint32_t lo = 0, hi = a.ntables;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (fin_roff[mid] <= g) lo = mid;
+                else hi = mid;
+            }
+            tk[e] = lo;
+            tof[e] = fin_toff[lo];
+            spk[e] = reinterpret_cast<const hg_span*>(fin_sp[lo])[g - fin_roff[lo]];
+        } else {
+            tk[e] = run_of(a, g);
+            tof[e] = a.table_off[tk[e]];
+            spk[e] = a.spans[tk[e]][g - a.run_off[tk[e]]];
+        }
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < KW_EPT; ++e) {
+        if (e >= ne || (fx[e].gd & DEAD)) continue;
+        const hg_span sp = spk[e];
+        hg_pair p;
+        p.key_off = tof[e] + sp.off + 16;
+        p.val_off = p.key_off + sp.klen;
+        p.klen = sp.klen;
+        p.vlen = sp.vlen;
+        lp[r++] = p;
+    }
+    __syncthreads();  // also publishes fin_base
+    const uint64_t w0 = 3 * fin_base, wcap = 3 * f.cap;
+    const uint64_t* s8 = reinterpret_cast<const uint64_t*>(s.seg);
+    uint64_t* o8 = reinterpret_cast<uint64_t*>(f.out);
+    for (uint32_t i = tid; i < 3 * ftot; i += KW_THREADS)
+        if (w0 + i < wcap) o8[w0 + i] = s8[i];
+}
+
 // ---- 4. live entries -> hg_pair ---------------------------------------------------------
 __global__ __launch_bounds__(THREADS) void merge_count_kernel(MergeArgs a, const MEnt* e,
                                                               uint32_t* tile_live) {
@@ -1455,11 +1785,38 @@ uint64_t round_offsets(uint64_t* r, uint64_t nr) {
 // `in` is never written unless it is b2).
 int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hgm::MEnt* in,
                   hgm::MEnt* b1, hgm::MEnt* b2, const MergeWs& w, unsigned long long* err,
-                  hgm::FinalArgs fa, hipStream_t stream) {
+                  hgm::FinalArgs fa, hipStream_t stream, const uint64_t* h_roff = nullptr) {
     using namespace hgm;
     const uint64_t ntiles = (a.n + TILE - 1) / TILE;
     fa.st = w.lb_status;
     fa.ntiles = (uint32_t)ntiles;
+    // 3..KW_MAX runs with their offsets on the host and HG_MERGE_KWAY=1: the
+    // one-pass k-way merge (section 3b; not the default: slower, see there)
+    const char* kw_env = getenv("HG_MERGE_KWAY");
+    if (h_roff && nr >= 3 && nr <= KW_MAX && kw_env && strcmp(kw_env, "1") == 0) {
+        KwArgs k{};
+        k.K = (uint32_t)nr;
+        uint64_t ns = 0;
+        for (uint32_t i = 0; i <= KW_MAX; ++i) {
+            const uint64_t o = h_roff[std::min<uint64_t>(i, nr)];
+            k.roff[i] = o;
+            k.soff[i] = (uint32_t)ns;
+            if (i < nr) ns += (h_roff[i + 1] - o + KW_S - 1) / KW_S;
+        }
+        k.ns = (uint32_t)ns;
+        k.ntiles = (uint32_t)((ns + KW_M - 1) / KW_M);
+        fa.ntiles = k.ntiles;
+        MEnt* samp = b1;
+        uint64_t* split = reinterpret_cast<uint64_t*>(b2);
+        hipLaunchKernelGGL(kw_sample_kernel, dim3((uint32_t)((ns + THREADS - 1) / THREADS)), dim3(THREADS), 0,
+                           stream, k, (const MEnt*)in, samp, w.lb_status);
+        hipLaunchKernelGGL(kw_split_kernel, dim3((uint32_t)((ns * KW_MAX + THREADS - 1) / THREADS)),
+                           dim3(THREADS), 0, stream, a, k, (const MEnt*)in, (const MEnt*)samp, split,
+                           (const unsigned long long*)err);
+        hipLaunchKernelGGL(kw_merge_kernel, dim3(k.ntiles), dim3(KW_THREADS), 0, stream, a, k,
+                           (const MEnt*)in, (const uint64_t*)split, err, fa);
+        return HG_LAUNCH_STATUS();
+    }
     if (nr >= 2) {
         bool first = true;  // the first round's split kernel zeroes the look-back statuses
         MEnt* cur = in;
@@ -1688,7 +2045,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     // the rounds ping-pong between e1 and e2, so e0 keeps the entries for the
     // exact loop / the epochs (the first round reads e0)
     int rc = launch_rounds(a, a.run_off + ntables + 1, nruns0, w.e0, w.e1, w.e2, w, w.err, fa,
-                           stream);
+                           stream, r0);
     if (rc != HG_OK) return rc;
     if (defer)
         hipLaunchKernelGGL(merge_flag_kernel, dim3(1), dim3(1), 0, stream,

@@ -660,3 +660,32 @@ def test_hop_entries_keep_tombstones(engine, monkeypatch, seed):
     assert out.kind == 0 and out.n == v.size and np.array_equal(got, want)
     assert (codes == 5).all(), codes  # every batch in hop mode
     assert (first_bad, links, repairs) == (nspec, 0, 0)
+
+
+
+@pytest.mark.parametrize("kv", [(16, 100), (8, 56), (1, 0), (200, 3000)])
+def test_uniform_stride_tables(engine, kv):
+    """Fixed-size records of several sizes: bit-exact, at the capacity
+    boundary too (cap = n, cap = n - 1: the capacity error), and torn last
+    records.  (With -DHG_SPEC_EMIT=1 these are the tables whose spans the
+    pre-pass writes itself -- off by default, hg_decode.hip.)"""
+    n = (24 << 20) // (16 + sum(kv))
+    data = oracle.encode(*corpus.fixed(n, kv[0], kv[1], seed=91))[0]
+    assert_same(engine, data)
+    assert_same(engine, data, cap=n)
+    assert_same(engine, data, cap=n - 1)
+    for cut in (BATCH * 5 + 3, data.size - 1):
+        assert_same(engine, data[:cut])
+
+
+@pytest.mark.parametrize("where", ["middle", "head", "tail"])
+def test_broken_stride_lattice(engine, where):
+    """One record of another size breaks the stride lattice: batches past it
+    are stride runs whose positions are not (x0 - entry) / R."""
+    n = (16 << 20) // 132
+    arena, pairs = corpus.fixed(n, 16, 100, seed=92)
+    i = {"middle": n // 2, "head": 3, "tail": n - 2}[where]
+    pairs = pairs.copy()
+    pairs["vlen"][i] = 37  # one shorter value (its bytes are the next ones in the arena)
+    data = oracle.encode(arena, pairs)[0]
+    assert_same(engine, data)

@@ -642,3 +642,41 @@ def test_compaction_key_length_change_on_the_stride_lattice(engine, monkeypatch,
     want, wblocks, wn = oracle.compacted_table(datas, block_stride=5)
     assert out.status == 0 and out.n == wn
     assert np.array_equal(out.data, want) and np.array_equal(out.blocks, wblocks)
+
+
+@pytest.mark.parametrize("shape", ["identical", "disjoint", "interleaved", "giant_tiny",
+                                   "long_prefix", "three"])
+def test_kway_merge_vs_rounds(engine, monkeypatch, shape):
+    """The one-pass k-way merge (3..8 runs, HG_MERGE_KWAY=1; hg_merge.hip
+    section 3b) against the oracle and the default 2-way rounds on shapes that
+    stress its sampled tiles: every key in every table (dead entries across
+    every tile edge), disjoint key ranges in reverse priority order (tiles of
+    one run), a perfect interleave, one large table among tiny and empty ones
+    (segments at the tile bound), keys sharing 16+ byte prefixes (tail
+    compares inside the LDS passes), and three runs (a run count that is not
+    a power of two)."""
+    rng = np.random.default_rng(77)
+    if shape == "long_prefix":
+        datas = encode_tables(sorted_tables(6, 30000, 0.5, 78, long_prefix=True))
+    else:
+        if shape == "identical":
+            base = np.unique(rng.integers(0, 1 << 40, size=100_000, dtype=np.uint64))
+            keys = [base] * 6
+        elif shape == "disjoint":
+            keys = [np.arange(50_000, dtype=np.uint64) + np.uint64((8 - t) * 1_000_000) for t in range(8)]
+        elif shape == "interleaved":
+            a = np.arange(7 * 40_000, dtype=np.uint64) * np.uint64(3)
+            keys = [a[t::7] for t in range(7)]
+        elif shape == "giant_tiny":
+            keys = _keyed_tables([300_000, 5, 1, 64, 65, 0, 2000, 1], 79)
+        else:
+            keys = _keyed_tables([70_000, 90_000, 50_000], 80)
+        datas = [_encode_keyed(kk, t) if len(kk) else np.zeros(0, np.uint8) for t, kk in enumerate(keys)]
+    monkeypatch.setenv("HG_MERGE_KWAY", "1")
+    res, got, _, offs = device_merge(engine, datas)
+    want, rc = oracle_merge_pairs(datas, offs)
+    assert rc == 0 and res.status == 0 and res.n == want.size
+    assert np.array_equal(got, want)
+    monkeypatch.delenv("HG_MERGE_KWAY")
+    res2, got2, _, _ = device_merge(engine, datas)
+    assert res2.status == 0 and np.array_equal(got2, got)

@@ -21,7 +21,7 @@ def main():
     eng.set_stream(torch.cuda.current_stream(dev))
     per = int(os.environ.get("PER_TABLE", 1_000_000))  # 8_134_407: the per-GPU share of cfg 5
     line = bench.compaction_leg(torch, eng, dev, 1, 0, per_table=per)
-    line["merge_path"] = "k-way buckets" if os.environ.get("HG_MERGE_KWAY") == "1" else "pairwise rounds"
+    line["merge_path"] = "one-pass k-way" if os.environ.get("HG_MERGE_KWAY") == "1" else "pairwise rounds"
     print(json.dumps(line), flush=True)
 
 

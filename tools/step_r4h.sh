@@ -10,3 +10,4 @@ run() {  # name, env...
 }
 run base X=1
 run stream HG_LIBRARY=$PWD/build_exp/stream/libhorreum_gpu.so
+ROUNDS=3 WL="cfg2 small medium" timeout -k 10 600 bash tools/ab_variants.sh base fuse | grep "^==\|cfg2\|small\|medium"

@@ -1,10 +1,12 @@
-# Round 4: compaction without the look-back-status and group-sum memsets and
-# with the merge error word in the staging copy, against HEAD (build_exp/prev);
-# cfg 3 encode both ways; the merge / encode / manager GPU tests.
+# Round 4: speculative spans in the pre-pass (HG_SPEC_EMIT): decode GPU tests
+# on the new library, then a same-box A/B against noemit / fuse, and the
+# kernel durations on cfg 2.
 set -e
-timeout -k 10 400 bash tools/ab_compact.sh base prev | grep "^=="
-for r in 1 2; do
-  echo "== encode base round $r"; timeout -k 10 200 python3 tools/encode_variants.py 2>&1 | grep '^{' | head -1
-  echo "== encode prev round $r"; HG_LIBRARY=$PWD/build_exp/prev/libhorreum_gpu.so timeout -k 10 200 python3 tools/encode_variants.py 2>&1 | grep '^{' | head -1
-done
-TAG=r4i PYT="tests/test_merge_gpu.py tests/test_encode_gpu.py tests/test_manager_gpu.py tests/test_multi_gpu.py tests/test_configs_gpu.py" tools/run.sh tests
+cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
+TAG=r4i_merge PYT=tests/test_merge_gpu.py tools/run.sh tests
+TAG=r4i tools/run.sh tests
+ROUNDS=3 WL="cfg2 small medium zsmall midlarge" timeout -k 10 700 bash tools/ab_variants.sh base noemit fuse
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4i_prof -o run \
+  -- python3 tools/decode_variants.py cfg2 > gpurun_out/r4i_prof.log 2>&1
+grep -h -E "decode_" gpurun_out/r4i_prof/run_kernel_stats.csv
+timeout -k 10 600 bash tools/ab_compact.sh base rounds kwnopass
