@@ -3222,6 +3222,7 @@ __device__ __forceinline__ void raw_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+
 // Thread 0 of every pre-pass batch, after its publication: the last batch
 // to finish checks whether every batch wrote its spans at their final
 // positions (speculative spans, spec_body: none bad -- so each links to its
@@ -3359,8 +3360,8 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
         __syncthreads();  // (B)
 #endif
-#ifdef HG_SPEC_STREAM_ONLY  // timing experiment: staging only after piece 0 (results invalid)
-        if (i > 0) continue;
+#ifdef HG_SPEC_STREAM_ONLY  // timing experiment: staging only (1: after piece 0; results invalid)
+        if (i > 0 || HG_SPEC_STREAM_ONLY == 2) continue;
 #endif
         if (i == 0 && b == 0) {
             X = X0 = a.entry;  // the first batch's entry is known exactly
@@ -3968,6 +3969,9 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
     if (HG_LW && !HG_LW_FUSE)
         hipLaunchKernelGGL(decode_lw_kernel, dim3(a.nspec), dim3(THREADS), 0, stream, a, a.sbatch,
                            const_cast<SpecPiece*>(a.spiece));
+#ifdef HG_SPEC_STREAM_ONLY  // (the general engine would redo the whole table)
+    return HG_LAUNCH_STATUS();
+#endif
     const uint32_t grid = a.nbatches > a.nspec ? a.nbatches : a.nspec;
     if (d_diag)
         hipLaunchKernelGGL(decode_kernel<true>, dim3(grid), dim3(THREADS), 0, stream, a);

@@ -102,10 +102,11 @@ __global__ __launch_bounds__(256) void glds_sweep_kernel(const uint8_t* src, uin
 }
 
 template <int NBUF, int AUX>
-void run_glds(const uint8_t* d, uint64_t len, uint32_t ppb, unsigned long long* out, const char* name) {
+void run_glds(const uint8_t* d, uint64_t len, uint32_t ppb, unsigned long long* out, const char* name,
+              size_t pad = 0) {
     const uint32_t npieces = (uint32_t)(len / PIECE);
     const uint32_t grid = npieces / ppb;
-    const size_t lds = (size_t)NBUF * PIECE;
+    const size_t lds = (size_t)NBUF * PIECE + pad;  // pad: extra LDS to cap occupancy
     CHECK(hipFuncSetAttribute((const void*)glds_sweep_kernel<NBUF, AUX>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int occ = 0;
@@ -193,6 +194,7 @@ int main() {
         run_glds<3, 2>(d, len, ppb, out, "glds x3 nt");
         run_glds<4, 2>(d, len, ppb, out, "glds x4 nt");
         run_glds<3, 0>(d, len, ppb, out, "glds x3");
+        run_glds<2, 2>(d, len, ppb, out, "glds x2 nt, 40 KB LDS", 40960 - 2 * PIECE);
     }
     if (getenv("SWEEP_GLDS_ONLY")) return 0;
     for (uint32_t ppb : {4u, 16u, 64u}) {
