@@ -28,6 +28,8 @@
 #              walks (nofuse: -DHG_LW_FUSE=0)
 #   glds_cfg4  compaction leg and cfg 4 (nofuse: -DHG_LW_FUSE=0; noglds:
 #              -DHG_SPEC_GLDS=0 -DHG_LW_FUSE=0)
+#   span8      lane-walk spans as 8-byte scratch entries (reverted code: the
+#              variant built from it was base; span16 = -DHG_LW_SPAN8=0)
 set -e
 root=$(cd "$(dirname "$0")/.." && pwd)
 variants() {  # name:defines per case (build side)
@@ -42,6 +44,7 @@ variants() {  # name:defines per case (build side)
     spec_emit) echo "emit:-DHG_SPEC_EMIT=1_-DHG_SPEC_ST_AFTER=1 kwnopass:-DHG_KW_NOPASS=1" ;;
     fuse) echo "stafter:-DHG_SPEC_ST_AFTER=1 nofuse:-DHG_LW_FUSE=0" ;;
     glds_cfg4) echo "nofuse:-DHG_LW_FUSE=0 noglds:-DHG_SPEC_GLDS=0_-DHG_LW_FUSE=0" ;;
+    span8) echo "span16:-DHG_LW_SPAN8=0" ;;
   esac
 }
 if [ "$1" = --build ]; then
@@ -75,6 +78,10 @@ case $1 in
     timeout -k 10 400 bash tools/ab_compact.sh base $(names $1) | grep "^==" ;;
   compact_gaps|gather_adj)  # VARIANTS: the older / reverted builds, placed in build_exp/
     timeout -k 10 500 bash tools/ab_compact.sh base ${VARIANTS:?} | grep "^==\|encode_records" ;;
+  span8)
+    TAG=ab4 PYT="tests/test_decode_gpu.py tests/test_merge_gpu.py tests/test_configs_gpu.py" tools/run.sh tests
+    ROUNDS=3 WL="cfg2 small medium zsmall midlarge zmidlarge mixed4k" timeout -k 10 700 bash tools/ab_variants.sh base span16
+    for v in base span16; do use $v; WL="small" kstats $v; done; use base ;;
   dma_asm|fuse)
     TAG=ab4 PYT="tests/test_decode_gpu.py tests/test_merge_gpu.py" tools/run.sh tests
     ROUNDS=3 WL="cfg2 small medium zsmall midlarge zmidlarge" timeout -k 10 700 bash tools/ab_variants.sh base $(names $1) ;;
