@@ -3259,6 +3259,10 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     const uint32_t b = blk;
     const uint32_t p0 = b * a.sbp;
     const uint32_t np = min(a.sbp, a.npieces - p0);
+#ifdef HG_SPEC_TIMELINE  // diagnostics build (tools/spec_timeline.py): realtime stamps
+    uint64_t* const tl = reinterpret_cast<uint64_t*>(a.scratch + (size_t)p0 * MAX_REC_PIECE);
+    if (tid == 0) tl[0] = __builtin_amdgcn_s_memrealtime();
+#endif
 #if HG_SPEC_GLDS
     __shared__ uint64_t spec_alt[SPEC_ALT_BYTES / 8];
     uint8_t* const buf0 = reinterpret_cast<uint8_t*>(s.data64);
@@ -3343,6 +3347,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             flush_prefixes();
             flush_spans();
         }
+#ifdef HG_SPEC_TIMELINE
+        if (i == 0 && tid == 0) tl[3] = __builtin_amdgcn_s_memrealtime();
+#endif
         if (!dma_cur) {                  // the tail piece
 #pragma unroll
             for (uint32_t q = 0; q < GPT; ++q)
@@ -3375,6 +3382,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             }
             __syncthreads();
             const uint32_t f = uni(s.guess);
+#ifdef HG_SPEC_TIMELINE
+            if (tid == 0) tl[4] = __builtin_amdgcn_s_memrealtime();
+#endif
             if (f == NO_GUESS) {  // no stride run: large records are hopped, others left
                 hop = true;
                 break;
@@ -3390,6 +3400,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             hop = true;
             break;
         }
+#ifdef HG_SPEC_TIMELINE
+        if (i == 0 && tid == 0) tl[1] = __builtin_amdgcn_s_memrealtime();
+#endif
         if (HG_SPEC_EMIT && spec) {
             if (i == 0) {
                 spec = ps.kind == PK_STRIDE && X0 >= a.entry && (X0 - a.entry) % ps.R == 0;
@@ -3452,6 +3465,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
     }
     if (__syncthreads_or(bad)) ok = false;  // some piece's run broke: not resolved here
+#ifdef HG_SPEC_TIMELINE
+    if (tid == 0) tl[2] = __builtin_amdgcn_s_memrealtime();
+#endif
 
 #if HG_LW_FUSE
     if (HG_LW && !ok && hop && __builtin_amdgcn_readfirstlane(s.hcode) == SB_HOP_SMALL) {
