@@ -3530,7 +3530,11 @@ __device__ void lw_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint3
 
 __global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
                                                               SpecPiece* sp) {
+#ifdef HG_SPEC_SWAP_PAIRS  // diagnostics: workgroup b takes batch b ^ 1 (XCD vs address)
+    spec_body<false>(a, sb, sp, (blockIdx.x ^ 1u) < a.nspec ? blockIdx.x ^ 1u : blockIdx.x);
+#else
     spec_body<false>(a, sb, sp, blockIdx.x);
+#endif
 }
 
 __global__ __launch_bounds__(THREADS, 4) void decode_lw_kernel(DecodeArgs a, SpecBatch* sb,

@@ -57,6 +57,8 @@ def main():
                           "rest_us": q(us[:, 2] - us[:, 1]),
                           "end_us": q(us[:, 2])}), flush=True)
         x = np.arange(nspec) % 8  # the XCD a workgroup lands on (round-robin dispatch)
+        if os.environ.get("SWAP_PAIRS"):  # batch b ran on workgroup b ^ 1
+            x = (np.arange(nspec) ^ 1) % 8
         print(json.dumps({"rep": rep, "by_blockIdx_mod_8": {
             "first_piece_us": [round(float(np.mean((us[:, 1] - us[:, 0])[x == k])), 1) for k in range(8)],
             "rest_us": [round(float(np.mean((us[:, 2] - us[:, 1])[x == k])), 1) for k in range(8)],
