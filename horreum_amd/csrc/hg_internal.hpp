@@ -57,7 +57,11 @@ extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
                                 hg_merge_result*, void*, void*, hipStream_t, int defer,
-                                const uint64_t* kp, uint32_t kp_tag);
+                                const uint64_t* kp, uint32_t kp_tag,
+                                const unsigned long long* d_err_pre);
+extern "C" int hgk_merge_prebuild(const uint64_t* kp, uint32_t ntables,
+                                  const hg_decode_result* d_results, uint64_t* d_run_off,
+                                  unsigned long long* d_err, void* d_ws, hipStream_t stream);
 extern "C" int hgk_merge_epochs(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
                                 hg_merge_result*, hg_merge_result*, void*, void*, hipStream_t);
@@ -110,6 +114,10 @@ struct hg_ctx {
     hgi::DevBuf x_res, x_aux;
     hgi::DevBuf x_arena, x_spans;  // split compaction: this context's key-range slices
     uint32_t kpre_calls = 0;       // compaction-mode decode tags (hg_decode.hip kpre_tag)
+    // compaction: the decode results' pinned copy and its event (the merge
+    // entries are built while the host waits on it)
+    hgi::PinBuf kres;
+    hipEvent_t kres_ev = nullptr;
 };
 
 namespace hgi {

@@ -1955,6 +1955,38 @@ extern "C" uint64_t hgk_merge_staging_bytes(uint32_t ntables) {
     return (12 * (uint64_t)ntables + 80) * 8;
 }
 
+// Compaction: the merge entries built before the host has the record counts
+// (hg_runtime.hip compact_core).  kent_runoff_kernel turns the decode results
+// into the tables' run offsets on the device (a table whose decode failed
+// counts 0: the call then fails on the host and the entries are unused) and
+// resets the order-check word; decode_entries_multi then fills the entries
+// at the start of the merge workspace (w.e0, laid out independently of n).
+__global__ void kent_runoff_kernel(const hg_decode_result* res, uint32_t ntables, uint64_t* run_off,
+                                   unsigned long long* err) {
+    if (threadIdx.x != 0) return;
+    uint64_t o = 0;
+    for (uint32_t t = 0; t < ntables; ++t) {
+        run_off[t] = o;
+        o += res[t].kind == HG_OK ? res[t].n_records : 0;
+    }
+    run_off[ntables] = o;
+    *err = ~0ull;
+}
+
+extern "C" int hgk_merge_prebuild(const uint64_t* kp, uint32_t ntables,
+                                  const hg_decode_result* d_results, uint64_t* d_run_off,
+                                  unsigned long long* d_err, void* d_ws, hipStream_t stream) {
+    using namespace hgm;
+    if (!kp || !ntables) return HG_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(kent_runoff_kernel, dim3(1), dim3(64), 0, stream, d_results, ntables, d_run_off,
+                       d_err);
+    const int rc = HG_LAUNCH_STATUS();
+    if (rc != HG_OK) return rc;
+    return hgk_decode_entries_launch(reinterpret_cast<const void*>(kp[3 * (uint64_t)ntables]), ntables,
+                                     (uint32_t)kp[3 * (uint64_t)ntables + 1], d_run_off,
+                                     merge_ws(d_ws, ntables, 0).e0, d_err, stream);
+}
+
 // defer: on input that is not strictly increasing, leave the result as
 // HG_ERR_UNSORTED (n_out 0, no pairs) for hgk_merge_epochs instead of running
 // the serial reference loop on the device.
@@ -1967,7 +1999,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                                 const uint64_t* counts, hg_pair* d_out, uint64_t cap,
                                 hg_merge_result* d_result, void* d_ws, void* staging,
                                 hipStream_t stream, int defer, const uint64_t* kp,
-                                uint32_t kp_tag) {
+                                uint32_t kp_tag, const unsigned long long* d_err_pre) {
     using namespace hgm;
     if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
     uint64_t n = 0;
@@ -2029,7 +2061,12 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     // kp[3 ntables] = the batched decode's device staging, kp[3 ntables + 1]
     // its pre-pass grid) instead of merge_prep_kernel's per-record chains
     const char* kent_env = getenv("HG_MERGE_KENT");  // "0": merge_prep_kernel (A/B runs)
-    if (kent_grid && !(kent_env && strcmp(kent_env, "0") == 0)) {
+    if (d_err_pre) {
+        // the entries were built into w.e0 by hgk_merge_prebuild while the
+        // host waited for the counts: take over its order-check word
+        if (hipMemcpyAsync(w.err, d_err_pre, 8, hipMemcpyDeviceToDevice, stream) != hipSuccess)
+            return HG_HIP_FAIL;
+    } else if (kent_grid && !(kent_env && strcmp(kent_env, "0") == 0)) {
         const int rk = hgk_decode_entries_launch(
             reinterpret_cast<const void*>(kp[3 * (uint64_t)ntables]), ntables, kent_grid, a.run_off,
             w.e0, w.err, stream);

@@ -157,9 +157,10 @@ int hg_ctx_destroy(hg_ctx* c) {
                       &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
                       &c->bws, &c->bstage_d, &c->x_res, &c->x_aux, &c->x_arena, &c->x_spans})
         if (b->p) hipFree(b->p);
-    for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage, &c->bstage})
+    for (PinBuf* b : {&c->hres, &c->h_stage[0], &c->h_stage[1], &c->mstage, &c->bstage, &c->kres})
         if (b->p) hipHostFree(b->p);
     if (c->mstage_ev) hipEventDestroy(c->mstage_ev);
+    if (c->kres_ev) hipEventDestroy(c->kres_ev);
     if (c->bstage_ev) hipEventDestroy(c->bstage_ev);
     for (int i = 0; i < c->naux; ++i) {
         if (c->aux[i]) hipStreamDestroy(c->aux[i]);
@@ -928,7 +929,8 @@ namespace {
 int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t arena_len,
                 const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
                 hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, int defer,
-                const uint64_t* kp = nullptr, uint32_t kp_tag = 0) {
+                const uint64_t* kp = nullptr, uint32_t kp_tag = 0,
+                const unsigned long long* d_err_pre = nullptr) {
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
@@ -955,7 +957,7 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
         if (ensure_pin(c->mstage, hgk_merge_staging_bytes(ntables) + 4096) != HG_OK)
             return HG_HIP_FAIL;
         r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
-                             d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag);
+                             d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag, d_err_pre);
         if (r != HG_OK) return r;
     }
     if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
@@ -1031,7 +1033,11 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     std::vector<uint64_t> caps(ntables), counts(ntables, 0);
     std::vector<hg_decode_result> hr(ntables);
     int r = ensure(c, c->mspans, (span_cap ? span_cap : 1) * sizeof(hg_span));
-    if (r == HG_OK) r = ensure(c, c->d_aux, ntables * sizeof(hg_decode_result) + 64);
+    // d_aux: the decode results, then (hgk_merge_prebuild) the run offsets and
+    // an order-check word -- sized once here, so it never moves under them
+    const size_t rbytes = ntables * sizeof(hg_decode_result);
+    const size_t roff_at = (rbytes + 64 + 255) & ~(size_t)255;
+    if (r == HG_OK) r = ensure(c, c->d_aux, roff_at + (ntables + 2) * sizeof(uint64_t) + 64);
     if (r != HG_OK) return r;
     hg_span* spans = static_cast<hg_span*>(c->mspans.p);
     for (uint32_t t = 0; t < ntables; ++t) {
@@ -1047,6 +1053,7 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     //    and piece tags) -- the entry builder then reads spans, not key lines
     std::vector<uint64_t> kp;
     uint32_t kp_tag = 0;
+    const unsigned long long* prebuilt_err = nullptr;  // the entries are built (hgk_merge_prebuild)
     const char* kmode = getenv("HG_COMPACT_KPRE");
     const bool use_kp = !(kmode && strcmp(kmode, "0") == 0) && !getenv("HG_DECODE_BATCH");
     if (ntables) {
@@ -1075,12 +1082,33 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
         } else {
             r = hg_decode_batch_dev_async(c, ntables, dt.data(), lens, ds.data(), caps.data(), dr);
         }
-        if (r == HG_OK &&
-            (hipMemcpyAsync(hr.data(), dr, ntables * sizeof(hg_decode_result),
-                            hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
-             hipStreamSynchronize(c->stream) != hipSuccess))
-            r = HG_HIP_FAIL;
         if (r != HG_OK) return r;
+        // The counts come back through a pinned copy and an event; meanwhile
+        // (compaction mode, a merge workspace for every possible record of
+        // at most 16 GiB) the merge entries are built on the device from the
+        // device-side counts, so the host round trip overlaps the entry
+        // builder instead of sitting between the kernels (HG_COMPACT_PREBUILD=0:
+        // after it, as before).
+        if (ensure_pin(c->kres, rbytes + 64) != HG_OK ||
+            (!c->kres_ev && hipEventCreateWithFlags(&c->kres_ev, hipEventDisableTiming) != hipSuccess) ||
+            hipMemcpyAsync(c->kres.p, dr, rbytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipEventRecord(c->kres_ev, c->stream) != hipSuccess)
+            return HG_HIP_FAIL;
+        const char* pb = getenv("HG_COMPACT_PREBUILD");
+        const char* ke = getenv("HG_MERGE_KENT");  // "0": the merge builds its entries itself
+        const uint64_t ws_ub = hgk_merge_workspace_bytes(ntables, span_cap) + 4096;
+        if (!kp.empty() && !(pb && strcmp(pb, "0") == 0) && !(ke && strcmp(ke, "0") == 0) &&
+            span_cap < (1ull << 31) && ws_ub <= (16ull << 30)) {
+            if ((r = ensure(c, c->mws, ws_ub)) != HG_OK) return r;
+            uint64_t* d_roff = reinterpret_cast<uint64_t*>(static_cast<char*>(c->d_aux.p) + roff_at);
+            unsigned long long* d_perr = reinterpret_cast<unsigned long long*>(d_roff + ntables + 1);
+            if ((r = hgk_merge_prebuild(kp.data(), ntables, dr, d_roff, d_perr, c->mws.p, c->stream)) !=
+                HG_OK)
+                return r;
+            prebuilt_err = d_perr;
+        }
+        if (hipEventSynchronize(c->kres_ev) != hipSuccess) return HG_HIP_FAIL;
+        memcpy(hr.data(), c->kres.p, rbytes);
         for (uint32_t t = 0; t < ntables; ++t) {
             if (hr[t].kind != HG_OK) {  // the reference's read_all unwrap (storage.rs:64-66)
                 *res = hg_merge_result{0, hr[t].kind, t, hr[t].err_offset};
@@ -1105,7 +1133,7 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     // with no output (the encode then writes nothing) and the epochs below run
     // the reference loop; otherwise merge and encode run back to back
     r = merge_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm, dres_m,
-                    1, kp.empty() ? nullptr : kp.data(), kp_tag);
+                    1, kp.empty() ? nullptr : kp.data(), kp_tag, prebuilt_err);
     if (r != HG_OK) return r;
     auto encode = [&]() -> int {
         if (nm == 0)
