@@ -680,3 +680,33 @@ def test_kway_merge_vs_rounds(engine, monkeypatch, shape):
     monkeypatch.delenv("HG_MERGE_KWAY")
     res2, got2, _, _ = device_merge(engine, datas)
     assert res2.status == 0 and np.array_equal(got2, got)
+
+
+@pytest.mark.parametrize("unsorted", [False, True])
+def test_compact_entries_prebuilt_or_not(engine, monkeypatch, unsorted):
+    """The merge entries built while the host waits for the record counts
+    (default) or after it (HG_COMPACT_PREBUILD=0): the same compacted bytes
+    as the oracle's, through the parallel merge and through the reference
+    loop (a table not strictly increasing), and a decode error still
+    reported for its table."""
+    import torch
+    keys = _keyed_tables([30_000, 20_000, 1, 25_000], 83)
+    datas = [_encode_keyed(k, t, dup_at=(100 if unsorted and t == 0 else None)) for t, k in enumerate(keys)]
+    want, _, wn = oracle.compacted_table(datas)
+    offs, total = [], 0
+    for d in datas:
+        offs.append(total)
+        total += (d.size + 7) & ~7
+    host = np.zeros(total, np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + d.size] = d
+    arena = torch.from_numpy(host).to(engine.device)
+    out = engine.empty(total)
+    lens = [d.size for d in datas]
+    for mode in ("1", "0"):
+        monkeypatch.setenv("HG_COMPACT_PREBUILD", mode)
+        c = engine.compact_dev(arena, offs, lens, out)
+        assert c.status == 0 and c.kind == 0 and c.n == wn, mode
+        assert np.array_equal(c.data.cpu().numpy(), want), mode
+        bad = engine.compact_dev(arena, offs, lens[:1] + [lens[1] - 5] + lens[2:], out)
+        assert bad.kind in (1, 2) and bad.table == 1, mode
