@@ -80,6 +80,8 @@ _u64 = ctypes.c_uint64
 _u32 = ctypes.c_uint32
 _PROTOS = {
     "hg_abi_version": (ctypes.c_int, []),
+    "hg_set_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64]),
+    "hg_get_knob": (ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "hg_status_string": (ctypes.c_char_p, [ctypes.c_int]),
     "hg_last_hip_error": (ctypes.c_char_p, []),
     "hg_ctx_create": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
@@ -171,6 +173,52 @@ def load_library(path=LIB_PATH):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+# Knobs (hg_set_knob): the library reads no environment variables.  Values
+# are integers; the words the A/B scripts used to put in the environment
+# are mapped here.
+KNOB_WORDS = {"HG_DECODE_BATCH": {"streams": 1}, "HG_MERGE_SERIAL": {"exact": 2},
+              "HG_COMPACT_ENCODE": {"pairs": 1}}
+
+
+def knob_value(name, value):
+    if isinstance(value, str):
+        words = KNOB_WORDS.get(name, {})
+        if value in words:
+            return words[value]
+        if name == "HG_MERGE_SERIAL":  # any other word: the reference loop
+            return 1
+        return int(value)
+    return int(value)
+
+
+def set_knob(name, value):
+    """Set library knob `name` (value < 0 clears it; see hg_set_knob)."""
+    lib = load_library()
+    if not hasattr(lib, "hg_set_knob"):  # an older experimental build reads the environment
+        if int(knob_value(name, value)) < 0:
+            os.environ.pop(name, None)
+        else:
+            os.environ[name] = str(value)
+        return
+    rc = lib.hg_set_knob(name.encode(), knob_value(name, value))
+    if rc != 0:
+        raise HorreumGpuError(rc, f"hg_set_knob({name})")
+
+
+def knobs_from_env(environ=None):
+    """Tools only (A/B scripts): forward HG_* knob variables of the
+    environment to the library.  The product never calls this."""
+    environ = os.environ if environ is None else environ
+    lib = load_library()
+    if not hasattr(lib, "hg_set_knob"):
+        return []
+    done = []
+    for name, value in environ.items():
+        if name.startswith("HG_") and lib.hg_set_knob(name.encode(), knob_value(name, value)) == 0:
+            done.append(name)
+    return done
 
 
 def status_string(status):

@@ -41,6 +41,7 @@
 #include <stdlib.h>
 
 #include "hg_device.hpp"
+#include "hg_knobs.hpp"
 
 namespace hgk {
 
@@ -155,15 +156,19 @@ struct SpecBatch {                // one per pre-pass batch
     uint64_t pad;
 };
 
-// HG_SPEC_EMIT: the pre-pass writes the spans of stride batches at their
-// speculated positions (spec_body; decode_body then has nothing to write
-// when every batch was such a batch).  Off: measured on cfg 2 the pre-pass
-// went 170 -> 267 us with the span stores among its reads (0.213 -> 0.274 ms
-// per decode, same box, profiles/r4_ab_spec_emit.log), far more than the 25
-// us decode_kernel takes to write them on its own.
-#ifndef HG_SPEC_EMIT
-#define HG_SPEC_EMIT 0
+// HG_TAIL_EMIT: lattice spans written in the pre-pass's tail (tail_emit).
+// A table whose records all have one (klen, vlen) -- the headline's shape --
+// is the lattice entry + i * R; every pre-pass workgroup whose own batch is
+// such a lattice run takes span tickets once its stream is done, so the span
+// stores fill the HBM time the last workgroups' streams leave idle instead of
+// running as a pass of their own in decode_kernel.  decode_kernel checks that
+// every batch was such a batch (DecodeCtl below) and then has nothing to do.
+// (Round 4 wrote these spans while the pieces streamed, HG_SPEC_EMIT: the
+// pre-pass went 170 -> 267 us -- stores among a stream's reads pace it.)
+#ifndef HG_TAIL_EMIT
+#define HG_TAIL_EMIT 1
 #endif
+constexpr uint32_t TAIL_C = 4096;  // spans per tail ticket (64 KiB of stores)
 // Control words of a decode call (zeroed with the statuses before launch).
 struct DecodeCtl {
     uint32_t ticket;              // decode_kernel batch tickets
@@ -171,13 +176,13 @@ struct DecodeCtl {
     uint32_t progress;            // general batches published (INCL / ERR): the look-back's
                                   // waits restart their budget whenever it moves
     uint32_t repairs;             // pre-pass batches spliced onto their predecessor's exit
-    // speculative spans (HG_SPEC_EMIT): stride batches that wrote their spans
-    // at (x0 - entry) / R, their records, and the largest R and ~R among them
-    // (spec_done: pre-pass batches finished; spec_all: all of them such
-    // batches, the result written)
-    uint32_t spec_cnt, spec_done;
-    unsigned long long spec_total, spec_rmax, spec_rnmax;
-    uint32_t spec_all, spec_pad;
+    // tail emission (HG_TAIL_EMIT): pre-pass batches that are lattice runs,
+    // the largest (klen << 32 | vlen) and its complement's among them (one
+    // shape <=> kv_max == ~kv_nmax), a batch that is not one (no more
+    // tickets), the span tickets taken
+    uint32_t lat_cnt, lat_dead;
+    unsigned long long kv_max, kv_nmax, lat_n;
+    uint32_t tail_ticket, tail_pad;
 };
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
@@ -1205,6 +1210,74 @@ __device__ __forceinline__ void link_arrive(const DecodeArgs& a, uint32_t j, uin
     if ((old >> 56) == 1 && ((old + add) & LINK_MASK) != 0) mark_bad(a.ctl, a.nspec, j);
 }
 
+// Records of the lattice entry + i * R whose starts lie in [entry, stop), or
+// 0 when they would not fit the table or the span buffer (no tail emission).
+__device__ __forceinline__ uint64_t lat_records(const DecodeArgs& a, uint64_t R) {
+    const uint64_t n = (a.stop - a.entry + R - 1) / R;
+    return (n <= a.cap && a.entry + n * R <= a.len) ? n : 0ull;
+}
+
+// Thread 0, with spec_publish: whether batch b is a lattice run (tail
+// emission; kv = its records' klen << 32 | vlen).  Atomics only -- no fence
+// (an agent-scope release writes back the XCD's L2 and stalls every stream
+// on it); decode_kernel reads the words after the kernel boundary.
+__device__ __forceinline__ void lat_publish(const DecodeArgs& a, bool lat, uint64_t kv) {
+    if (!HG_TAIL_EMIT) return;
+    DecodeCtl* c = a.ctl;
+    if (lat) {
+        // (every lattice batch stores the same count when they agree on kv)
+        __hip_atomic_store(&c->lat_n, (unsigned long long)lat_records(a, 16 + (kv >> 32) + (kv & 0xFFFFFFFFu)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        atomicAdd(&c->lat_cnt, 1u);
+        atomicMax(&c->kv_max, (unsigned long long)kv);
+        atomicMax(&c->kv_nmax, ~(unsigned long long)kv);
+    } else {
+        __hip_atomic_store(&c->lat_dead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// Every pre-pass batch was a lattice run of one (klen, vlen) and the runs
+// chain from the entry (no batch bad): the spans are the lattice's, written
+// by tail_emit (lat_n: their count, 0 if they do not fit).  Read by
+// decode_kernel, after the pre-pass's kernel boundary.
+__device__ __forceinline__ bool lat_all(const DecodeArgs& a) {
+    if (!HG_TAIL_EMIT) return false;
+    const DecodeCtl* c = a.ctl;
+    return c->bad_rev == 0 && c->lat_cnt == a.nspec && c->kv_max == ~c->kv_nmax && c->lat_n != 0;
+}
+
+// The tail of a lattice batch's workgroup (all threads): span tickets of
+// TAIL_C lattice records each until they run out or some batch turns out not
+// to be a lattice run (then decode_kernel writes every span itself; the
+// spans written here are overwritten or lie past the result's count).  The
+// last workgroups' streams are still running meanwhile -- these stores take
+// HBM time they leave idle.
+__device__ void tail_emit(const DecodeArgs& a, uint64_t R, uint32_t kl, uint32_t vl, uint32_t* s_tk) {
+    const uint64_t n = lat_records(a, R);
+    if (!n) return;
+    const uint32_t ntk = (uint32_t)((n + TAIL_C - 1) / TAIL_C);
+    DecodeCtl* c = a.ctl;
+    const uint32_t tid = threadIdx.x;
+    for (;;) {
+        if (tid == 0) {
+            uint32_t t = ~0u;
+            if (!__hip_atomic_load(&c->lat_dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
+                !__hip_atomic_load(&c->bad_rev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                t = atomicAdd(&c->tail_ticket, 1u);
+            *s_tk = t;
+        }
+        __syncthreads();
+        const uint32_t t = uni(*s_tk);
+        __syncthreads();
+        if (t >= ntk) return;
+        const uint64_t i1 = min((uint64_t)(t + 1) * TAIL_C, n);
+        uint64_t i = (uint64_t)t * TAIL_C + tid;
+        uint64_t off = a.obase + a.entry + i * R;
+        const uint64_t step = THREADS * R;
+        for (; i < i1; i += THREADS, off += step) write_span(a.spans, i, off, kl, vl);
+    }
+}
+
 // Record base of pre-pass batch e (all batches below e resolved): the group
 // sums before e's group plus the counts before e inside it.  One wave, one
 // round of independent loads (plus one per 64 further groups).
@@ -1481,9 +1554,20 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         if (DIAG && tid == 0) dg[slot] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start); \
     } while (0)
 
-    // every span already written by the pre-pass (HG_SPEC_EMIT; spec_body's
-    // last batch checked it and wrote the result)
-    const bool sd = HG_SPEC_EMIT && a.ctl->spec_all == 1u;
+    // every span already written by the pre-pass's tail (HG_TAIL_EMIT):
+    // workgroup 0 reports the result, nothing else is left
+    if (lat_all(a)) {
+        if (blk == 0 && tid == 0) {
+            hg_decode_result r;
+            r.n_records = a.ctl->lat_n;
+            r.kind = HG_OK;
+            r.reserved = 0;
+            r.err_offset = a.range ? a.obase + a.sbatch[a.nspec - 1].exit : 0;
+            *a.result = r;
+        }
+        return;
+    }
+    constexpr bool sd = false;
     // ---- spans of the pre-pass's resolved prefix (workgroup e = batch e) ----------
     const uint32_t fb = first_bad(a.ctl, a.nspec);
     // Only batches whose whole general batch is resolved: the general engine
@@ -3183,13 +3267,6 @@ __device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb,
 #ifndef HG_SPEC_GLDS
 #define HG_SPEC_GLDS 1
 #endif
-// HG_SPEC_ST_AFTER: a piece's stores issued behind the next piece's DMA with
-// counted waits that skip them (1), or behind the wait for the DMA (0).
-// Measured 0 faster: cfg 2 0.2034 -> 0.2128 ms with 1 (same box, 3 rounds,
-// profiles/r4_ab_fuse.log) -- waiting for the record stores paces the stream.
-#ifndef HG_SPEC_ST_AFTER
-#define HG_SPEC_ST_AFTER 0
-#endif
 // HG_LW_FUSE: the lane walks of SB_HOP_SMALL batches run in the pre-pass
 // workgroup itself (no decode_lw_kernel launch); the second piece buffer is
 // then also lw_batch's chunk buffer of waves 2 and 3.  With the pieces
@@ -3222,34 +3299,6 @@ __device__ __forceinline__ void raw_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-
-// Thread 0 of every pre-pass batch, after its publication: the last batch
-// to finish checks whether every batch wrote its spans at their final
-// positions (speculative spans, spec_body: none bad -- so each links to its
-// predecessor's exit and the first enters at the entry -- all of them such
-// batches, one R, room for all) and then writes the result and sets
-// spec_all, so decode_kernel has nothing left to do.  A batch the lane walks
-// publish later is not such a batch, so its count never completes the set.
-__device__ __forceinline__ void spec_last_check(const DecodeArgs& a, const SpecBatch* sb) {
-    __threadfence();
-    if (atomicAdd(&a.ctl->spec_done, 1u) != a.nspec - 1) return;
-    __threadfence();
-    DecodeCtl* c = a.ctl;
-    const uint32_t bad = __hip_atomic_load(&c->bad_rev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t cnt = __hip_atomic_load(&c->spec_cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned long long n = ld_agent(&c->spec_total);
-    const unsigned long long rmax = ld_agent(&c->spec_rmax), rnmax = ld_agent(&c->spec_rnmax);
-    if (bad != 0 || cnt != a.nspec || rmax != ~rnmax || n > a.cap) return;
-    hg_decode_result r;
-    r.n_records = n;
-    r.kind = HG_OK;
-    r.reserved = 0;
-    r.err_offset = a.range ? a.obase + __hip_atomic_load(&sb[a.nspec - 1].exit, __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT)
-                           : 0;
-    *a.result = r;
-    c->spec_all = 1u;
-}
 
 template <bool KPRE>
 __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
@@ -3300,28 +3349,11 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         pf_n = 0;
         return n + (w64 == 0 ? 1u : 0u);
     };
-    // Speculative spans (HG_SPEC_EMIT): a stride batch entered at X0 with
-    // (X0 - entry) % R == 0 whose pieces all have that R writes its records'
-    // spans at (x - entry) / R -- their final positions if every batch before
-    // it is such a batch with the same R and the chain links up.  decode_kernel
-    // checks exactly that (DecodeCtl: no batch bad, spec_cnt == nspec, one R)
-    // and then has nothing left to write; otherwise it writes every span as
-    // before.  A piece's spans are written during the next piece, behind its
-    // staging wait (stores count in vmcnt, as the prefixes above).
-    bool spec = HG_SPEC_EMIT != 0;
-    uint64_t spec_R = 0, spec_idx = 0;            // the batch's R, the next record's position
-    uint64_t sw_x = 0, sw_idx = 0;                // the pending piece: first record, position
-    uint32_t sw_n = 0, sw_kl = 0, sw_vl = 0;
-    auto flush_spans = [&]() -> uint32_t {
-        if (!HG_SPEC_EMIT || !sw_n) return 0u;
-        for (uint32_t t = tid; t < sw_n; t += THREADS)
-            if (sw_idx + t < a.cap) write_span(a.spans, sw_idx + t, a.obase + sw_x + t * spec_R, sw_kl, sw_vl);
-        // (past the capacity some stores are skipped: count none)
-        const uint32_t n = sw_idx + sw_n <= a.cap && w64 < sw_n ? (sw_n - w64 + THREADS - 1) / THREADS : 0u;
-        sw_n = 0;
-        return n;
-    };
-    uint32_t nst_prev = 0;  // stores this wave issued after the DMA of the piece being staged
+    // Lattice run (tail emission, HG_TAIL_EMIT): every piece a stride run of
+    // one (klen, vlen) and the entry on the lattice a.entry + i * R.
+    bool lat = HG_TAIL_EMIT != 0;
+    uint64_t lat_R = 0;
+    uint32_t lat_kl = 0, lat_vl = 0;
     // Two barriers per piece: (A) the previous piece is done with LDS; stage
     // v and the halo and put the next piece's loads in flight before (B).
     for (uint32_t i = 0; i < np; ++i) {
@@ -3334,19 +3366,8 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         data = cur;
         raw_barrier();  // (A) every wave is done with the other buffer (piece i - 1)
         const bool dma_next = i + 1 < np && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
-        if (HG_SPEC_ST_AFTER) {
-            // the previous piece's prefixes and spans go out behind the next
-            // piece's DMA; the wait for this piece's DMA allows every younger
-            // operation (vector memory operations complete in issue order),
-            // so it never waits for a store
-            const uint32_t nst = flush_prefixes() + flush_spans();
-            lw_wait_vm(nst_prev + (dma_next ? GPT : 0) + nst);  // this wave's part of piece i landed
-            nst_prev = nst;
-        } else {
-            lw_wait_vm(dma_next ? GPT : 0);  // (and every store before the DMA)
-            flush_prefixes();
-            flush_spans();
-        }
+        lw_wait_vm(dma_next ? GPT : 0);  // (and every store before the DMA)
+        flush_prefixes();
 #ifdef HG_SPEC_TIMELINE
         if (i == 0 && tid == 0) tl[3] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -3366,12 +3387,8 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         if (i == 0 && tid < np) s.halo[tid] = h;
         spec_stage(s, v, i);
         flush_prefixes();  // the previous piece's prefixes, ahead of the next loads
-        flush_spans();
         if (i + 1 < np) load_piece(a, p + 1, v);  // in flight while this piece is verified
         __syncthreads();  // (B)
-#endif
-#ifdef HG_SPEC_STREAM_ONLY  // timing experiment: staging only (1: after piece 0; results invalid)
-        if (i > 0 || HG_SPEC_STREAM_ONLY == 2) continue;
 #endif
         if (i == 0 && b == 0) {
             X = X0 = a.entry;  // the first batch's entry is known exactly
@@ -3403,22 +3420,14 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
 #ifdef HG_SPEC_TIMELINE
         if (i == 0 && tid == 0) tl[1] = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (HG_SPEC_EMIT && spec) {
-            if (i == 0) {
-                spec = ps.kind == PK_STRIDE && X0 >= a.entry && (X0 - a.entry) % ps.R == 0;
-                if (spec) {
-                    spec_R = ps.R;
-                    spec_idx = (X0 - a.entry) / ps.R;
-                }
-            }
-            if (spec && ps.kind == PK_STRIDE) {
-                spec = ps.R == spec_R;
-                sw_x = ps.x;
-                sw_idx = spec_idx;
-                sw_n = spec ? ps.count : 0u;
-                sw_kl = ps.kl;
-                sw_vl = ps.vl;
-                spec_idx += ps.count;
+        if (HG_TAIL_EMIT && lat && ps.kind == PK_STRIDE) {
+            if (!lat_R) {
+                lat = X0 >= a.entry && (X0 - a.entry) % ps.R == 0;
+                lat_R = ps.R;
+                lat_kl = ps.kl;
+                lat_vl = ps.vl;
+            } else {
+                lat = ps.kl == lat_kl && ps.vl == lat_vl;
             }
         }
         if (tid == 0) {
@@ -3431,7 +3440,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             o.pad = 0;
             sp[p] = o;
         }
-        nst_prev += w64 == 0 ? 2u : 0u;  // the 32-byte record: two stores at least
         if (KPRE && ps.kind == PK_STRIDE) {  // compaction mode: key prefixes from LDS
             const uint32_t xr = (uint32_t)(X - base), R = (uint32_t)ps.R;
 #pragma unroll
@@ -3459,7 +3467,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     lw_wait_vm(0);  // a break leaves the next piece's DMA in flight
 #endif
     flush_prefixes();
-    flush_spans();
     if (hop) {
         bad = 0;
         ok = hop_batch(s, a, p0, np, sp, X0, X, total);
@@ -3473,16 +3480,14 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     if (HG_LW && !ok && hop && __builtin_amdgcn_readfirstlane(s.hcode) == SB_HOP_SMALL) {
         uint32_t why = 0;
         const bool lok = lw_batch(s, spec_alt, a, p0, np, sp, X0, X, total, why);
-        if (tid == 0) spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
+        if (tid == 0) {
+            spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
+            lat_publish(a, false, 0);
+        }
         return;
     }
 #endif
-    if (HG_SPEC_EMIT && tid == 0 && spec && !hop && ok) {
-        atomicAdd(&a.ctl->spec_cnt, 1u);
-        atomicAdd(&a.ctl->spec_total, (unsigned long long)total);
-        atomicMax(&a.ctl->spec_rmax, (unsigned long long)spec_R);
-        atomicMax(&a.ctl->spec_rnmax, ~(unsigned long long)spec_R);
-    }
+    lat = lat && lat_R && !hop && ok;
     if (tid == 0) {
         const uint32_t code = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
         if (HG_LW && !HG_LW_FUSE && !ok && code == SB_HOP_SMALL) {
@@ -3497,8 +3502,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         } else {
             spec_publish(a, sb, b, X0, X, total, ok, code);
         }
-        if (HG_SPEC_EMIT) spec_last_check(a, sb);
+        lat_publish(a, lat, ((uint64_t)lat_kl << 32) | lat_vl);
     }
+    if (lat) tail_emit(a, lat_R, lat_kl, lat_vl, &s.guess);
 }
 
 // The lane-walk mode as its own launch between the pre-pass and decode_kernel:
@@ -3525,7 +3531,10 @@ __device__ void lw_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint3
     const bool ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total, why);
     // SpecBatch.pad bits 8..15 of a failed batch: 1 the first quarter's guessed
     // entry, 2 a quarter entered exactly, 3 too many re-streams
-    if (threadIdx.x == 0) spec_publish(a, sb, b, X0, X, total, ok, ok ? SB_LW : (SB_LW_DEAD | (why << 8)));
+    if (threadIdx.x == 0) {
+        spec_publish(a, sb, b, X0, X, total, ok, ok ? SB_LW : (SB_LW_DEAD | (why << 8)));
+        lat_publish(a, false, 0);
+    }
 }
 
 __global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
@@ -3839,12 +3848,9 @@ uint32_t resident_workgroups(K kernel, int slot) {
     return (uint32_t)cached[slot][dev];
 }
 
-uint64_t env_or(const char* name, uint64_t dflt) {
-    if (const char* e = getenv(name)) {
-        const long v = atol(e);
-        if (v > 0) return (uint64_t)v;
-    }
-    return dflt;
+uint64_t knob_or(const char* name, uint64_t dflt) {
+    const int64_t v = hgk_knob(name, 0);
+    return v > 0 ? (uint64_t)v : dflt;
 }
 
 // Pieces per general batch: about one round of batches over decode_kernel's
@@ -3862,12 +3868,12 @@ uint32_t pow2_in(uint64_t want, uint32_t lo, uint32_t hi) {
 }
 uint32_t general_pieces(uint64_t npieces, uint32_t resident) {
     using namespace hgk;
-    return pow2_in(env_or("HG_DECODE_BP", (npieces + resident - 1) / resident), BATCH_MIN, BATCH);
+    return pow2_in(knob_or("HG_DECODE_BP", (npieces + resident - 1) / resident), BATCH_MIN, BATCH);
 }
 uint32_t spec_pieces(uint32_t bp, uint64_t npieces, uint32_t cus) {
     using namespace hgk;
     const uint64_t want = (npieces + 4ull * cus - 1) / (4ull * cus);
-    const uint32_t s = pow2_in(env_or("HG_DECODE_SBP", want), SPEC_BP_MIN, SPEC_BP);
+    const uint32_t s = pow2_in(knob_or("HG_DECODE_SBP", want), SPEC_BP_MIN, SPEC_BP);
     return s < bp ? s : bp;
 }
 uint32_t device_cus() {
@@ -3983,18 +3989,11 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
     // 1. pre-pass (stride runs, hop walks): verifies, links neighbours, sums records per group
     // 2. decode_kernel: spans of the resolved prefix, then the general engine
     //    from the first unresolved batch on (exits at once if there is none)
-    // HG_DECODE_SPEC_PAD: extra dynamic LDS per pre-pass workgroup (bytes) to cap
-    // its occupancy (experiments).
-    const size_t spec_pad = (size_t)env_or("HG_DECODE_SPEC_PAD", 0) > 65536 ? 0
-                          : (size_t)env_or("HG_DECODE_SPEC_PAD", 0);
-    hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), spec_pad, stream, a,
+    hipLaunchKernelGGL(decode_spec_kernel, dim3(a.nspec), dim3(THREADS), 0, stream, a,
                        a.sbatch, const_cast<SpecPiece*>(a.spiece));
     if (HG_LW && !HG_LW_FUSE)
         hipLaunchKernelGGL(decode_lw_kernel, dim3(a.nspec), dim3(THREADS), 0, stream, a, a.sbatch,
                            const_cast<SpecPiece*>(a.spiece));
-#ifdef HG_SPEC_STREAM_ONLY  // (the general engine would redo the whole table)
-    return HG_LAUNCH_STATUS();
-#endif
     const uint32_t grid = a.nbatches > a.nspec ? a.nbatches : a.nspec;
     if (d_diag)
         hipLaunchKernelGGL(decode_kernel<true>, dim3(grid), dim3(THREADS), 0, stream, a);

@@ -138,6 +138,7 @@ struct DeviceGuard {
 int set_dev(hg_ctx* c);
 int ensure(hg_ctx* c, DevBuf& b, size_t bytes);
 int ensure_pin(PinBuf& b, size_t bytes);
+bool try_grow(hg_ctx* c, DevBuf& b, size_t bytes);
 int rt_encode_dev(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
                   uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off, uint32_t block_stride,
                   hg_block* d_blocks, uint64_t* out_len, bool gather);

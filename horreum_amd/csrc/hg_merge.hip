@@ -42,6 +42,7 @@
 #include <vector>
 
 #include "hg_device.hpp"
+#include "hg_knobs.hpp"
 
 namespace hgm {
 
@@ -919,12 +920,7 @@ __global__ __launch_bounds__(KW_THREADS, 2) void kw_merge_kernel(MergeArgs a, Kw
     __syncthreads();
     MEnt fx[KW_EPT];
     const uint32_t d0 = tid * KW_EPT;
-#ifdef HG_KW_NOPASS  // timing experiment: no merge passes (results invalid)
-    for (uint32_t e = 0; e < KW_EPT; ++e) fx[e] = s.seg[min(d0 + e, N - 1)];
-    for (uint32_t w = K; w < K; w <<= 1) {
-#else
     for (uint32_t w = 1; w < K; w <<= 1) {
-#endif
         // pass: runs [2 p w, (2 p + 1) w) (A) and [(2 p + 1) w, (2 p + 2) w) (B) merge
         uint32_t pend = 0, ai = 0, bj = 0, A0 = 0, Am = 0, B1 = 0;
 #pragma unroll
@@ -1792,8 +1788,7 @@ int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hg
     fa.ntiles = (uint32_t)ntiles;
     // 3..KW_MAX runs with their offsets on the host and HG_MERGE_KWAY=1: the
     // one-pass k-way merge (section 3b; not the default: slower, see there)
-    const char* kw_env = getenv("HG_MERGE_KWAY");
-    if (h_roff && nr >= 3 && nr <= KW_MAX && kw_env && strcmp(kw_env, "1") == 0) {
+    if (h_roff && nr >= 3 && nr <= KW_MAX && hgk_knob("HG_MERGE_KWAY", 0) == 1) {
         KwArgs k{};
         k.K = (uint32_t)nr;
         uint64_t ns = 0;
@@ -1905,7 +1900,7 @@ int rank_path(const hgm::MergeArgs& a, const MergeWs& w, const uint64_t* start, 
     hipLaunchKernelGGL(merge_scan_kernel, dim3(1), dim3(1024), 0, stream, (const uint32_t*)w.tile_live,
                        (uint32_t)ntiles, w.tile_base, w.ep_res);
     // ranks < n; HG_RANK_NOPACK: plain ranks at any size (tests the > 2^26 form)
-    const uint32_t pack = n < (1ull << 26) && !getenv("HG_RANK_NOPACK") ? 1u : 0u;
+    const uint32_t pack = n < (1ull << 26) && !hgk_knob("HG_RANK_NOPACK", 0) ? 1u : 0u;
     hipLaunchKernelGGL(rank_scatter_kernel, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream, a,
                        (const MEnt*)cur, (const uint64_t*)w.tile_base, w.rank, pack);
     int rc = HG_LAUNCH_STATUS();
@@ -2060,13 +2055,13 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     // workgroup per pre-pass batch (hg_decode.hip, decode_entries_multi;
     // kp[3 ntables] = the batched decode's device staging, kp[3 ntables + 1]
     // its pre-pass grid) instead of merge_prep_kernel's per-record chains
-    const char* kent_env = getenv("HG_MERGE_KENT");  // "0": merge_prep_kernel (A/B runs)
+    const bool kent_on = hgk_knob("HG_MERGE_KENT", 1) != 0;  // 0: merge_prep_kernel (A/B runs)
     if (d_err_pre) {
         // the entries were built into w.e0 by hgk_merge_prebuild while the
         // host waited for the counts: take over its order-check word
         if (hipMemcpyAsync(w.err, d_err_pre, 8, hipMemcpyDeviceToDevice, stream) != hipSuccess)
             return HG_HIP_FAIL;
-    } else if (kent_grid && !(kent_env && strcmp(kent_env, "0") == 0)) {
+    } else if (kent_grid && kent_on) {
         const int rk = hgk_decode_entries_launch(
             reinterpret_cast<const void*>(kp[3 * (uint64_t)ntables]), ntables, kent_grid, a.run_off,
             w.e0, w.err, stream);
@@ -2141,9 +2136,9 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
     // The reference loop itself from heads hd (host, table-local; nullptr:
     // the tables' first records) with n0 records emitted: the rank path (one
     // wave over dense ranks) for up to RANK_MAX_TABLES tables, else the
-    // round-2 loop over entries.  HG_MERGE_SERIAL=exact forces the latter (A/B).
-    const char* serial_env = getenv("HG_MERGE_SERIAL");
-    const bool exact_loop = serial_env && strcmp(serial_env, "exact") == 0;
+    // round-2 loop over entries.  Knob HG_MERGE_SERIAL 2 forces the latter (A/B).
+    const int64_t serial_knob = hgk_knob("HG_MERGE_SERIAL", 0);
+    const bool exact_loop = serial_knob == 2;
     auto serial = [&](const uint64_t* hd0, uint64_t n0) -> int {
         if (ntables <= RANK_MAX_TABLES && !exact_loop)
             return rank_path(a, w, hd0, n0, d_out, cap, d_result, h_result, h, stream);
@@ -2166,12 +2161,11 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
     // order check -- and the one epoch below is the whole merge again.
     // an epoch costs a few launches and host round trips (~0.1-0.2 ms): many
     // disorder points -> the serial loop
-    if (D > EPOCH_MAX_DISORDER || D > n / 128 + 1 || serial_env) return serial(nullptr, 0);
+    if (D > EPOCH_MAX_DISORDER || D > n / 128 + 1 || serial_knob) return serial(nullptr, 0);
     // test hook: epoch number HG_MERGE_TEST_EPOCH_FAIL reports a failure after
     // it ran (as a look-back wait over its budget would), so the hand-over to
     // the serial loop from the epochs' heads is exercised
-    const char* fail_env = getenv("HG_MERGE_TEST_EPOCH_FAIL");
-    const long fail_at = fail_env ? strtol(fail_env, nullptr, 10) : -1;
+    const long fail_at = (long)hgk_knob("HG_MERGE_TEST_EPOCH_FAIL", -1);
     std::vector<uint64_t> dl(D);
     if ((rc = sync_copy(dl.data(), w.dis_list, D * 8, hipMemcpyDeviceToHost, stream)) != HG_OK)
         return rc;

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "hg_internal.hpp"
+#include "hg_knobs.hpp"
 
 using namespace hgi;
 
@@ -149,10 +150,7 @@ uint64_t share_bytes(uint64_t len) { return ((len + 255) & ~255ull) + (len / 16)
 // free now.  A share larger than this is decoded in groups of tables, one
 // group after another; a table larger than the budget is a group of its own.
 uint64_t group_budget() {
-    if (const char* e = getenv("HG_DECODE_GROUP_BYTES")) {
-        const long long v = atoll(e);
-        if (v > 0) return (uint64_t)v;
-    }
+    if (const int64_t v = hgk_knob("HG_DECODE_GROUP_BYTES", 0); v > 0) return (uint64_t)v;
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr == 0) return 4ull << 30;
     return (uint64_t)(fr / 10 * 4);

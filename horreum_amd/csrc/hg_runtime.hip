@@ -16,6 +16,7 @@
 
 
 #include "hg_internal.hpp"
+#include "hg_knobs.hpp"
 
 using namespace hgi;
 
@@ -77,6 +78,25 @@ int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
     return HG_OK;
 }
 
+// Grow b to `bytes` if that allocation succeeds (the old buffer is kept
+// otherwise, and the HIP error cleared): false when it does not.
+bool try_grow(hg_ctx* c, DevBuf& b, size_t bytes) {
+    if (b.bytes >= bytes) return true;
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) {  // work queued on the old buffer
+        (void)hipFree(p);
+        return false;
+    }
+    if (b.p) (void)hipFree(b.p);
+    b.p = p;
+    b.bytes = bytes;
+    return true;
+}
+
 int ensure_pin(PinBuf& b, size_t bytes) {
     if (b.bytes >= bytes) return HG_OK;
     if (b.p) hipHostFree(b.p);
@@ -108,6 +128,66 @@ int hgk_debug_d2h(void* dst, const void* src, uint64_t n) {
 }
 
 int hg_abi_version(void) { return HG_ABI_VERSION; }
+
+// ---- knobs (hg_set_knob): the only run-time switches of the library --------
+namespace {
+struct Knob {
+    const char* name;
+    int64_t value;
+    bool set;
+};
+Knob g_knobs[] = {
+    {"HG_DECODE_BP", 0, false},          // pieces per general decode batch (power of two)
+    {"HG_DECODE_SBP", 0, false},         // pieces per pre-pass batch
+    {"HG_DECODE_BATCH", 0, false},       // 1: batched decode on auxiliary streams
+    {"HG_DECODE_STREAMS", 0, false},     // auxiliary streams of that mode
+    {"HG_DECODE_GROUP_BYTES", 0, false}, // device byte budget of a multi-context decode group
+    {"HG_DECODE_HOST_SERIAL", 0, false}, // 1: host decode without the overlapped chunks
+    {"HG_DEC_CHUNK_MB", 0, false},       // host decode chunk (MiB)
+    {"HG_ENCODE_HOST_SERIAL", 0, false}, // 1: host encode without the overlapped chunks
+    {"HG_ENC_CHUNK_MB", 0, false},       // host encode output chunk (MiB)
+    {"HG_HOST_TIMING", 0, false},        // 1: host encode phase times on stderr
+    {"HG_HOST_COPY_THREADS", 0, false},  // host staging copy threads
+    {"HG_COMPACT_KPRE", 0, false},       // 0: no key prefixes from the compaction decode
+    {"HG_COMPACT_PREBUILD", 0, false},   // 0: merge entries built after the host has the counts
+    {"HG_COMPACT_ENCODE", 0, false},     // 1: compaction encode by the general pair gather
+    {"HG_MERGE_KENT", 0, false},         // 0: merge entries by merge_prep_kernel
+    {"HG_MERGE_KWAY", 0, false},         // 1: the one-pass k-way merge (3..KW_MAX runs)
+    {"HG_MERGE_SERIAL", 0, false},       // 1: the reference loop (rank path), 2: the round-2 loop
+    {"HG_MERGE_TEST_EPOCH_FAIL", 0, false},  // test hook: epoch k reports a failure
+    {"HG_RANK_NOPACK", 0, false},        // 1: rank path with plain ranks at any size
+};
+std::mutex g_knob_mu;
+Knob* find_knob(const char* name) {
+    if (!name) return nullptr;
+    for (Knob& k : g_knobs)
+        if (strcmp(k.name, name) == 0) return &k;
+    return nullptr;
+}
+}  // namespace
+
+int64_t hgk_knob(const char* name, int64_t dflt) {
+    std::lock_guard<std::mutex> g(g_knob_mu);
+    const Knob* k = find_knob(name);
+    return k && k->set ? k->value : dflt;
+}
+
+int hg_set_knob(const char* name, int64_t value) {
+    std::lock_guard<std::mutex> g(g_knob_mu);
+    Knob* k = find_knob(name);
+    if (!k) return HG_ERR_INVALID_ARG;
+    k->set = value >= 0;
+    k->value = value >= 0 ? value : 0;
+    return HG_OK;
+}
+
+int hg_get_knob(const char* name, int64_t* value) {
+    std::lock_guard<std::mutex> g(g_knob_mu);
+    const Knob* k = find_knob(name);
+    if (!k || !value) return HG_ERR_INVALID_ARG;
+    *value = k->set ? k->value : -1;
+    return HG_OK;
+}
 
 const char* hg_status_string(int s) {
     switch (s) {
@@ -329,11 +409,9 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
         if (lens[i] >= kMaxLen) return HG_ERR_TOO_LARGE;
     }
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
-    const char* mode = getenv("HG_DECODE_BATCH");
-    if (!(mode && strcmp(mode, "streams") == 0))
+    if (hgk_knob("HG_DECODE_BATCH", 0) != 1)
         return batch_one_launch(c, ntables, d_tables, lens, d_spans, caps, d_results, 0, nullptr);
-    int fan = 4;
-    if (const char* e = getenv("HG_DECODE_STREAMS")) fan = atoi(e);
+    int fan = (int)hgk_knob("HG_DECODE_STREAMS", 4);
     fan = std::max(1, std::min<int>(fan, hg_ctx::kAux));
     fan = std::min<int>(fan, std::max<uint32_t>(ntables, 1));
     int r = rt_ensure_aux(c, fan);
@@ -398,7 +476,7 @@ static bool rt_host_pinned(const void* p) {
 
 static unsigned copy_threads() {
     unsigned t = kCopyThreads;
-    if (const char* e = getenv("HG_HOST_COPY_THREADS")) t = (unsigned)std::max(1, atoi(e));
+    t = (unsigned)std::max<int64_t>(1, hgk_knob("HG_HOST_COPY_THREADS", t));
     const unsigned hw = std::thread::hardware_concurrency();
     return std::max(1u, std::min({t, hw ? hw : 1u, kMaxCopyThreads}));
 }
@@ -536,8 +614,7 @@ int hg_host_is_pinned(const void* h_ptr) { return h_ptr && rt_host_pinned(h_ptr)
 // chunk reads its exit and count.  HG_DEC_CHUNK_MB sets the chunk (default 128).
 static int decode_host_overlapped(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spans,
                                   uint64_t cap, uint64_t* n_out, hg_err* err) {
-    const char* env = getenv("HG_DEC_CHUNK_MB");
-    const uint64_t C = (uint64_t)(env ? std::max(1, atoi(env)) : 128) << 20;
+    const uint64_t C = (uint64_t)std::max<int64_t>(1, hgk_knob("HG_DEC_CHUNK_MB", 128)) << 20;
     const uint64_t K = (len + C - 1) / C;
     int r = rt_ensure_aux(c, 2);
     if (r == HG_OK) r = ensure(c, c->d_in, len);
@@ -609,9 +686,8 @@ int hg_decode_host(hg_ctx* c, const uint8_t* h_sst, uint64_t len, hg_span* h_spa
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     {
-        const char* env = getenv("HG_DEC_CHUNK_MB");
-        const uint64_t C = (uint64_t)(env ? std::max(1, atoi(env)) : 128) << 20;
-        if (len >= 2 * C && getenv("HG_DECODE_HOST_SERIAL") == nullptr && rt_host_pinned(h_sst) &&
+        const uint64_t C = (uint64_t)std::max<int64_t>(1, hgk_knob("HG_DEC_CHUNK_MB", 128)) << 20;
+        if (len >= 2 * C && !hgk_knob("HG_DECODE_HOST_SERIAL", 0) && rt_host_pinned(h_sst) &&
             (!cap || rt_host_pinned(h_spans)))
             return decode_host_overlapped(c, h_sst, len, h_spans, cap, n_out, err);
     }
@@ -797,9 +873,8 @@ static int encode_host_overlapped(hg_ctx* c, const uint8_t* h_arena, uint64_t ar
     // 64 MiB 183 ms, 128 MiB 142 ms, 192-256 MiB 76 ms, 512 MiB 82 ms, one
     // upload-then-download pass 118 ms (smaller copies behind cross-stream
     // waits fall off a cliff).  HG_ENC_CHUNK_MB overrides.
-    const char* env_chunk = getenv("HG_ENC_CHUNK_MB");
-    const uint64_t kChunkOut = (uint64_t)(env_chunk ? std::max(1, atoi(env_chunk)) : 256) << 20;
-    const bool tm = getenv("HG_HOST_TIMING") != nullptr;
+    const uint64_t kChunkOut = (uint64_t)std::max<int64_t>(1, hgk_knob("HG_ENC_CHUNK_MB", 256)) << 20;
+    const bool tm = hgk_knob("HG_HOST_TIMING", 0) != 0;
     auto now = [] { return std::chrono::duration<double, std::milli>(
                         std::chrono::steady_clock::now().time_since_epoch()).count(); };
     const double t_start = now();
@@ -885,7 +960,7 @@ int hg_encode_host(hg_ctx* c, const uint8_t* h_arena, uint64_t arena_len, const 
     for (uint64_t i = 0; i < n; ++i) total += 16ull + h_pairs[i].klen + h_pairs[i].vlen;
     if (out_len) *out_len = total;
     if (total > cap) return HG_ERR_CAPACITY;
-    if (n && total && arena_len && getenv("HG_ENCODE_HOST_SERIAL") == nullptr &&
+    if (n && total && arena_len && !hgk_knob("HG_ENCODE_HOST_SERIAL", 0) &&
         rt_host_pinned(h_arena) && rt_host_pinned(h_pairs) && rt_host_pinned(h_out))
         return encode_host_overlapped(c, h_arena, arena_len, h_pairs, n, h_out, total, h_rec_off,
                                       block_stride, h_blocks);
@@ -1054,8 +1129,26 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     std::vector<uint64_t> kp;
     uint32_t kp_tag = 0;
     const unsigned long long* prebuilt_err = nullptr;  // the entries are built (hgk_merge_prebuild)
-    const char* kmode = getenv("HG_COMPACT_KPRE");
-    const bool use_kp = !(kmode && strcmp(kmode, "0") == 0) && !getenv("HG_DECODE_BATCH");
+    const bool use_kp = hgk_knob("HG_COMPACT_KPRE", 1) != 0 && hgk_knob("HG_DECODE_BATCH", 0) != 1;
+    // Merge entries built before the host has the record counts (below) need
+    // a merge workspace for every record the tables could hold (lens / 16):
+    // taken only when that bound is modest -- the workspace already has it,
+    // or it fits 1/16 of the free device memory (at most 16 GiB) -- and
+    // sized here, before the decode is queued, so that growing it (a stream
+    // sync) does not sit between the decode and the entry builder.  If the
+    // allocation fails the merge simply builds its entries after the counts.
+    bool prebuild = false;
+    if (use_kp && ntables && hgk_knob("HG_COMPACT_PREBUILD", 1) != 0 &&
+        hgk_knob("HG_MERGE_KENT", 1) != 0 && span_cap < (1ull << 31)) {
+        const uint64_t ws_ub = hgk_merge_workspace_bytes(ntables, span_cap) + 4096;
+        if (c->mws.bytes >= ws_ub) {
+            prebuild = true;
+        } else if (ws_ub <= (16ull << 30)) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && ws_ub <= fr / 16) prebuild = try_grow(c, c->mws, ws_ub);
+            else (void)hipGetLastError();
+        }
+    }
     if (ntables) {
         hg_decode_result* dr = static_cast<hg_decode_result*>(c->d_aux.p);
         if (use_kp) {
@@ -1094,12 +1187,9 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
             hipMemcpyAsync(c->kres.p, dr, rbytes, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
             hipEventRecord(c->kres_ev, c->stream) != hipSuccess)
             return HG_HIP_FAIL;
-        const char* pb = getenv("HG_COMPACT_PREBUILD");
-        const char* ke = getenv("HG_MERGE_KENT");  // "0": the merge builds its entries itself
-        const uint64_t ws_ub = hgk_merge_workspace_bytes(ntables, span_cap) + 4096;
-        if (!kp.empty() && !(pb && strcmp(pb, "0") == 0) && !(ke && strcmp(ke, "0") == 0) &&
-            span_cap < (1ull << 31) && ws_ub <= (16ull << 30)) {
-            if ((r = ensure(c, c->mws, ws_ub)) != HG_OK) return r;
+        // (kp[3 ntables + 1]: the pre-pass grid -- with none the entry
+        // builder would launch nothing and the merge must build them itself)
+        if (prebuild && !kp.empty() && kp[3 * (size_t)ntables + 1] != 0) {
             uint64_t* d_roff = reinterpret_cast<uint64_t*>(static_cast<char*>(c->d_aux.p) + roff_at);
             unsigned long long* d_perr = reinterpret_cast<unsigned long long*>(d_roff + ntables + 1);
             if ((r = hgk_merge_prebuild(kp.data(), ntables, dr, d_roff, d_perr, c->mws.p, c->stream)) !=
@@ -1142,8 +1232,7 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
                        : HG_HIP_FAIL;
         // the merged pairs are whole records of the decoded tables: gathered as
         // records (HG_COMPACT_ENCODE=pairs: the general gather, for A/B runs)
-        const char* em = getenv("HG_COMPACT_ENCODE");
-        if (em && strcmp(em, "pairs") == 0)
+        if (hgk_knob("HG_COMPACT_ENCODE", 0) == 1)
             return hgk_encode_launch_ex(arena, pairs, nm, &dres_m->n_out, true, d_out, cap,
                                         d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, 0,
                                         block_stride, d_blk, dres_e,

@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define HG_ABI_VERSION 5
+#define HG_ABI_VERSION 6
 
 /* Status codes: return values, and the `kind` field of hg_err / results. */
 enum hg_status {
@@ -155,6 +155,14 @@ const char* hg_status_string(int status);
  * "file:line: hipErrorName (code)", or "" if none yet.  Diagnostics only
  * (a HIP failure has no counterpart in the reference, which runs on the CPU). */
 const char* hg_last_hip_error(void);
+
+/* Knobs: batch-geometry overrides, A/B switches and test hooks (ABI 6).
+ * The library reads no environment variables; these are its only run-time
+ * switches, process-wide, all defaulting to the measured best (the list and
+ * their meaning: DESIGN.md section 7).  value < 0 clears a knob.  Returns
+ * HG_ERR_INVALID_ARG for an unknown name.  hg_get_knob: -1 when unset. */
+int hg_set_knob(const char* name, int64_t value);
+int hg_get_knob(const char* name, int64_t* value);
 
 /* Create a context bound to HIP device `device` with its own stream. */
 int hg_ctx_create(int device, hg_ctx** out);

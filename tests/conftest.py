@@ -25,3 +25,18 @@ def engine():
     e = Engine(0)
     yield e
     e.close()
+
+
+@pytest.fixture
+def knobs():
+    """knobs(name, value): set a library knob (hg_set_knob) for this test;
+    every knob set is cleared afterwards."""
+    from horreum_amd import abi
+    touched = []
+
+    def set_knob(name, value):
+        abi.set_knob(name, value)
+        touched.append(name)
+    yield set_knob
+    for name in touched:
+        abi.set_knob(name, -1)

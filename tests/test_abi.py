@@ -20,7 +20,7 @@ def test_library_exports_every_header_symbol():
 
 def test_abi_version_and_status_strings():
     lib = abi.load_library()
-    assert lib.hg_abi_version() == 5
+    assert lib.hg_abi_version() == 6
     for st in abi.Status:
         s = lib.hg_status_string(int(st)).decode()
         assert s and s != "unknown status", st
@@ -64,3 +64,28 @@ def test_engine_refuses_without_gpu():
     from horreum_amd.engine import Engine
     with pytest.raises(abi.HorreumGpuError):
         Engine(0)
+
+
+def test_knobs_set_get_clear():
+    """hg_set_knob: the library's only run-time switches (no environment
+    reads); unknown names are refused, value < 0 clears."""
+    lib = abi.load_library()
+    v = ctypes.c_int64()
+    assert lib.hg_get_knob(b"HG_DECODE_BP", ctypes.byref(v)) == 0 and v.value == -1
+    assert lib.hg_set_knob(b"HG_DECODE_BP", 64) == 0
+    assert lib.hg_get_knob(b"HG_DECODE_BP", ctypes.byref(v)) == 0 and v.value == 64
+    assert lib.hg_set_knob(b"HG_DECODE_BP", -1) == 0
+    assert lib.hg_get_knob(b"HG_DECODE_BP", ctypes.byref(v)) == 0 and v.value == -1
+    assert lib.hg_set_knob(b"HG_NO_SUCH_KNOB", 1) == abi.Status.INVALID_ARG
+    assert lib.hg_set_knob(None, 1) == abi.Status.INVALID_ARG
+    assert abi.knob_value("HG_MERGE_SERIAL", "exact") == 2
+    assert abi.knob_value("HG_DECODE_BATCH", "streams") == 1
+
+
+def test_library_reads_no_environment():
+    """The release library's behaviour cannot be changed by a service's
+    environment: no getenv / secure_getenv import in libhorreum_gpu.so."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--undefined-only", abi.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert "getenv" not in out, [l for l in out.splitlines() if "getenv" in l]

@@ -180,14 +180,14 @@ def test_capacity_cut_inside_pieces(engine, cut):
 
 @pytest.mark.parametrize("chunk_mb", ["16", None])
 @pytest.mark.parametrize("shuffled", [False, True])
-def test_host_encode_page_locked_chunks(engine, shuffled, chunk_mb, monkeypatch):
+def test_host_encode_page_locked_chunks(engine, shuffled, chunk_mb, knobs):
     """hg_encode_host with page-locked arena, pairs and output takes the
     chunked path (upload of chunk i+1 overlapping the download of chunk i);
     > 64 MiB of output so several chunks run, with record offsets and blocks
     (global across chunks); shuffled pairs make every chunk reach far into
     the arena.  HG_ENC_CHUNK_MB=16 forces several chunks."""
     if chunk_mb:
-        monkeypatch.setenv("HG_ENC_CHUNK_MB", chunk_mb)
+        knobs("HG_ENC_CHUNK_MB", chunk_mb)
     rng = np.random.default_rng(21 + shuffled)
     n = 400_000
     kl = rng.integers(0, 48, n)

@@ -150,7 +150,7 @@ def test_compaction_of_duplicate_key_table(engine, golden, tmp_path):
     assert m.tables[0].get_all(engine) == merged
 
 
-def test_cold_open_over_the_byte_budget(engine, tmp_path, monkeypatch):
+def test_cold_open_over_the_byte_budget(engine, tmp_path, knobs):
     """A directory larger than the batched decode's device byte budget opens
     group by group (HG_DECODE_GROUP_BYTES set below one table's share, so
     every table is a group), spans identical to the oracle's; the context's
@@ -166,7 +166,7 @@ def test_cold_open_over_the_byte_budget(engine, tmp_path, monkeypatch):
         data = oracle.encode(arena, rec)[0]
         (tmp_path / f"table_{i}").write_bytes(data.tobytes())
         want.append(oracle.decode(data)[0])
-    monkeypatch.setenv("HG_DECODE_GROUP_BYTES", str(64 << 10))
+    knobs("HG_DECODE_GROUP_BYTES", str(64 << 10))
     m = SSTableManager(tmp_path, 10, 1000, engine)
     assert len(m.tables) == 6
     for t, w in zip(m.tables, want):
@@ -175,6 +175,6 @@ def test_cold_open_over_the_byte_budget(engine, tmp_path, monkeypatch):
         data = np.fromfile(t.file.path, dtype=np.uint8)
         assert got == [data[int(s["off"]) + 16:int(s["off"]) + 16 + int(s["klen"])].tobytes()
                        for s in w]
-    monkeypatch.setenv("HG_DECODE_GROUP_BYTES", str(1 << 40))
+    knobs("HG_DECODE_GROUP_BYTES", str(1 << 40))
     m2 = SSTableManager(tmp_path, 10, 1000, engine)  # one group: same tables
     assert [t.get_size() for t in m2.tables] == [t.get_size() for t in m.tables]

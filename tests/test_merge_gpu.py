@@ -558,26 +558,26 @@ def test_rank_path_mixed_and_long_prefixes(engine):
     _exact_case(engine, tables)
 
 
-def test_rank_path_plain_ranks(engine, monkeypatch):
+def test_rank_path_plain_ranks(engine, knobs):
     """HG_RANK_NOPACK: the loop over plain ranks (winner by ballot and bit
     scan), the form used past 2^26 entries, on shuffled tables of 3, 12, 20
     and 40 tables (every DPP depth)."""
-    monkeypatch.setenv("HG_RANK_NOPACK", "1")
+    knobs("HG_RANK_NOPACK", "1")
     for k, seed in ((3, 71), (12, 72), (20, 73), (40, 74)):
         _rank_case(engine, _shuffled_keyed([1500] * k, seed, dup_frac=0.2))
 
 
-def test_rank_path_equals_exact_loop(engine, monkeypatch):
+def test_rank_path_equals_exact_loop(engine, knobs):
     """HG_MERGE_SERIAL=exact runs the round-2 loop over 24-byte entries:
     both loops give the oracle's output on the same input."""
     datas = _shuffled_keyed([3_000, 2_000, 2_500], 66, dup_frac=0.2)
     _rank_case(engine, datas)
-    monkeypatch.setenv("HG_MERGE_SERIAL", "exact")
+    knobs("HG_MERGE_SERIAL", "exact")
     _rank_case(engine, datas)
 
 
 @pytest.mark.parametrize("fail_at", [0, 1, 3])
-def test_epoch_failure_hands_over_to_the_loop(engine, monkeypatch, fail_at):
+def test_epoch_failure_hands_over_to_the_loop(engine, knobs, fail_at):
     """an epoch that fails (a look-back wait over its budget on a
     shared card, forced here by HG_MERGE_TEST_EPOCH_FAIL) no longer fails the
     merge: the serial loop resumes from the epochs' heads and record count."""
@@ -586,7 +586,7 @@ def test_epoch_failure_hands_over_to_the_loop(engine, monkeypatch, fail_at):
     rng = np.random.default_rng(53)
     datas = [_encode_keyed(k, t, swap_at=int(rng.integers(1, k.size - 2)))
              for t, k in enumerate(keys)]
-    monkeypatch.setenv("HG_MERGE_TEST_EPOCH_FAIL", str(fail_at))
+    knobs("HG_MERGE_TEST_EPOCH_FAIL", str(fail_at))
     _rank_case(engine, datas, table=1)
 
 
@@ -614,7 +614,7 @@ def test_rank_path_8x250k_shuffled_timed(engine):
 
 
 @pytest.mark.parametrize("kent", ["1", "0"])
-def test_compaction_key_length_change_on_the_stride_lattice(engine, monkeypatch, kent):
+def test_compaction_key_length_change_on_the_stride_lattice(engine, knobs, kent):
     """a stride piece of 16 B keys / 100 B values holding one
     record of a 10 B key and a 106 B value -- the same 132-byte size, so it
     sits exactly on the piece's stride lattice but its header differs.  The
@@ -622,7 +622,7 @@ def test_compaction_key_length_change_on_the_stride_lattice(engine, monkeypatch,
     a prefix taken for this record would carry 6 value bytes.  Both entry
     builders (HG_MERGE_KENT=1: per pre-pass batch; 0: merge_prep_kernel) must
     give the oracle's compaction byte for byte."""
-    monkeypatch.setenv("HG_MERGE_KENT", kent)
+    knobs("HG_MERGE_KENT", kent)
     rng = np.random.default_rng(81)
     tables = []
     for t in range(3):
@@ -646,7 +646,7 @@ def test_compaction_key_length_change_on_the_stride_lattice(engine, monkeypatch,
 
 @pytest.mark.parametrize("shape", ["identical", "disjoint", "interleaved", "giant_tiny",
                                    "long_prefix", "three"])
-def test_kway_merge_vs_rounds(engine, monkeypatch, shape):
+def test_kway_merge_vs_rounds(engine, knobs, shape):
     """The one-pass k-way merge (3..8 runs, HG_MERGE_KWAY=1; hg_merge.hip
     section 3b) against the oracle and the default 2-way rounds on shapes that
     stress its sampled tiles: every key in every table (dead entries across
@@ -672,18 +672,18 @@ def test_kway_merge_vs_rounds(engine, monkeypatch, shape):
         else:
             keys = _keyed_tables([70_000, 90_000, 50_000], 80)
         datas = [_encode_keyed(kk, t) if len(kk) else np.zeros(0, np.uint8) for t, kk in enumerate(keys)]
-    monkeypatch.setenv("HG_MERGE_KWAY", "1")
+    knobs("HG_MERGE_KWAY", "1")
     res, got, _, offs = device_merge(engine, datas)
     want, rc = oracle_merge_pairs(datas, offs)
     assert rc == 0 and res.status == 0 and res.n == want.size
     assert np.array_equal(got, want)
-    monkeypatch.delenv("HG_MERGE_KWAY")
+    knobs("HG_MERGE_KWAY", -1)
     res2, got2, _, _ = device_merge(engine, datas)
     assert res2.status == 0 and np.array_equal(got2, got)
 
 
 @pytest.mark.parametrize("unsorted", [False, True])
-def test_compact_entries_prebuilt_or_not(engine, monkeypatch, unsorted):
+def test_compact_entries_prebuilt_or_not(engine, knobs, unsorted):
     """The merge entries built while the host waits for the record counts
     (default) or after it (HG_COMPACT_PREBUILD=0): the same compacted bytes
     as the oracle's, through the parallel merge and through the reference
@@ -704,7 +704,7 @@ def test_compact_entries_prebuilt_or_not(engine, monkeypatch, unsorted):
     out = engine.empty(total)
     lens = [d.size for d in datas]
     for mode in ("1", "0"):
-        monkeypatch.setenv("HG_COMPACT_PREBUILD", mode)
+        knobs("HG_COMPACT_PREBUILD", mode)
         c = engine.compact_dev(arena, offs, lens, out)
         assert c.status == 0 and c.kind == 0 and c.n == wn, mode
         assert np.array_equal(c.data.cpu().numpy(), want), mode

@@ -19,6 +19,8 @@ from horreum_amd import synth  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
 from horreum_amd.index import Index  # noqa: E402
 from horreum_amd.table import PersistedFile  # noqa: E402
+from horreum_amd import abi as _abi  # noqa: E402
+_abi.knobs_from_env()  # the A/B scripts' HG_* knobs (the library reads no environment)
 
 
 def main():

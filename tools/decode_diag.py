@@ -20,6 +20,8 @@ import torch  # noqa: E402
 
 from horreum_amd import abi, synth  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
+from horreum_amd import abi as _abi  # noqa: E402
+_abi.knobs_from_env()  # the A/B scripts' HG_* knobs (the library reads no environment)
 
 NAMES = ["t_spec", "t_agg", "t_lb", "t_end", "n_stride", "n_general", "n_serial", "guess",
          "spins", "count", "flags", "redo", "c_prep", "c_relax", "rounds", "n_short",

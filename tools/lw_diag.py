@@ -21,6 +21,8 @@ import torch  # noqa: E402
 from decode_variants import workloads  # noqa: E402
 from horreum_amd import abi  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
+from horreum_amd import abi as _abi  # noqa: E402
+_abi.knobs_from_env()  # the A/B scripts' HG_* knobs (the library reads no environment)
 
 PIECE, BATCH_MIN, SPEC_BP_MIN, DIAG_WORDS, LW_PROF = 16384, 16, 4, 24, 8
 NAMES = ["fetch_masks", "guess_walk", "chain", "relax", "store", "stitch", "leadin", "nrounds"]

@@ -17,6 +17,8 @@ import torch  # noqa: E402
 from decode_variants import workloads as _workloads  # noqa: E402
 from horreum_amd import synth  # noqa: E402
 from horreum_amd.engine import Engine  # noqa: E402
+from horreum_amd import abi as _abi  # noqa: E402
+_abi.knobs_from_env()  # the A/B scripts' HG_* knobs (the library reads no environment)
 
 
 def workloads(dev):
