@@ -85,6 +85,25 @@ def max_over_ranks(value, world, device=None):
     return float(t.item())
 
 
+_SIDE = None  # a gloo group over all ranks: CPU-side waits (no kernel on the GPUs)
+
+
+def init_side_group():
+    """Every rank calls this once after init_process_group."""
+    global _SIDE
+    import torch.distributed as dist
+    _SIDE = dist.new_group(backend="gloo")
+
+
+def side_barrier(world):
+    """Barrier on the gloo side group: a rank waiting here runs nothing on
+    its GPU -- an RCCL barrier would keep an allreduce kernel spinning on the
+    GPUs rank 0 drives in the cross-GPU leg."""
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier(group=_SIDE)
+
+
 def barrier(world, device=None):
     if world > 1:
         import torch.distributed as dist
@@ -296,6 +315,7 @@ def main(argv=None):
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        init_side_group()
     device = torch.device("cuda", local)
     torch.cuda.set_device(device)
 
@@ -362,7 +382,10 @@ def main(argv=None):
         devices = (list(range(world)) if world > 1 and ndev >= world and
                    os.environ.get("HG_BENCH_SHARE_GPU") != "1" else
                    [local] * ctx_env if ctx_env > 1 else None)
-        barrier(world, device)
+        # the other ranks wait on the gloo side group: nothing of theirs runs
+        # on the GPUs rank 0 drives meanwhile
+        torch.cuda.synchronize(device)
+        side_barrier(world)
         if devices is None:
             extra["multi_gpu_split"] = {"skipped": "one GPU and HG_BENCH_MULTI_CTX unset"}
         elif rank == 0:
@@ -370,7 +393,7 @@ def main(argv=None):
                 extra["multi_gpu_split"] = multi_split_leg(torch, eng, devices)
             except Exception as e:  # noqa: BLE001 -- a failed leg must not lose the bench line
                 extra["multi_gpu_split"] = {"error": repr(e)}
-        barrier(world, device)
+        side_barrier(world)
 
     cpu = (cpu_baseline(sst, n, args.cpu_sample_mb, args.cpu_seconds)
            if (rank == 0 and world == 1) else None)
@@ -820,6 +843,7 @@ def multi_split_leg(torch, eng, devices, ntab=8, per_table=1_000_000, decode_tab
     m = MultiEngine(devices)
     try:
         t_multi, (rc, ol, orc, res) = med3(lambda: m.compact_dev(tabs, owner, outs))
+        phases = m.last_phases()  # of the last of the timed calls
         got_len = sum(int(x) for x in ol)
         ok = rc == 0 and got_len == ref_len
         pos = 0
@@ -856,6 +880,8 @@ def multi_split_leg(torch, eng, devices, ntab=8, per_table=1_000_000, decode_tab
                         "GiB_s": round(total / t_multi / GIB, 3),
                         "single_context_ms": round(t_single * 1e3, 3),
                         "slice_bytes": slices, "parity_bytes_ok": bool(ok),
+                        "per_context_ms": phases,
+                        "waiting_ranks": "gloo side group (CPU): no RCCL kernel on the GPUs",
                         "parity": "slices concatenated == one context's hg_compact_dev"},
             "decode_host": {"api": "hg_multi_decode_host", "tables": decode_tables,
                             "bytes": hbytes, "ms": round(t_dec * 1e3, 3),

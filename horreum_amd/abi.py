@@ -216,16 +216,23 @@ def knobs_from_env(environ=None):
         return []
     done = []
     for name, value in environ.items():
-        if name.startswith("HG_") and lib.hg_set_knob(name.encode(), knob_value(name, value)) == 0:
+        if not name.startswith("HG_"):
+            continue
+        try:
+            v = knob_value(name, value)
+        except ValueError:  # not a knob (HG_LIBRARY, HG_BENCH_*, ...)
+            continue
+        if lib.hg_set_knob(name.encode(), v) == 0:
             done.append(name)
     return done
 
 
 def status_string(status):
-    try:
-        return load_library().hg_status_string(int(status)).decode()
-    except HorreumGpuError:
-        return Status(status).name if status in Status._value2member_map_ else "unknown"
+    # (the loaded library's text; never loads it here: a HorreumGpuError
+    # raised by load_library itself formats its status through this)
+    if _lib is not None:
+        return _lib.hg_status_string(int(status)).decode()
+    return Status(status).name if status in Status._value2member_map_ else "unknown"
 
 
 def last_hip_error():

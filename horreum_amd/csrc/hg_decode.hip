@@ -156,19 +156,15 @@ struct SpecBatch {                // one per pre-pass batch
     uint64_t pad;
 };
 
-// HG_TAIL_EMIT: lattice spans written in the pre-pass's tail (tail_emit).
-// A table whose records all have one (klen, vlen) -- the headline's shape --
-// is the lattice entry + i * R; every pre-pass workgroup whose own batch is
-// such a lattice run takes span tickets once its stream is done, so the span
-// stores fill the HBM time the last workgroups' streams leave idle instead of
-// running as a pass of their own in decode_kernel.  decode_kernel checks that
-// every batch was such a batch (DecodeCtl below) and then has nothing to do.
-// (Round 4 wrote these spans while the pieces streamed, HG_SPEC_EMIT: the
-// pre-pass went 170 -> 267 us -- stores among a stream's reads pace it.)
-#ifndef HG_TAIL_EMIT
-#define HG_TAIL_EMIT 1
-#endif
-constexpr uint32_t TAIL_C = 4096;  // spans per tail ticket (64 KiB of stores)
+// Spans are written by decode_kernel, after the pre-pass, never by the
+// pre-pass itself: span stores that share HBM with the table stream cost
+// more than a store pass of their own.  Measured on cfg 2 (same box, A/B):
+// spans written while the pieces stream (round 4, HG_SPEC_EMIT) 0.213 ->
+// 0.274 ms; each pre-pass workgroup writing its batch's spans once its own
+// stream is done, the others still streaming (round 5, "tail emission", all
+// of a lattice table's spans then known from x0 and R) 0.203 -> 0.255 ms,
+// nontemporal stores 0.254 ms (profiles/r5_ab_tail_emit.log); a first form
+// of the latter that handed out span tickets from one counter 0.59 ms.
 // Control words of a decode call (zeroed with the statuses before launch).
 struct DecodeCtl {
     uint32_t ticket;              // decode_kernel batch tickets
@@ -176,13 +172,6 @@ struct DecodeCtl {
     uint32_t progress;            // general batches published (INCL / ERR): the look-back's
                                   // waits restart their budget whenever it moves
     uint32_t repairs;             // pre-pass batches spliced onto their predecessor's exit
-    // tail emission (HG_TAIL_EMIT): pre-pass batches that are lattice runs,
-    // the largest (klen << 32 | vlen) and its complement's among them (one
-    // shape <=> kv_max == ~kv_nmax), a batch that is not one (no more
-    // tickets), the span tickets taken
-    uint32_t lat_cnt, lat_dead;
-    unsigned long long kv_max, kv_nmax, lat_n;
-    uint32_t tail_ticket, tail_pad;
 };
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
@@ -1210,74 +1199,6 @@ __device__ __forceinline__ void link_arrive(const DecodeArgs& a, uint32_t j, uin
     if ((old >> 56) == 1 && ((old + add) & LINK_MASK) != 0) mark_bad(a.ctl, a.nspec, j);
 }
 
-// Records of the lattice entry + i * R whose starts lie in [entry, stop), or
-// 0 when they would not fit the table or the span buffer (no tail emission).
-__device__ __forceinline__ uint64_t lat_records(const DecodeArgs& a, uint64_t R) {
-    const uint64_t n = (a.stop - a.entry + R - 1) / R;
-    return (n <= a.cap && a.entry + n * R <= a.len) ? n : 0ull;
-}
-
-// Thread 0, with spec_publish: whether batch b is a lattice run (tail
-// emission; kv = its records' klen << 32 | vlen).  Atomics only -- no fence
-// (an agent-scope release writes back the XCD's L2 and stalls every stream
-// on it); decode_kernel reads the words after the kernel boundary.
-__device__ __forceinline__ void lat_publish(const DecodeArgs& a, bool lat, uint64_t kv) {
-    if (!HG_TAIL_EMIT) return;
-    DecodeCtl* c = a.ctl;
-    if (lat) {
-        // (every lattice batch stores the same count when they agree on kv)
-        __hip_atomic_store(&c->lat_n, (unsigned long long)lat_records(a, 16 + (kv >> 32) + (kv & 0xFFFFFFFFu)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        atomicAdd(&c->lat_cnt, 1u);
-        atomicMax(&c->kv_max, (unsigned long long)kv);
-        atomicMax(&c->kv_nmax, ~(unsigned long long)kv);
-    } else {
-        __hip_atomic_store(&c->lat_dead, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Every pre-pass batch was a lattice run of one (klen, vlen) and the runs
-// chain from the entry (no batch bad): the spans are the lattice's, written
-// by tail_emit (lat_n: their count, 0 if they do not fit).  Read by
-// decode_kernel, after the pre-pass's kernel boundary.
-__device__ __forceinline__ bool lat_all(const DecodeArgs& a) {
-    if (!HG_TAIL_EMIT) return false;
-    const DecodeCtl* c = a.ctl;
-    return c->bad_rev == 0 && c->lat_cnt == a.nspec && c->kv_max == ~c->kv_nmax && c->lat_n != 0;
-}
-
-// The tail of a lattice batch's workgroup (all threads): span tickets of
-// TAIL_C lattice records each until they run out or some batch turns out not
-// to be a lattice run (then decode_kernel writes every span itself; the
-// spans written here are overwritten or lie past the result's count).  The
-// last workgroups' streams are still running meanwhile -- these stores take
-// HBM time they leave idle.
-__device__ void tail_emit(const DecodeArgs& a, uint64_t R, uint32_t kl, uint32_t vl, uint32_t* s_tk) {
-    const uint64_t n = lat_records(a, R);
-    if (!n) return;
-    const uint32_t ntk = (uint32_t)((n + TAIL_C - 1) / TAIL_C);
-    DecodeCtl* c = a.ctl;
-    const uint32_t tid = threadIdx.x;
-    for (;;) {
-        if (tid == 0) {
-            uint32_t t = ~0u;
-            if (!__hip_atomic_load(&c->lat_dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) &&
-                !__hip_atomic_load(&c->bad_rev, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                t = atomicAdd(&c->tail_ticket, 1u);
-            *s_tk = t;
-        }
-        __syncthreads();
-        const uint32_t t = uni(*s_tk);
-        __syncthreads();
-        if (t >= ntk) return;
-        const uint64_t i1 = min((uint64_t)(t + 1) * TAIL_C, n);
-        uint64_t i = (uint64_t)t * TAIL_C + tid;
-        uint64_t off = a.obase + a.entry + i * R;
-        const uint64_t step = THREADS * R;
-        for (; i < i1; i += THREADS, off += step) write_span(a.spans, i, off, kl, vl);
-    }
-}
-
 // Record base of pre-pass batch e (all batches below e resolved): the group
 // sums before e's group plus the counts before e inside it.  One wave, one
 // round of independent loads (plus one per 64 further groups).
@@ -1554,26 +1475,12 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         if (DIAG && tid == 0) dg[slot] = (uint32_t)(__builtin_amdgcn_s_memtime() - t_start); \
     } while (0)
 
-    // every span already written by the pre-pass's tail (HG_TAIL_EMIT):
-    // workgroup 0 reports the result, nothing else is left
-    if (lat_all(a)) {
-        if (blk == 0 && tid == 0) {
-            hg_decode_result r;
-            r.n_records = a.ctl->lat_n;
-            r.kind = HG_OK;
-            r.reserved = 0;
-            r.err_offset = a.range ? a.obase + a.sbatch[a.nspec - 1].exit : 0;
-            *a.result = r;
-        }
-        return;
-    }
-    constexpr bool sd = false;
     // ---- spans of the pre-pass's resolved prefix (workgroup e = batch e) ----------
     const uint32_t fb = first_bad(a.ctl, a.nspec);
     // Only batches whose whole general batch is resolved: the general engine
     // redoes a general batch that holds an unresolved pre-pass batch (and
     // reuses the scratch spans of its pieces meanwhile).
-    if (!sd && blk < fb && min((blk / a.q + 1) * a.q, a.nspec) <= fb) {
+    if (blk < fb && min((blk / a.q + 1) * a.q, a.nspec) <= fb) {
         const uint32_t e = blk;
         const uint32_t ep0 = e * a.sbp;
         const uint32_t enp = min(a.sbp, a.npieces - ep0);
@@ -1592,7 +1499,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             *a.result = r;
         }
     }
-    if (sd || fb >= a.nspec || blk >= a.nbatches) return;  // nothing left for the general engine
+    if (fb >= a.nspec || blk >= a.nbatches) return;  // nothing left for the general engine
     if (tid == 0) s.batch = atomicAdd(a.ticket, 1u);
     __syncthreads();
     if (min((s.batch + 1) * a.q, a.nspec) <= fb) {
@@ -3349,11 +3256,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         pf_n = 0;
         return n + (w64 == 0 ? 1u : 0u);
     };
-    // Lattice run (tail emission, HG_TAIL_EMIT): every piece a stride run of
-    // one (klen, vlen) and the entry on the lattice a.entry + i * R.
-    bool lat = HG_TAIL_EMIT != 0;
-    uint64_t lat_R = 0;
-    uint32_t lat_kl = 0, lat_vl = 0;
     // Two barriers per piece: (A) the previous piece is done with LDS; stage
     // v and the halo and put the next piece's loads in flight before (B).
     for (uint32_t i = 0; i < np; ++i) {
@@ -3420,16 +3322,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
 #ifdef HG_SPEC_TIMELINE
         if (i == 0 && tid == 0) tl[1] = __builtin_amdgcn_s_memrealtime();
 #endif
-        if (HG_TAIL_EMIT && lat && ps.kind == PK_STRIDE) {
-            if (!lat_R) {
-                lat = X0 >= a.entry && (X0 - a.entry) % ps.R == 0;
-                lat_R = ps.R;
-                lat_kl = ps.kl;
-                lat_vl = ps.vl;
-            } else {
-                lat = ps.kl == lat_kl && ps.vl == lat_vl;
-            }
-        }
         if (tid == 0) {
             SpecPiece o;
             o.x = ps.x;
@@ -3480,14 +3372,10 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     if (HG_LW && !ok && hop && __builtin_amdgcn_readfirstlane(s.hcode) == SB_HOP_SMALL) {
         uint32_t why = 0;
         const bool lok = lw_batch(s, spec_alt, a, p0, np, sp, X0, X, total, why);
-        if (tid == 0) {
-            spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
-            lat_publish(a, false, 0);
-        }
+        if (tid == 0) spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
         return;
     }
 #endif
-    lat = lat && lat_R && !hop && ok;
     if (tid == 0) {
         const uint32_t code = hop ? s.hcode : (ok ? SB_STRIDE : SB_STRIDE_BROKE);
         if (HG_LW && !HG_LW_FUSE && !ok && code == SB_HOP_SMALL) {
@@ -3502,9 +3390,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         } else {
             spec_publish(a, sb, b, X0, X, total, ok, code);
         }
-        lat_publish(a, lat, ((uint64_t)lat_kl << 32) | lat_vl);
     }
-    if (lat) tail_emit(a, lat_R, lat_kl, lat_vl, &s.guess);
 }
 
 // The lane-walk mode as its own launch between the pre-pass and decode_kernel:
@@ -3531,10 +3417,7 @@ __device__ void lw_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint3
     const bool ok = lw_batch(s, lw_alt, a, p0, np, sp, X0, X, total, why);
     // SpecBatch.pad bits 8..15 of a failed batch: 1 the first quarter's guessed
     // entry, 2 a quarter entered exactly, 3 too many re-streams
-    if (threadIdx.x == 0) {
-        spec_publish(a, sb, b, X0, X, total, ok, ok ? SB_LW : (SB_LW_DEAD | (why << 8)));
-        lat_publish(a, false, 0);
-    }
+    if (threadIdx.x == 0) spec_publish(a, sb, b, X0, X, total, ok, ok ? SB_LW : (SB_LW_DEAD | (why << 8)));
 }
 
 __global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,

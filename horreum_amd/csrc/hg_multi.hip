@@ -22,6 +22,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -49,6 +51,23 @@ int fan_out(uint32_t n, F fn) {
     for (int r : rc)
         if (r != HG_OK) return r;
     return HG_OK;
+}
+
+// Phase times of the last hg_multi_compact_dev (diagnostics for the bench's
+// cross-GPU leg, hgk_multi_last_phases): per context, ms of [0] its decode of
+// the tables it owns (host wall clock, the decode synchronises), [1] the
+// sample / splitter / cut steps (wall clock, all contexts together), and of
+// its key range [2] the slice copies, [3] the merge, [4] the encode (HIP
+// events on the context's stream).
+constexpr uint32_t kPhases = 5, kPhaseCtx = 64;
+struct Phases {
+    std::mutex mu;
+    uint32_t nctx = 0;
+    double ms[kPhaseCtx][kPhases] = {};
+} g_phases;
+double wall_ms() {
+    return std::chrono::duration<double, std::milli>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
 int sync_d2h(hg_ctx* c, void* dst, const void* src, size_t n) {
@@ -410,6 +429,18 @@ int hg_multi_decode_file_host(hg_ctx* const* ctxs, uint32_t nctx, const uint8_t*
 }
 
 // ---- compaction split by key range -----------------------------------------------------
+// Diagnostics only (not in include/horreum_gpu.h; bench.py's cross-GPU leg):
+// the phase times of the last hg_multi_compact_dev that split by key range
+// (see Phases), kPhases doubles per context into out[0 .. 5 * max_ctx);
+// returns the contexts recorded.
+uint32_t hgk_multi_last_phases(double* out, uint32_t max_ctx) {
+    std::lock_guard<std::mutex> g(g_phases.mu);
+    const uint32_t n = g_phases.nctx < max_ctx ? g_phases.nctx : max_ctx;
+    for (uint32_t ci = 0; ci < n; ++ci)
+        for (uint32_t k = 0; k < kPhases; ++k) out[ci * kPhases + k] = g_phases.ms[ci][k];
+    return n;
+}
+
 }  // extern "C"
 
 namespace {
@@ -460,8 +491,9 @@ struct RangeOut {
 // cut or inside a slice); nothing usable was produced.
 int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const uint64_t* lens,
                   Owned& ow, uint8_t* const* dsts, const uint64_t* caps, std::vector<RangeOut>& O,
-                  bool& separable) {
+                  bool& separable, double (*ph)[kPhases] = nullptr) {
     separable = true;
+    const double t_cut0 = wall_ms();
     // 2. samples of every table's keys (on its owner), then nctx - 1 splitters
     std::vector<std::vector<KeyRef>> samples(nctx);
     constexpr uint64_t kSamples = 256;  // per table
@@ -600,10 +632,29 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
             return HG_OK;
         }
     }
+    if (ph)
+        for (uint32_t ci = 0; ci < nctx && ci < kPhaseCtx; ++ci) ph[ci][1] = wall_ms() - t_cut0;
     // 4. range g on context g: its slice of every table copied from the
     //    table's owner (bytes and decoded spans, device to device: each byte
     //    crosses once, nothing is uploaded or decoded again), merged, encoded
     O.assign(nrange, RangeOut{});
+    // (ph: timing events per range -- start, copies done, merged, encoded)
+    struct TEvents {
+        std::vector<hipEvent_t> ev;
+        ~TEvents() {
+            for (hipEvent_t e : ev)
+                if (e) (void)hipEventDestroy(e);
+        }
+    } tev;
+    if (ph) tev.ev.assign(4 * (size_t)nrange, nullptr);
+    auto stamp = [&](uint32_t g, uint32_t k) {
+        if (!ph || g >= kPhaseCtx) return;
+        hipEvent_t& e = tev.ev[4 * (size_t)g + k];
+        if (hipEventCreate(&e) != hipSuccess || hipEventRecord(e, ctxs[g]->stream) != hipSuccess) {
+            (void)hipGetLastError();
+            e = nullptr;
+        }
+    };
     // every owner's decode (and sample / cut work) is ordered before the copies
     // out of it by an event on its stream -- not only by the host having
     // synchronised it (decode_share's D2H), which an asynchronous decode would drop
@@ -627,6 +678,7 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
         for (uint32_t ci = 0; ci < nctx; ++ci)
             if (ci != g && hipStreamWaitEvent(c->stream, evs.ev[ci], 0) != hipSuccess)
                 return (int)HG_HIP_FAIL;
+        stamp(g, 0);
         std::vector<uint64_t> pos(ntables), toff(ntables), cnt(ntables), sps(ntables);
         uint64_t ab = 0, nb = 0;
         for (uint32_t t = 0; t < ntables; ++t) {
@@ -657,12 +709,14 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
             toff[t] = pos[t] - cut_off[t][g];
             sp[t] = spans + sps[t];
         }
+        stamp(g, 1);
         hg_merge_result mr{};
         rr = hg_merge_dev(c, ntables, arena, ab, toff.data(), sp.data(), cnt.data(),
                           static_cast<hg_pair*>(c->mpairs.p), nb, &mr);
         if (rr != HG_OK) return rr;
         O[g].n = mr.n_out;
         O[g].exact = mr.table;
+        stamp(g, 2);
         if (mr.table) return (int)HG_OK;  // not range-separable: decided after the join
         uint8_t* dst = dsts ? dsts[g] : nullptr;
         uint64_t cap = dsts ? caps[g] : ab;
@@ -677,9 +731,21 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
                            static_cast<uint64_t*>(c->d_aux.p), 0, nullptr, &enc, true);
         // the slice's size also on HG_ERR_CAPACITY, so the caller can resize and retry
         O[g].bytes = enc;
+        stamp(g, 3);
         return rr;
     });
     if (r != HG_OK) return r;
+    for (uint32_t g = 0; ph && g < nrange && g < kPhaseCtx; ++g) {
+        hipEvent_t* e = &tev.ev[4 * (size_t)g];
+        for (uint32_t k = 0; k < 3; ++k) {
+            float ms = 0.f;
+            ph[g][2 + k] = (e[k] && e[k + 1] && hipEventSynchronize(e[k + 1]) == hipSuccess &&
+                            hipEventElapsedTime(&ms, e[k], e[k + 1]) == hipSuccess)
+                               ? (double)ms
+                               : -1.0;
+        }
+    }
+    (void)hipGetLastError();
     for (const RangeOut& o : O)
         if (o.exact) separable = false;
     return HG_OK;
@@ -821,8 +887,12 @@ int hg_multi_compact_dev(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
         ow.slot[t] = (uint32_t)ow.sh[owner[t]].ids.size();
         ow.sh[owner[t]].ids.push_back(t);
     }
+    double ph[kPhaseCtx][kPhases] = {};
     int r = fan_out(nctx, [&](uint32_t ci) {
-        return decode_share_dev(ctxs[ci], ow.sh[ci], d_tables, lens);
+        const double t0 = wall_ms();
+        const int rr = decode_share_dev(ctxs[ci], ow.sh[ci], d_tables, lens);
+        if (ci < kPhaseCtx) ph[ci][0] = wall_ms() - t0;
+        return rr;
     });
     if (r != HG_OK) return r;
     for (uint32_t ci = 0; ci < nctx; ++ci)
@@ -830,7 +900,14 @@ int hg_multi_compact_dev(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
             if (res.kind != HG_OK) return single();  // reports the table's error
     std::vector<RangeOut> O;
     bool separable = true;
-    if ((r = split_compact(ctxs, nctx, ntables, lens, ow, d_outs, caps, O, separable)) != HG_OK) {
+    r = split_compact(ctxs, nctx, ntables, lens, ow, d_outs, caps, O, separable, ph);
+    {
+        std::lock_guard<std::mutex> g(g_phases.mu);
+        g_phases.nctx = nctx < kPhaseCtx ? nctx : kPhaseCtx;
+        for (uint32_t ci = 0; ci < g_phases.nctx; ++ci)
+            for (uint32_t k = 0; k < kPhases; ++k) g_phases.ms[ci][k] = ph[ci][k];
+    }
+    if (r != HG_OK) {
         if (r == HG_ERR_CAPACITY)  // a slice did not fit its caller buffer
             for (uint32_t g = 0; g < O.size(); ++g) out_lens[g] = O[g].bytes;
         return r;

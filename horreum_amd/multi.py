@@ -106,6 +106,22 @@ class MultiEngine:
             raise HorreumGpuError(rc, "hg_multi_compact_dev")
         return rc, list(ol), list(orc), res
 
+    PHASES = ("decode_ms", "sample_cut_ms", "copies_ms", "merge_ms", "encode_ms")
+
+    def last_phases(self):
+        """Per context, the phase times of the last compact_dev that split by
+        key range (diagnostics export hgk_multi_last_phases): its decode of
+        the tables it owns, the sample / splitter / cut steps, and for its key
+        range the slice copies, the merge and the encode (ms; -1 unknown)."""
+        fn = getattr(self.lib, "hgk_multi_last_phases", None)
+        if fn is None:
+            return []
+        fn.restype = ctypes.c_uint32
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+        out = (ctypes.c_double * (5 * self.n))()
+        m = fn(ctypes.cast(out, ctypes.c_void_p), self.n)
+        return [dict(zip(self.PHASES, [round(out[5 * g + k], 4) for k in range(5)])) for g in range(m)]
+
     def compact(self, tables, block_stride=0, out=None):
         """hg_multi_compact_host: SSTableManager::compact's byte work split by
         key range over the contexts (`tables` newest first) -> CompactOut."""

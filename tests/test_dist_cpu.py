@@ -28,6 +28,8 @@ def _worker(rank, world, port, q):
         r, w, local = bench.dist_env()
         plan = bench.shard_plan(r, w)
         bench.barrier(w)
+        bench.init_side_group()  # the cross-GPU leg's CPU-side waits
+        bench.side_barrier(w)
         slowest = bench.max_over_ranks(0.010 * (r + 1), w)  # rank 1 is "slower"
         q.put((r, w, local, plan["seed"], plan["n"], slowest))
     finally:
