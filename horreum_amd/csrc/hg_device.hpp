@@ -7,6 +7,17 @@
 #include "../../include/horreum_gpu.h"
 #include "hg_err.hpp"
 
+// Records mode of a merge (compaction; hgk_merge_launch in hg_merge.hip):
+// the last round writes the live records' bytes to out (cap bytes; rec_off,
+// nullable: each record's output offset) and the encode result -- no hg_pair
+// array, no encode pass.
+struct hgk_merge_records {
+    uint8_t* out;
+    uint64_t cap;
+    uint64_t* rec_off;
+    hg_encode_result* enc_result;
+};
+
 namespace hgk {
 
 constexpr uint64_t V40 = (1ull << 40) - 1;  // 40-bit positions/counts in status words

@@ -792,6 +792,22 @@ extern "C" int hgk_encode_blocks_launch(const uint64_t* d_rec_off, uint64_t n,
     return HG_LAUNCH_STATUS();
 }
 
+// Block entries of a compaction written by the merge's records mode: the
+// record count (*d_n, at most n_ub) and the total length (d_res->out_len)
+// are on the device; grid sized for n_ub.
+extern "C" int hgk_encode_blocks_launch_dev(const uint64_t* d_rec_off, uint64_t n_ub,
+                                            const uint64_t* d_n, const hg_encode_result* d_res,
+                                            uint32_t block_stride, hg_block* d_blocks,
+                                            hipStream_t stream) {
+    using namespace hgk;
+    if (n_ub == 0 || block_stride == 0) return HG_OK;
+    const uint64_t nb = (n_ub + block_stride - 1) / block_stride;
+    const uint32_t grid = (uint32_t)((nb + 255) / 256);
+    hipLaunchKernelGGL(blocks_kernel, dim3(grid), dim3(256), 0, stream, d_rec_off, n_ub, block_stride,
+                       d_res, (uint64_t)0, d_blocks, nb, d_n);
+    return HG_LAUNCH_STATUS();
+}
+
 // Encoded size only (hg_encoded_size on device pairs): the tile sums and
 // their scan, no copy -- d_result->out_len = sum(16 + klen + vlen).
 extern "C" int hgk_encode_size_launch(const hg_pair* d_pairs, uint64_t n,

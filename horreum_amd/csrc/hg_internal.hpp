@@ -54,11 +54,16 @@ extern "C" int hgk_decode_entries_launch(const void* d_stage, uint32_t ntab, uin
 extern "C" uint32_t hgk_decode_multi_geometry(const void* h_stage, uint32_t ntab);
 extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
+#include "hg_device.hpp"  // hgk_merge_records
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
                                 hg_merge_result*, void*, void*, hipStream_t, int defer,
                                 const uint64_t* kp, uint32_t kp_tag,
-                                const unsigned long long* d_err_pre);
+                                const unsigned long long* d_err_pre,
+                                const hgk_merge_records* rec, int* rec_emitted);
+extern "C" int hgk_encode_blocks_launch_dev(const uint64_t* d_rec_off, uint64_t n_ub,
+                                            const uint64_t* d_n, const hg_encode_result* d_res,
+                                            uint32_t stride, hg_block* d_blocks, hipStream_t stream);
 extern "C" int hgk_merge_prebuild(const uint64_t* kp, uint32_t ntables,
                                   const hg_decode_result* d_results, uint64_t* d_run_off,
                                   unsigned long long* d_err, void* d_ws, hipStream_t stream);

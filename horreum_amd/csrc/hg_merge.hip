@@ -400,7 +400,10 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
     }
     if (j == 0) {
         split[t] = i;
-        if (zst && t < nb_tiles) zst[t] = 0;
+        if (zst && t < nb_tiles) {  // (both status words of a tile: records mode uses two)
+            zst[t] = 0;
+            zst[nb_tiles + t] = 0;
+        }
     }
 }
 
@@ -410,10 +413,18 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
 // its pairs at their final positions; the last tile writes the result.
 struct FinalArgs {
     unsigned long long* st;  // [ntiles] look-back status (zeroed): flag << 62 | live count
+                             // (records mode: then [ntiles] of output bytes, same flags)
     hg_pair* out;
     uint64_t cap;
     hg_merge_result* result;
     uint32_t ntiles;
+    // records mode (merge_level_kernel<2>, compaction): the live records
+    // themselves, gathered from the arena into rec_out (rec_cap bytes) at
+    // their output offsets -- no hg_pair array, no encode pass
+    uint8_t* rec_out;
+    uint64_t rec_cap;
+    uint64_t* rec_off;             // nullable: each record's output offset (block index)
+    hg_encode_result* enc_result;  // out_len, HG_ERR_CAPACITY past rec_cap
 };
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INCL = 2ull << 62;
 constexpr unsigned long long LB_VAL = (1ull << 62) - 1;
@@ -474,21 +485,145 @@ __device__ uint64_t final_lookback(const FinalArgs& f, uint32_t t, uint64_t agg,
     return acc;
 }
 
+// Records mode: the look-back over (live records, output bytes) of the tiles
+// before tile t -- two status words per tile, st[t] and st[ntiles + t], each
+// written whole with the same flag (AGG, then INCL); a predecessor whose two
+// words do not show the same flag yet (caught between its two stores) reads
+// as not ready.  Wave 0; every lane gets (base_c, base_b).
+__device__ void final_lookback2(const FinalArgs& f, uint32_t t, uint64_t agg_c, uint64_t agg_b,
+                                unsigned long long* err, uint64_t& base_c, uint64_t& base_b) {
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long* stb = f.st + f.ntiles;
+    base_c = base_b = 0;
+    if (t == 0) {
+        if (lane == 0) {
+            hgk::st_agent(&f.st[0], LB_INCL | agg_c);
+            hgk::st_agent(&stb[0], LB_INCL | agg_b);
+        }
+        return;
+    }
+    if (lane == 0) {
+        hgk::st_agent(&f.st[t], LB_AGG | agg_c);
+        hgk::st_agent(&stb[t], LB_AGG | agg_b);
+    }
+    uint64_t acc_c = 0, acc_b = 0;
+    int64_t j0 = (int64_t)t - 1;
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t j = j0 - (int64_t)lane;
+        unsigned long long w = j >= 0 ? hgk::ld_agent(&f.st[j]) : LB_INCL;
+        unsigned long long wb = j >= 0 ? hgk::ld_agent(&stb[j]) : LB_INCL;
+        unsigned long long incl, rel;
+        for (;;) {
+            const uint32_t fl = (w >> 62) == (wb >> 62) ? (uint32_t)(w >> 62) : 0u;
+            incl = __ballot(fl == 2);
+            const int fi = incl ? __ffsll((long long)incl) - 1 : 63;
+            rel = fi >= 63 ? ~0ull : ((1ull << (fi + 1)) - 1ull);
+            if (!(__ballot(fl == 0) & rel)) break;
+            if (++spins > (1u << 22)) {
+                if (lane == 0) {
+                    atomicMin(err, 0ull);
+                    hgk::st_agent(&f.st[t], LB_INCL | agg_c);
+                    hgk::st_agent(&stb[t], LB_INCL | agg_b);
+                }
+                return;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            bool moved = false;
+            if (j >= 0 && fl == 0) {
+                const unsigned long long w2 = hgk::ld_agent(&f.st[j]);
+                const unsigned long long wb2 = hgk::ld_agent(&stb[j]);
+                moved = w2 != w || wb2 != wb;
+                w = w2;
+                wb = wb2;
+            }
+            if (__ballot(moved)) spins = 0;
+        }
+        const bool in = (rel >> lane) & 1ull;
+        acc_c += hgk::wave_sum<uint64_t>(in ? (w & LB_VAL) : 0ull);
+        acc_b += hgk::wave_sum<uint64_t>(in ? (wb & LB_VAL) : 0ull);
+        if (incl) break;
+        j0 -= 64;
+    }
+    if (lane == 0) {
+        hgk::st_agent(&f.st[t], LB_INCL | (acc_c + agg_c));
+        hgk::st_agent(&stb[t], LB_INCL | (acc_b + agg_b));
+    }
+    base_c = acc_c;
+    base_b = acc_b;
+}
+
+// 16 bytes of the arena from p, never outside [0, len) (a window past either
+// end is assembled byte by byte: records at the arena's edges).
+__device__ __forceinline__ uint4 arena16(const uint8_t* arena, uint64_t len, int64_t p) {
+    if (p >= 0 && (uint64_t)p + 16 <= len) return *reinterpret_cast<const uint4*>(arena + p);
+    uint8_t b[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t q = p + i;
+        b[i] = (q >= 0 && (uint64_t)q < len) ? arena[q] : 0;
+    }
+    return make_uint4(b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24),
+                      b[4] | (b[5] << 8) | (b[6] << 16) | ((uint32_t)b[7] << 24),
+                      b[8] | (b[9] << 8) | (b[10] << 16) | ((uint32_t)b[11] << 24),
+                      b[12] | (b[13] << 8) | (b[14] << 16) | ((uint32_t)b[15] << 24));
+}
+// Byte mask of dword i for the bytes of a 16-byte window below n (n in [0, 16]).
+__device__ __forceinline__ uint32_t low_mask(uint32_t n, uint32_t i) {
+    const int32_t k = (int32_t)n - 4 * (int32_t)i;
+    return k >= 4 ? ~0u : (k <= 0 ? 0u : (1u << (8 * k)) - 1u);
+}
+// The low n (< 16) bytes of v to dst by 8 / 4 / 2 / 1-byte stores.
+__device__ __forceinline__ void store_low(uint8_t* dst, uint4 v, uint32_t n) {
+    const uint64_t lo = ((uint64_t)v.y << 32) | v.x, hi = ((uint64_t)v.w << 32) | v.z;
+    uint32_t o = 0;
+    uint64_t cur = lo;
+    if (n & 8) {
+        *reinterpret_cast<uint64_t*>(dst) = lo;
+        o = 8;
+        cur = hi;
+    }
+    if (n & 4) {
+        *reinterpret_cast<uint32_t*>(dst + o) = (uint32_t)cur;
+        cur >>= 32;
+        o += 4;
+    }
+    if (n & 2) {
+        *reinterpret_cast<uint16_t*>(dst + o) = (uint16_t)cur;
+        cur >>= 16;
+        o += 2;
+    }
+    if (n & 1) dst[o] = (uint8_t)cur;
+}
+typedef uint32_t m_u32x4 __attribute__((ext_vector_type(4)));
+// Records mode: 16-byte output pieces per lane per step of the gather (their
+// loads in flight together) and the kernel's waves per SIMD.
+#ifndef HG_REC_GU
+#define HG_REC_GU 1  // cfg 5 leg: 1 595 us, 2 630 us (more spills)
+#endif
+constexpr uint32_t REC_GU = HG_REC_GU;
+#ifndef HG_REC_WAVES
+#define HG_REC_WAVES 5
+#endif
+
 // err: the order check's result; merging unsorted runs is meaningless (and
 // their merge paths are not monotone), so every round skips work once set.
-// FINAL: the last round, emitting pairs (f) instead of entries (out unused).
-template <bool FINAL>
+// MODE 0: a round writing entries; 1 (FINAL): the last round, emitting pairs
+// (f) instead of entries (out unused); 2 (FINAL, records mode): the last
+// round of a compaction, writing the live records' bytes themselves.
+template <int MODE>
 // Occupancy over registers: bounded to 5 (6 for the last round) waves/SIMD
 // the rounds run faster despite a few spilled registers (cfg 5 leg: 96 -> 92
 // and 185 -> 167 us against 4 waves/SIMD unbounded).
-__global__ __launch_bounds__(THREADS, FINAL ? 6 : 5) void merge_level_kernel(MergeArgs a, LevelArgs l,
+__global__ __launch_bounds__(THREADS, MODE == 1 ? 6 : MODE == 2 ? HG_REC_WAVES : 5) void merge_level_kernel(MergeArgs a, LevelArgs l,
                                                               const MEnt* in, MEnt* out,
                                                               const uint64_t* split,
                                                               unsigned long long* err,
                                                               FinalArgs f) {
+    constexpr bool FINAL = MODE != 0;
     __shared__ LevelSmem s;
     __shared__ uint32_t fin_tmp[THREADS / 64];
-    __shared__ uint64_t fin_base;
+    __shared__ uint64_t fin_base, fin_bbase, fin_tmp64[THREADS / 64];
     // FINAL: the tables' run offsets, span arrays and arena offsets in LDS
     // (up to FIN_LDS_TABLES tables), so a live record's span lookup is one
     // HBM load after an LDS search instead of a chain of dependent loads
@@ -512,7 +647,11 @@ __global__ __launch_bounds__(THREADS, FINAL ? 6 : 5) void merge_level_kernel(Mer
     // A FINAL tile that stops early still publishes its status (count 0), so
     // no later tile waits on it; the exact loop then redoes the merge.
     auto fin_abort = [&]() {
-        if (FINAL && tid < 64) final_lookback(f, bx, 0, err);
+        if (MODE == 1 && tid < 64) final_lookback(f, bx, 0, err);
+        if (MODE == 2 && tid < 64) {
+            uint64_t bc, bb;
+            final_lookback2(f, bx, 0, 0, err, bc, bb);
+        }
     };
     // The error word is loaded with the splits (one round trip) and tested
     // before anything is staged: once the order check failed the splits are
@@ -635,31 +774,20 @@ __global__ __launch_bounds__(THREADS, FINAL ? 6 : 5) void merge_level_kernel(Mer
                 for (uint32_t i = tid; i < 3 * nt; i += THREADS) o8[i] = src[i];
             } else {
                 // live entries before this thread's in the tile, the tiles'
-                // before it (look-back), then the pairs at their positions
+                // before it (look-back), then the pairs (MODE 1) or the
+                // records' bytes (MODE 2) at their positions
                 uint32_t ftot;
                 const uint32_t fpre = hgk::block_excl_scan<THREADS / 64>(fcnt, fin_tmp, ftot);
-                if (tid < 64) {
-                    const uint64_t b = final_lookback(f, bx, ftot, err);
-                    if (tid == 0) {
-                        fin_base = b;
-                        if (bx + 1 == f.ntiles) {
-                            hg_merge_result r;
-                            r.n_out = b + ftot;
-                            r.kind = HG_OK;
-                            r.table = 0;
-                            r.index = 0;
-                            *f.result = r;
-                        }
-                    }
-                }
-                hg_pair* lp = reinterpret_cast<hg_pair*>(s.seg);
-                uint32_t r = fpre;
                 // the spans of this thread's outputs, every load issued
                 // before the first is used (branch-free: an output past the
-                // tile or dead looks up entry 0 and is dropped below)
+                // tile or dead looks up entry 0 and is dropped below).  MODE
+                // 1 looks them up after the look-back (their registers are
+                // not live across it: no spills), MODE 2 before (it needs
+                // the record sizes for the byte look-back)
                 uint32_t tk[EPT];
                 hg_span spk[EPT];
                 uint64_t tof[EPT];
+                auto lookups = [&]() {
 #pragma unroll
                 for (uint32_t k = 0; k < EPT; ++k) {
                     const uint64_t g = d + k < e ? (uint64_t)(fx[k].gd & ~DEAD) : 0ull;
@@ -679,24 +807,153 @@ __global__ __launch_bounds__(THREADS, FINAL ? 6 : 5) void merge_level_kernel(Mer
                         spk[k] = a.spans[tk[k]][g - a.run_off[tk[k]]];
                     }
                 }
+                };
+                if (MODE == 1) {
+                    if (tid < 64) {
+                        const uint64_t b = final_lookback(f, bx, ftot, err);
+                        if (tid == 0) {
+                            fin_base = b;
+                            if (bx + 1 == f.ntiles) {
+                                hg_merge_result r;
+                                r.n_out = b + ftot;
+                                r.kind = HG_OK;
+                                r.table = 0;
+                                r.index = 0;
+                                *f.result = r;
+                            }
+                        }
+                    }
+                    lookups();
+                    hg_pair* lp = reinterpret_cast<hg_pair*>(s.seg);
+                    uint32_t r = fpre;
 #pragma unroll
-                for (uint32_t k = 0; k < EPT; ++k) {
-                    if (d + k >= e || (fx[k].gd & DEAD)) continue;
-                    const hg_span sp = spk[k];
-                    hg_pair p;
-                    p.key_off = tof[k] + sp.off + 16;
-                    p.val_off = p.key_off + sp.klen;
-                    p.klen = sp.klen;
-                    p.vlen = sp.vlen;
-                    lp[r++] = p;
+                    for (uint32_t k = 0; k < EPT; ++k) {
+                        if (d + k >= e || (fx[k].gd & DEAD)) continue;
+                        const hg_span sp = spk[k];
+                        hg_pair p;
+                        p.key_off = tof[k] + sp.off + 16;
+                        p.val_off = p.key_off + sp.klen;
+                        p.klen = sp.klen;
+                        p.vlen = sp.vlen;
+                        lp[r++] = p;
+                    }
+                    __syncthreads();  // also publishes fin_base
+                    // the tile's pairs are words [3 base, 3 (base + ftot)) of out
+                    const uint64_t w0 = 3 * fin_base, wcap = 3 * f.cap;
+                    const uint64_t* s8 = reinterpret_cast<const uint64_t*>(s.seg);
+                    uint64_t* o8 = reinterpret_cast<uint64_t*>(f.out);
+                    for (uint32_t i = tid; i < 3 * ftot; i += THREADS)
+                        if (w0 + i < wcap) o8[w0 + i] = s8[i];
+                } else {
+                    // records mode: each live record's source (its header in
+                    // the arena) and output offset in the tile go to LDS --
+                    // src[0, ftot), off[0, ftot], in place of the segments --
+                    // then the tile's output bytes [B, B + btot) are written
+                    // as 16-byte pieces aligned in the OUTPUT (a piece takes
+                    // the bytes of the record it starts in and, across a record
+                    // boundary, the next one's; the pieces at the tile's two
+                    // edges only the tile's own bytes)
+                    lookups();
+                    uint64_t bsz = 0;
+#pragma unroll
+                    for (uint32_t k = 0; k < EPT; ++k)
+                        if (d + k < e && !(fx[k].gd & DEAD)) bsz += 16ull + spk[k].klen + spk[k].vlen;
+                    uint64_t bx64 = bsz;  // block exclusive scan (u64)
+#pragma unroll
+                    for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+                        const uint64_t y = __shfl_up(bx64, dd, 64);
+                        if ((tid & 63u) >= dd) bx64 += y;
+                    }
+                    if ((tid & 63u) == 63u) fin_tmp64[tid >> 6] = bx64;
+                    __syncthreads();
+                    uint64_t bpre = bx64 - bsz, btot = 0;
+#pragma unroll
+                    for (uint32_t w = 0; w < THREADS / 64; ++w) {
+                        bpre += w < (tid >> 6) ? fin_tmp64[w] : 0ull;
+                        btot += fin_tmp64[w];
+                    }
+                    if (tid < 64) {
+                        uint64_t bc, bb;
+                        final_lookback2(f, bx, ftot, btot, err, bc, bb);
+                        if (tid == 0) {
+                            fin_base = bc;
+                            fin_bbase = bb;
+                            if (bx + 1 == f.ntiles) {
+                                hg_merge_result r;
+                                r.n_out = bc + ftot;
+                                r.kind = HG_OK;
+                                r.table = 0;
+                                r.index = 0;
+                                *f.result = r;
+                                hg_encode_result er;
+                                er.out_len = bb + btot;
+                                er.kind = bb + btot <= f.rec_cap ? HG_OK : HG_ERR_CAPACITY;
+                                er.reserved = 0;
+                                *f.enc_result = er;
+                            }
+                        }
+                    }
+                    uint64_t* lsrc = reinterpret_cast<uint64_t*>(s.seg);
+                    uint64_t* loff = lsrc + TILE;
+                    uint32_t r = fpre;
+                    uint64_t o = bpre;
+#pragma unroll
+                    for (uint32_t k = 0; k < EPT; ++k) {
+                        if (d + k >= e || (fx[k].gd & DEAD)) continue;
+                        lsrc[r] = tof[k] + spk[k].off;
+                        loff[r] = o;
+                        o += 16ull + spk[k].klen + spk[k].vlen;
+                        ++r;
+                    }
+                    if (tid == 0) loff[ftot] = btot;
+                    __syncthreads();  // also publishes fin_base / fin_bbase
+                    const uint64_t B = fin_bbase, bc = fin_base;
+                    if (f.rec_off)
+                        for (uint32_t i = tid; i < ftot; i += THREADS) f.rec_off[bc + i] = B + loff[i];
+                    const uint64_t P0 = B >> 4, np = ((B + btot + 15) >> 4) - P0;
+                    const float scale = btot ? (float)ftot / (float)btot : 0.f;
+                    for (uint64_t i0 = 0; btot && i0 < np; i0 += (uint64_t)THREADS * REC_GU) {
+                        uint4 v[REC_GU], w2[REC_GU];
+                        uint32_t n1[REC_GU], need[REC_GU];
+                        uint64_t lo[REC_GU];
+#pragma unroll
+                        for (uint32_t u = 0; u < REC_GU; ++u) {  // every load before any store
+                            const uint64_t i = min(i0 + (uint64_t)u * THREADS + tid, np - 1);
+                            const uint64_t A = (P0 + i) << 4;
+                            lo[u] = (A > B ? A : B) - B;  // tile-relative
+                            need[u] = (uint32_t)(min(A + 16, B + btot) - B - lo[u]);
+                            uint32_t rr = min((uint32_t)((float)lo[u] * scale), ftot - 1);  // interpolate, walk
+                            while (rr > 0 && loff[rr] > lo[u]) --rr;
+                            while (rr + 1 < ftot && loff[rr + 1] <= lo[u]) ++rr;
+                            const uint64_t rem = loff[rr + 1] - lo[u];  // record rr's bytes from lo
+                            n1[u] = rem < 16 ? (uint32_t)rem : 16u;
+                            v[u] = arena16(a.arena, a.arena_len, (int64_t)(lsrc[rr] + (lo[u] - loff[rr])));
+                            w2[u] = n1[u] < need[u]  // the next record supplies bytes [n1, need)
+                                        ? arena16(a.arena, a.arena_len, (int64_t)lsrc[rr + 1] - (int64_t)n1[u])
+                                        : make_uint4(0, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (uint32_t u = 0; u < REC_GU; ++u) {
+                            if (i0 + (uint64_t)u * THREADS + tid >= np) continue;
+                            uint4 x = v[u];
+                            if (n1[u] < need[u]) {
+                                x.x = (x.x & low_mask(n1[u], 0)) | (w2[u].x & ~low_mask(n1[u], 0));
+                                x.y = (x.y & low_mask(n1[u], 1)) | (w2[u].y & ~low_mask(n1[u], 1));
+                                x.z = (x.z & low_mask(n1[u], 2)) | (w2[u].z & ~low_mask(n1[u], 2));
+                                x.w = (x.w & low_mask(n1[u], 3)) | (w2[u].w & ~low_mask(n1[u], 3));
+                            }
+                            const uint64_t O = B + lo[u];  // absolute output offset
+                            if (O >= f.rec_cap) continue;
+                            const uint32_t lim = (uint32_t)min((uint64_t)need[u], f.rec_cap - O);
+                            if (lim == 16) {
+                                m_u32x4 xv = {x.x, x.y, x.z, x.w};
+                                __builtin_nontemporal_store(xv, reinterpret_cast<m_u32x4*>(f.rec_out + O));
+                            } else {
+                                store_low(f.rec_out + O, x, lim);
+                            }
+                        }
+                    }
                 }
-                __syncthreads();  // also publishes fin_base
-                // the tile's pairs are words [3 base, 3 (base + ftot)) of out
-                const uint64_t w0 = 3 * fin_base, wcap = 3 * f.cap;
-                const uint64_t* s8 = reinterpret_cast<const uint64_t*>(s.seg);
-                uint64_t* o8 = reinterpret_cast<uint64_t*>(f.out);
-                for (uint32_t i = tid; i < 3 * ftot; i += THREADS)
-                    if (w0 + i < wcap) o8[w0 + i] = s8[i];
             }
         }
         d0 = d1;
@@ -1731,7 +1988,7 @@ MergeWs merge_ws(void* d_ws, uint32_t ntables, uint64_t n) {
     w.tile_base = reinterpret_cast<uint64_t*>(p);
     p += al256(ntiles * 8);
     w.lb_status = reinterpret_cast<unsigned long long*>(p);
-    p += al256(ntiles * 8);
+    p += al256(2 * ntiles * 8);
     w.d_stage = reinterpret_cast<uint64_t*>(p);
     p += al256(stage);
     w.err = reinterpret_cast<unsigned long long*>(p);
@@ -1781,7 +2038,8 @@ uint64_t round_offsets(uint64_t* r, uint64_t nr) {
 // `in` is never written unless it is b2).
 int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hgm::MEnt* in,
                   hgm::MEnt* b1, hgm::MEnt* b2, const MergeWs& w, unsigned long long* err,
-                  hgm::FinalArgs fa, hipStream_t stream, const uint64_t* h_roff = nullptr) {
+                  hgm::FinalArgs fa, hipStream_t stream, const uint64_t* h_roff = nullptr,
+                  int* rec_emitted = nullptr) {
     using namespace hgm;
     const uint64_t ntiles = (a.n + TILE - 1) / TILE;
     fa.st = w.lb_status;
@@ -1828,11 +2086,17 @@ int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hg
                                first ? w.lb_status : (unsigned long long*)nullptr);
             first = false;
             if (nr == 2)  // the last round emits the pairs
-                hipLaunchKernelGGL(merge_level_kernel<true>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
-                                   stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
-                                   err, fa);
+                if (fa.rec_out) {  // compaction: the records themselves
+                    hipLaunchKernelGGL(merge_level_kernel<2>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
+                                       stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
+                                       err, fa);
+                    if (rec_emitted) *rec_emitted = 1;
+                } else
+                    hipLaunchKernelGGL(merge_level_kernel<1>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
+                                       stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
+                                       err, fa);
             else
-                hipLaunchKernelGGL(merge_level_kernel<false>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
+                hipLaunchKernelGGL(merge_level_kernel<0>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
                                    stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
                                    err, fa);
             roff += nr + 1;
@@ -1891,7 +2155,7 @@ int rank_path(const hgm::MergeArgs& a, const MergeWs& w, const uint64_t* start, 
         hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
                            (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)serr,
                            (unsigned long long*)nullptr);
-        hipLaunchKernelGGL(merge_level_kernel<false>, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream,
+        hipLaunchKernelGGL(merge_level_kernel<0>, dim3((uint32_t)ntiles), dim3(THREADS), 0, stream,
                            a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base, serr, fa);
         std::swap(cur, nxt);
     }
@@ -1994,8 +2258,10 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                                 const uint64_t* counts, hg_pair* d_out, uint64_t cap,
                                 hg_merge_result* d_result, void* d_ws, void* staging,
                                 hipStream_t stream, int defer, const uint64_t* kp,
-                                uint32_t kp_tag, const unsigned long long* d_err_pre) {
+                                uint32_t kp_tag, const unsigned long long* d_err_pre,
+                                const hgk_merge_records* rec, int* rec_emitted) {
     using namespace hgm;
+    if (rec_emitted) *rec_emitted = 0;
     if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
     uint64_t n = 0;
     for (uint32_t t = 0; t < ntables; ++t) n += counts[t];
@@ -2070,14 +2336,20 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         const uint32_t g1 = (uint32_t)((n + THREADS * PREP_U - 1) / (THREADS * PREP_U));
         hipLaunchKernelGGL(merge_prep_kernel, dim3(g1), dim3(THREADS), 0, stream, a, w.e0, w.err);
     }
-    FinalArgs fa;
+    FinalArgs fa{};
     fa.out = d_out;
     fa.cap = cap;
     fa.result = d_result;
+    if (rec) {  // records mode: the last round writes the records (no pairs)
+        fa.rec_out = rec->out;
+        fa.rec_cap = rec->cap;
+        fa.rec_off = rec->rec_off;
+        fa.enc_result = rec->enc_result;
+    }
     // the rounds ping-pong between e1 and e2, so e0 keeps the entries for the
     // exact loop / the epochs (the first round reads e0)
     int rc = launch_rounds(a, a.run_off + ntables + 1, nruns0, w.e0, w.e1, w.e2, w, w.err, fa,
-                           stream, r0);
+                           stream, r0, rec_emitted);
     if (rc != HG_OK) return rc;
     if (defer)
         hipLaunchKernelGGL(merge_flag_kernel, dim3(1), dim3(1), 0, stream,
@@ -2229,7 +2501,7 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
             return HG_HIP_FAIL;
         MergeArgs ae = a;
         ae.n = ne;
-        FinalArgs fa;
+        FinalArgs fa{};
         fa.out = d_out + std::min(N, cap);
         fa.cap = cap > N ? cap - N : 0;
         fa.result = w.ep_res;

@@ -151,6 +151,7 @@ Knob g_knobs[] = {
     {"HG_COMPACT_KPRE", 0, false},       // 0: no key prefixes from the compaction decode
     {"HG_COMPACT_PREBUILD", 0, false},   // 0: merge entries built after the host has the counts
     {"HG_COMPACT_ENCODE", 0, false},     // 1: compaction encode by the general pair gather
+    {"HG_COMPACT_RECORDS", 0, false},    // 1: compaction merge writes the records (no pairs, no encode pass)
     {"HG_MERGE_KENT", 0, false},         // 0: merge entries by merge_prep_kernel
     {"HG_MERGE_KWAY", 0, false},         // 1: the one-pass k-way merge (3..KW_MAX runs)
     {"HG_MERGE_SERIAL", 0, false},       // 1: the reference loop (rank path), 2: the round-2 loop
@@ -1005,7 +1006,9 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
                 const uint64_t* table_off, const hg_span* const* d_spans, const uint64_t* counts,
                 hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, int defer,
                 const uint64_t* kp = nullptr, uint32_t kp_tag = 0,
-                const unsigned long long* d_err_pre = nullptr) {
+                const unsigned long long* d_err_pre = nullptr,
+                const hgk_merge_records* rec = nullptr, int* rec_emitted = nullptr) {
+    if (rec_emitted) *rec_emitted = 0;
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
@@ -1032,7 +1035,8 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
         if (ensure_pin(c->mstage, hgk_merge_staging_bytes(ntables) + 4096) != HG_OK)
             return HG_HIP_FAIL;
         r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
-                             d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag, d_err_pre);
+                             d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag, d_err_pre,
+                             rec, rec_emitted);
         if (r != HG_OK) return r;
     }
     if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
@@ -1222,8 +1226,20 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     // tables that are not strictly increasing: the merge reports HG_ERR_UNSORTED
     // with no output (the encode then writes nothing) and the epochs below run
     // the reference loop; otherwise merge and encode run back to back
+    // records mode (knob HG_COMPACT_RECORDS 1): the merge's last round writes
+    // the live records' bytes itself (look-back over record and byte
+    // counts) -- no hg_pair array, no encode pass; the encode below runs
+    // whenever the merge did not take that path.  Off by default: measured
+    // slower (same box, alternating; cfg 5 legs 8 x 1 M 1.201-1.209 ms with
+    // pairs + encode vs 1.226-1.231, 8 x 1 GiB 8.95-9.01 vs 9.02-9.05 ms;
+    // profiles/r5_ab_compact_records.log): the fused round's gather runs at 5
+    // waves/SIMD behind a look-back per tile, the record gather at 8.
+    hgk_merge_records rec{d_out, cap, d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, dres_e};
+    const bool rec_mode = hgk_knob("HG_COMPACT_RECORDS", 0) == 1 && hgk_knob("HG_COMPACT_ENCODE", 0) != 1;
+    int emitted = 0;
     r = merge_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm, dres_m,
-                    1, kp.empty() ? nullptr : kp.data(), kp_tag, prebuilt_err);
+                    1, kp.empty() ? nullptr : kp.data(), kp_tag, prebuilt_err, rec_mode ? &rec : nullptr,
+                    &emitted);
     if (r != HG_OK) return r;
     auto encode = [&]() -> int {
         if (nm == 0)
@@ -1242,7 +1258,13 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
                                          block_stride, d_blk, dres_e,
                                          reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
     };
-    if ((r = encode()) != HG_OK) return r;
+    if (!emitted) {
+        if ((r = encode()) != HG_OK) return r;
+    } else if (d_blk) {
+        r = hgk_encode_blocks_launch_dev(static_cast<const uint64_t*>(c->recoff.p), nm, &dres_m->n_out,
+                                         dres_e, block_stride, d_blk, c->stream);
+        if (r != HG_OK) return r;
+    }
     char* h = static_cast<char*>(c->hres.p);
     if (hipMemcpyAsync(h, c->mres.p, 128, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)

@@ -710,3 +710,83 @@ def test_compact_entries_prebuilt_or_not(engine, knobs, unsorted):
         assert np.array_equal(c.data.cpu().numpy(), want), mode
         bad = engine.compact_dev(arena, offs, lens[:1] + [lens[1] - 5] + lens[2:], out)
         assert bad.kind in (1, 2) and bad.table == 1, mode
+
+
+def _arena(engine, datas, pad=8):
+    import torch
+    offs, total = [], 0
+    for d in datas:
+        offs.append(total)
+        total += (d.size + pad - 1) // pad * pad
+    host = np.zeros(max(total, 1), np.uint8)
+    for o, d in zip(offs, datas):
+        host[o:o + d.size] = d
+    return torch.from_numpy(host).to(engine.device), offs
+
+
+@pytest.mark.parametrize("shape", ["mixed_long_prefix", "big_values", "tiny_records", "few_per_tile",
+                                   "one_table_dominates", "odd_arena_offsets"])
+@pytest.mark.parametrize("stride", [0, 3])
+def test_compact_records_mode(engine, knobs, shape, stride):
+    """Compaction's merge in records mode (the last round writes the live
+    records' bytes at offsets from a look-back over record and byte counts;
+    no pair array, no encode pass) == the oracle's compacted table and index,
+    and == the pairs + encode path (knob HG_COMPACT_RECORDS 0), byte for
+    byte; a capacity a few bytes short gives HG_ERR_CAPACITY with the full
+    size and exactly the bytes that fit."""
+    import zlib
+    rng = np.random.default_rng(zlib.crc32(shape.encode()))
+    pad = 8
+    if shape == "mixed_long_prefix":
+        tables = sorted_tables(6, 20000, 0.4, 41, long_prefix=True)
+    elif shape == "big_values":  # records spanning many 16-byte pieces
+        tables = []
+        for t in range(4):
+            ks = sorted({rng.integers(0, 256, 12, dtype=np.uint8).tobytes() for _ in range(900)})
+            tables.append([(k, None if rng.random() < 0.1 else
+                            rng.integers(0, 256, int(rng.integers(200, 3000)), dtype=np.uint8).tobytes())
+                           for k in ks])
+    elif shape == "tiny_records":  # 16-18 byte records: pieces straddle records every time
+        tables = []
+        for t in range(5):
+            ks = sorted({bytes([int(x)]) for x in rng.integers(0, 256, 200)} |
+                        {bytes([int(x), int(y)]) for x, y in rng.integers(0, 256, (3000, 2))})
+            tables.append([(k, None) for k in ks])
+    elif shape == "few_per_tile":  # mostly dead: every table holds the same keys
+        ks = sorted({rng.integers(0, 256, 8, dtype=np.uint8).tobytes() for _ in range(5000)})
+        tables = [[(k, bytes([t]) * 5) for k in ks] for t in range(8)]
+    elif shape == "one_table_dominates":
+        tables = sorted_tables(3, 30000, 0.02, 42)
+        tables[1] = sorted_tables(1, 30000, 0.95, 43)[0]
+    else:  # tables at odd arena offsets: sources of every alignment
+        tables = sorted_tables(4, 8000, 0.5, 44)
+        pad = 1
+    datas = encode_tables(tables)
+    want, wblocks, wn = oracle.compacted_table(datas, block_stride=stride)
+    arena, offs = _arena(engine, datas, pad)
+    lens = [d.size for d in datas]
+    outs = {}
+    for mode in (1, 0):
+        knobs("HG_COMPACT_RECORDS", mode)
+        out = engine.empty(want.size + 64)
+        out.fill_(0xAB)
+        blocks = engine.empty(24 * (wn // stride + 2)) if stride else None
+        c = engine.compact_dev(arena, offs, lens, out, stride, blocks)
+        assert c.status == 0 and c.kind == 0 and c.n == wn, (mode, c)
+        got = out.cpu().numpy()
+        assert np.array_equal(got[:want.size], want), mode
+        assert (got[want.size:] == 0xAB).all(), mode  # nothing past the table
+        if stride:
+            assert np.array_equal(c.blocks.cpu().numpy().view(wblocks.dtype), wblocks), mode
+        outs[mode] = got
+        for short in (1, 17):
+            if want.size <= short:
+                continue
+            small = engine.empty(want.size - short + 64)
+            small.fill_(0xCD)
+            c2 = engine.compact_dev(arena, offs, lens, small[: want.size - short])
+            assert c2.status == 5 and c2.n == wn, (mode, c2)
+            s2 = small.cpu().numpy()
+            assert np.array_equal(s2[: want.size - short], want[: want.size - short]), (mode, short)
+            assert (s2[want.size - short:] == 0xCD).all(), (mode, short)
+    assert np.array_equal(outs[0], outs[1])

@@ -6,8 +6,8 @@
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
 for round in 1 2; do for n in "$@"; do
   d=gpurun_out/cl_${n}_$round; rm -rf $d
-  unset HG_LIBRARY HG_MERGE_KWAY HG_COMPACT_ENCODE HG_MERGE_KENT HG_COMPACT_PREBUILD
-  case $n in base) ;; kway) export HG_MERGE_KWAY=1 ;; noprebuild) export HG_COMPACT_PREBUILD=0 ;; encpairs) export HG_COMPACT_ENCODE=pairs ;; nokent) export HG_MERGE_KENT=0 ;; *) export HG_LIBRARY=build_exp/$n/libhorreum_gpu.so ;; esac
+  unset HG_LIBRARY HG_MERGE_KWAY HG_COMPACT_ENCODE HG_MERGE_KENT HG_COMPACT_PREBUILD HG_COMPACT_RECORDS
+  case $n in base) ;; pairs) export HG_COMPACT_RECORDS=0 ;; kway) export HG_MERGE_KWAY=1 ;; noprebuild) export HG_COMPACT_PREBUILD=0 ;; encpairs) export HG_COMPACT_ENCODE=pairs ;; nokent) export HG_MERGE_KENT=0 ;; *) export HG_LIBRARY=build_exp/$n/libhorreum_gpu.so ;; esac
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $d -- python3 tools/compact_leg.py > $d.log 2>&1 || { tail -5 $d.log; exit 1; }
   echo "== $n round $round: $(grep "^{" $d.log | tail -1 | python3 -c "import json,sys; l=json.loads(sys.stdin.read()); print(l['ms'], l['status'], l.get('merged_records'))")"
   f=$(find $d -name "*kernel_stats.csv" | head -1)
