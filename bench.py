@@ -114,6 +114,7 @@ def barrier(world, device=None):
 
 
 DECODE_KERNELS = ("decode_spec_kernel", "decode_kernel")
+PMC_TAG = "r5"  # the round whose profiles/<tag>_pmc_*.json the legs cite
 
 
 def load_traffic(kernels):
@@ -365,7 +366,7 @@ def main(argv=None):
                                                          exact=True)
         extra["compaction_cfg5_share"] = compaction_leg(torch, eng, device, world, rank,
                                                         per_table=8_134_407, exact=True,
-                                                        pmc_name="r4_pmc_compaction_share.json")
+                                                        pmc_name=f"{PMC_TAG}_pmc_compaction_share.json")
 
     if not args.no_extra:
         extra["decode_general"] = general_legs(torch, eng, device, world)
@@ -480,7 +481,7 @@ def general_legs(torch, eng, device, world, reps=8):
     against the headline's algorithmic bytes (L + 16 n), HIP-event time of
     the decode call; every span checked against the generator's own record
     layout; PMC traffic from the committed, source-hashed profile of the
-    shape (profiles/r4_pmc_<shape>.json)."""
+    shape (profiles/<PMC_TAG>_pmc_<shape>.json)."""
     from horreum_amd import synth
     out = {}
     for key, label, m, kr, vr, tomb, seed, zero in GENERAL_SHAPES:
@@ -505,7 +506,7 @@ def general_legs(torch, eng, device, world, reps=8):
         ok = nn == wn and kind == 0 and bool(np.array_equal(
             spans[: nn * 16].cpu().numpy().view("<u8").reshape(-1, 2), want))
         alg = L + 16 * wn
-        kern, src = load_leg_pmc(f"r4_pmc_{key}.json", ("hg_decode.hip",))
+        kern, src = load_leg_pmc(f"{PMC_TAG}_pmc_{key}.json", ("hg_decode.hip",))
         traffic = sum(v.get("hbm_read_bytes", 0) + v.get("hbm_write_bytes", 0)
                       for k, v in kern.items() if "decode" in k) or None
         out[key] = {"workload": label, "bytes": L, "records": wn,
@@ -910,7 +911,7 @@ def cfg5_value_seed(rank, t):
 
 
 def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000, host=False,
-                   pmc_name="r4_pmc_compaction.json", exact=False):
+                   pmc_name=f"{PMC_TAG}_pmc_compaction.json", exact=False):
     """BASELINE config 5 on this GPU's key range: 8 sorted tables of
     `per_table` records each (16 B keys / 100 B values, 132 B records), 25 %
     of each table's keys shared by all tables.  The global dataset is 8

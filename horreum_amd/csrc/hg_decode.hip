@@ -1894,7 +1894,10 @@ __global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_kernel(DecodeArg
 //      (a wrong guess, or no record starts in its window) is re-walked from
 //      that exit.  So the batch's spans are exact given its entry, like a
 //      stride batch's, and the pre-pass links check the entries as usual.
-constexpr uint32_t HOP_SEG_PIECES = 4;                    // 64 KiB segments
+#ifndef HG_HOP_SEG
+#define HG_HOP_SEG 4
+#endif
+constexpr uint32_t HOP_SEG_PIECES = HG_HOP_SEG;           // 64 KiB segments
 constexpr uint32_t HOP_SEGS = SPEC_BP / HOP_SEG_PIECES;   // per pre-pass batch, at most
 // Batches whose piece 0 shows at most HOP_WIDE_CAND candidate run ends walk
 // HOP_WIDE-piece (128 KiB) segments: half the guesses for chains twice as
