@@ -133,6 +133,8 @@ struct DecodeArgs {
     uint32_t nspec;              // stride pre-pass batches
     uint32_t sbp;                // pieces per pre-pass batch (SPEC_BP_MIN..SPEC_BP)
     uint32_t q;                  // pre-pass batches per general batch (bp / sbp)
+    uint32_t hop_wide;           // hop batches with at most this many piece-0 run ends walk
+                                 // wide segments (HOP_WIDE_CAND, or 0: see hop_wide_cand)
 };
 
 // The piece tags (decode_layout: right after the piece records).
@@ -1899,7 +1901,8 @@ __global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_kernel(DecodeArg
 #endif
 constexpr uint32_t HOP_SEG_PIECES = HG_HOP_SEG;           // 64 KiB segments
 constexpr uint32_t HOP_SEGS = SPEC_BP / HOP_SEG_PIECES;   // per pre-pass batch, at most
-// Batches whose piece 0 shows at most HOP_WIDE_CAND candidate run ends walk
+// (Round 5: only when the pre-pass grid fits the resident workgroups -- see
+// hop_wide_cand.)  Batches whose piece 0 shows at most HOP_WIDE_CAND candidate run ends walk
 // HOP_WIDE-piece (128 KiB) segments: half the guesses for chains twice as
 // long (a walk takes up to HOP_MAX_RECS records per 4 pieces).  Shorter
 // segments measured slower on every hop shape (cfg 4, 32 x 64 MiB: 32 KiB
@@ -2122,7 +2125,7 @@ __device__ bool hop_batch(SpecSmem& s, const DecodeArgs& a, uint32_t p0, uint32_
         }
     }
     // pieces per segment (uniform): wide segments for sparse candidates
-    const uint32_t hsp = uni(s.hcnt[0]) <= HOP_WIDE_CAND ? HOP_WIDE : HOP_SEG_PIECES;
+    const uint32_t hsp = uni(s.hcnt[0]) <= a.hop_wide ? HOP_WIDE : HOP_SEG_PIECES;
     const uint32_t maxr = HOP_MAX_RECS / HOP_SEG_PIECES * hsp;
     const uint32_t nseg = (np + hsp - 1) / hsp;
     uint8_t* w = reinterpret_cast<uint8_t*>(s.data64) + wid * (HOP_WIN + 16);
@@ -3717,7 +3720,7 @@ namespace {
 // Workgroups of `kernel` (256 threads) resident at once on the current device.
 template <typename K>
 uint32_t resident_workgroups(K kernel, int slot) {
-    static int cached[4][64] = {{0}};
+    static int cached[8][64] = {{0}};
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) dev = 0;
     if (!cached[slot][dev]) {
@@ -3761,6 +3764,16 @@ uint32_t spec_pieces(uint32_t bp, uint64_t npieces, uint32_t cus) {
     const uint64_t want = (npieces + 4ull * cus - 1) / (4ull * cus);
     const uint32_t s = pow2_in(knob_or("HG_DECODE_SBP", want), SPEC_BP_MIN, SPEC_BP);
     return s < bp ? s : bp;
+}
+// Wide hop segments (half the guess rounds, chains twice as long) pay off
+// while the pre-pass grid fits the resident workgroups at once; a grid of
+// more batches than resident slots (cfg 4's 32 tables: 2,048 pre-pass
+// workgroups over ~1,024 slots) runs faster on 64 KiB segments throughout
+// (same box, 2 rounds, profiles/r5_ab_hop_geometry.log: cfg 4 0.227-0.228 ->
+// 0.2145-0.2151 ms; one 793 MB table of 8 B-4 KiB values, 757 workgroups,
+// 0.0857 -> 0.0907 ms the other way).
+uint32_t hop_wide_cand(uint64_t grid, uint32_t resident) {
+    return grid > resident ? 0u : hgk::HOP_WIDE_CAND;
 }
 uint32_t device_cus() {
     static int cached[64] = {0};
@@ -3832,6 +3845,7 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     a.kpre_tag = kpre_tag;
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
     a.q = a.bp / a.sbp;
+    a.hop_wide = HOP_WIDE_CAND;
     zero_bytes = (l.status_off + 2 * (uint64_t)a.nbatches * 8 + 7) & ~7ull;
     const uint64_t ll[8] = {l.sbatch_off, l.spiece_off, a.nspec, a.sbp, a.bp, a.nbatches,
                             l.status_off, 0};
@@ -3869,8 +3883,9 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
     const uint32_t bp = general_pieces(npieces, res_gen);
     const uint32_t sbp = spec_pieces(bp, npieces, device_cus());
     uint64_t zero_bytes = 0;
-    const DecodeArgs a = make_args(d_sst, len, d_spans, cap, d_result, d_ws, d_diag, bp, sbp,
-                                   zero_bytes, begin, stop, entry, range, rlen);
+    DecodeArgs a = make_args(d_sst, len, d_spans, cap, d_result, d_ws, d_diag, bp, sbp,
+                             zero_bytes, begin, stop, entry, range, rlen);
+    a.hop_wide = hop_wide_cand(a.nspec, resident_workgroups(decode_spec_kernel, 3));
     if (hipMemsetAsync(d_ws, 0, zero_bytes, stream) != hipSuccess) return HG_HIP_FAIL;
     // 1. pre-pass (stride runs, hop walks): verifies, links neighbours, sums records per group
     // 2. decode_kernel: spans of the resolved prefix, then the general engine
@@ -3981,16 +3996,23 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
     uint32_t* pre_s = reinterpret_cast<uint32_t*>(hs + ms.pre_s);
     uint32_t* pre_d = reinterpret_cast<uint32_t*>(hs + ms.pre_d);
     pre_s[0] = pre_d[0] = 0;
+    uint64_t nspec_all = 0;
     for (uint32_t i = 0; i < ntab; ++i) {
         args[i] = make_args(d_tables[i], lens[i], d_spans[i], caps[i], d_results + i,
                             static_cast<char*>(d_ws) + ws_off[i], nullptr, bp, sbp, zb[i], 0,
                             ~0ull, 0, false, ~0ull, kpre_tag);
         const uint32_t gs = lens[i] ? args[i].nspec : 0;
+        nspec_all += gs;
         const uint32_t gd = lens[i] ? (args[i].nbatches > args[i].nspec ? args[i].nbatches
                                                                           : args[i].nspec)
                                     : 0;
         pre_s[i + 1] = pre_s[i] + gs;
         pre_d[i + 1] = pre_d[i] + gd;
+    }
+    {
+        const uint32_t hw = hop_wide_cand(nspec_all, kpre_tag ? resident_workgroups(decode_spec_multi<true>, 4)
+                                                             : resident_workgroups(decode_spec_multi<false>, 5));
+        for (uint32_t i = 0; i < ntab; ++i) args[i].hop_wide = hw;
     }
     const uint64_t bytes = hgk_decode_multi_stage_bytes(ntab);
     if (hipMemcpyAsync(d_stage, h_stage, bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
