@@ -7,16 +7,23 @@
 #include "../../include/horreum_gpu.h"
 #include "hg_err.hpp"
 
-// Records mode of a merge (compaction; hgk_merge_launch in hg_merge.hip):
-// the last round writes the live records' bytes to out (cap bytes; rec_off,
-// nullable: each record's output offset) and the encode result -- no hg_pair
-// array, no encode pass.
+// Compaction extras of a merge (hgk_merge_launch in hg_merge.hip).
+// out non-null: records mode -- the last round writes the live records' bytes
+// to out (cap bytes; rec_off, nullable: each record's output offset) and the
+// encode result, no hg_pair array, no encode pass.  zero (nullable):
+// zero_words words the defer-mode flag kernel clears for the encode that
+// follows on the stream (its block sums; a memset launch fewer).
 struct hgk_merge_records {
     uint8_t* out;
     uint64_t cap;
     uint64_t* rec_off;
     hg_encode_result* enc_result;
+    uint64_t* zero;
+    uint64_t zero_words;
 };
+// hgk_merge_launch's done flags
+constexpr int HGK_MERGE_EMITTED = 1;  // records mode wrote the records
+constexpr int HGK_MERGE_ZEROED = 2;   // the flag kernel cleared rec->zero
 
 namespace hgk {
 

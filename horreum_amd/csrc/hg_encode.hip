@@ -687,7 +687,7 @@ int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t 
                        const uint64_t* d_n, int mode, uint64_t rec_arena_len, uint8_t* d_out,
                        uint64_t cap, uint64_t* d_rec_off, uint64_t rec_base,
                        uint32_t block_stride, hg_block* d_blocks, hg_encode_result* d_result,
-                       unsigned long long* d_status, hipStream_t stream) {
+                       unsigned long long* d_status, hipStream_t stream, bool gsum_zeroed = false) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
@@ -698,7 +698,8 @@ int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t 
             return HG_HIP_FAIL;
         return HG_OK;
     }
-    if (hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess) return HG_HIP_FAIL;
+    if (!gsum_zeroed && hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess)
+        return HG_HIP_FAIL;
     hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
                        d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum), d_n);
     if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
@@ -754,9 +755,19 @@ extern "C" int hgk_encode_launch_records(const uint8_t* d_arena, uint64_t arena_
                                          uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
                                          uint32_t block_stride, hg_block* d_blocks,
                                          hg_encode_result* d_result, unsigned long long* d_status,
-                                         hipStream_t stream) {
+                                         hipStream_t stream, int gsum_zeroed) {
     return encode_launch_mode(d_arena, d_pairs, n, d_n, 2, arena_len, d_out, cap, d_rec_off, 0,
-                              block_stride, d_blocks, d_result, d_status, stream);
+                              block_stride, d_blocks, d_result, d_status, stream, gsum_zeroed != 0);
+}
+
+// The group sums an encode of n pairs accumulates into (words from d_status):
+// cleared by the launch unless its caller had them cleared earlier on the
+// stream (gsum_zeroed; the compaction's merge flag kernel does).
+extern "C" void hgk_encode_group_sums(uint64_t n, uint64_t* first_word, uint64_t* words) {
+    using namespace hgk;
+    const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
+    *first_word = nt;
+    *words = (nt + ENC_GROUP - 1) / ENC_GROUP;
 }
 
 extern "C" int hgk_encode_launch_at(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,

@@ -34,7 +34,8 @@ extern "C" int hgk_encode_launch_ex(const uint8_t*, const hg_pair*, uint64_t, co
 extern "C" int hgk_encode_launch_records(const uint8_t*, uint64_t, const hg_pair*, uint64_t,
                                          const uint64_t*, uint8_t*, uint64_t, uint64_t*, uint32_t,
                                          hg_block*, hg_encode_result*, unsigned long long*,
-                                         hipStream_t);
+                                         hipStream_t, int gsum_zeroed);
+extern "C" void hgk_encode_group_sums(uint64_t n, uint64_t* first_word, uint64_t* words);
 extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
                                         hipStream_t);
 extern "C" int hgk_encode_size_launch(const hg_pair*, uint64_t, hg_encode_result*, unsigned long long*,
@@ -60,7 +61,7 @@ extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64
                                 hg_merge_result*, void*, void*, hipStream_t, int defer,
                                 const uint64_t* kp, uint32_t kp_tag,
                                 const unsigned long long* d_err_pre,
-                                const hgk_merge_records* rec, int* rec_emitted);
+                                const hgk_merge_records* rec, int* done);
 extern "C" int hgk_encode_blocks_launch_dev(const uint64_t* d_rec_off, uint64_t n_ub,
                                             const uint64_t* d_n, const hg_encode_result* d_res,
                                             uint32_t stride, hg_block* d_blocks, hipStream_t stream);

@@ -1435,7 +1435,8 @@ __global__ __launch_bounds__(64) void merge_exact_kernel(MergeArgs a, const MEnt
                                                          ExactHead* hs, hg_pair* out, uint64_t cap,
                                                          hg_merge_result* result,
                                                          const uint64_t* start, uint64_t n0) {
-    if (*err == ~0ull) return;  // every table strictly increasing: the rounds did the merge
+    // err nullptr (the epochs' hand-over): run the loop unconditionally
+    if (err && *err == ~0ull) return;  // every table strictly increasing: the rounds did the merge
     const uint32_t lane = threadIdx.x;
     bool any = false;
     for (uint32_t t = lane; t < a.ntables; t += 64) {
@@ -1587,8 +1588,12 @@ __global__ __launch_bounds__(THREADS) void merge_bound_kernel(MergeArgs a, const
 
 // defer mode: the merge found input that is not strictly increasing and
 // leaves it to the host's epoch driver (no pairs, n_out 0)
-__global__ void merge_flag_kernel(const unsigned long long* err, hg_merge_result* result) {
-    if (*err == ~0ull) return;
+// zero/zero_words: a buffer the next kernel on the stream accumulates into
+// (the compaction's encode block sums), cleared here instead of by a memset
+__global__ void merge_flag_kernel(const unsigned long long* err, hg_merge_result* result,
+                                  uint64_t* zero, uint64_t zero_words) {
+    for (uint64_t i = threadIdx.x; i < zero_words; i += blockDim.x) zero[i] = 0;
+    if (threadIdx.x != 0 || *err == ~0ull) return;
     hg_merge_result r;
     r.n_out = 0;
     r.kind = HG_ERR_UNSORTED;
@@ -2039,7 +2044,7 @@ uint64_t round_offsets(uint64_t* r, uint64_t nr) {
 int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hgm::MEnt* in,
                   hgm::MEnt* b1, hgm::MEnt* b2, const MergeWs& w, unsigned long long* err,
                   hgm::FinalArgs fa, hipStream_t stream, const uint64_t* h_roff = nullptr,
-                  int* rec_emitted = nullptr) {
+                  int* done = nullptr) {
     using namespace hgm;
     const uint64_t ntiles = (a.n + TILE - 1) / TILE;
     fa.st = w.lb_status;
@@ -2090,7 +2095,7 @@ int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hg
                     hipLaunchKernelGGL(merge_level_kernel<2>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
                                        stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
                                        err, fa);
-                    if (rec_emitted) *rec_emitted = 1;
+                    if (done) *done |= HGK_MERGE_EMITTED;
                 } else
                     hipLaunchKernelGGL(merge_level_kernel<1>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
                                        stream, a, l, (const MEnt*)cur, nxt, (const uint64_t*)w.tile_base,
@@ -2259,9 +2264,9 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
                                 hg_merge_result* d_result, void* d_ws, void* staging,
                                 hipStream_t stream, int defer, const uint64_t* kp,
                                 uint32_t kp_tag, const unsigned long long* d_err_pre,
-                                const hgk_merge_records* rec, int* rec_emitted) {
+                                const hgk_merge_records* rec, int* done) {
     using namespace hgm;
-    if (rec_emitted) *rec_emitted = 0;
+    if (done) *done = 0;
     if (ntables == 0 || ntables > MAX_TABLES) return HG_ERR_INVALID_ARG;
     uint64_t n = 0;
     for (uint32_t t = 0; t < ntables; ++t) n += counts[t];
@@ -2322,11 +2327,13 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     // kp[3 ntables] = the batched decode's device staging, kp[3 ntables + 1]
     // its pre-pass grid) instead of merge_prep_kernel's per-record chains
     const bool kent_on = hgk_knob("HG_MERGE_KENT", 1) != 0;  // 0: merge_prep_kernel (A/B runs)
+    // the entries were built into w.e0 by hgk_merge_prebuild while the host
+    // waited for the counts: its order-check word is the one the rounds and
+    // the flag read (w.err, set by the staging copy, stays unused)
+    unsigned long long* const err =
+        d_err_pre ? const_cast<unsigned long long*>(d_err_pre) : w.err;
     if (d_err_pre) {
-        // the entries were built into w.e0 by hgk_merge_prebuild while the
-        // host waited for the counts: take over its order-check word
-        if (hipMemcpyAsync(w.err, d_err_pre, 8, hipMemcpyDeviceToDevice, stream) != hipSuccess)
-            return HG_HIP_FAIL;
+        // entries in place (hgk_merge_prebuild)
     } else if (kent_grid && kent_on) {
         const int rk = hgk_decode_entries_launch(
             reinterpret_cast<const void*>(kp[3 * (uint64_t)ntables]), ntables, kent_grid, a.run_off,
@@ -2340,7 +2347,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     fa.out = d_out;
     fa.cap = cap;
     fa.result = d_result;
-    if (rec) {  // records mode: the last round writes the records (no pairs)
+    if (rec && rec->out) {  // records mode: the last round writes the records (no pairs)
         fa.rec_out = rec->out;
         fa.rec_cap = rec->cap;
         fa.rec_off = rec->rec_off;
@@ -2348,15 +2355,18 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     }
     // the rounds ping-pong between e1 and e2, so e0 keeps the entries for the
     // exact loop / the epochs (the first round reads e0)
-    int rc = launch_rounds(a, a.run_off + ntables + 1, nruns0, w.e0, w.e1, w.e2, w, w.err, fa,
-                           stream, r0, rec_emitted);
+    int rc = launch_rounds(a, a.run_off + ntables + 1, nruns0, w.e0, w.e1, w.e2, w, err, fa,
+                           stream, r0, done);
     if (rc != HG_OK) return rc;
-    if (defer)
-        hipLaunchKernelGGL(merge_flag_kernel, dim3(1), dim3(1), 0, stream,
-                           (const unsigned long long*)w.err, d_result);
-    else
+    if (defer) {
+        uint64_t* const zero = rec ? rec->zero : nullptr;
+        const uint64_t zero_words = zero ? rec->zero_words : 0;
+        hipLaunchKernelGGL(merge_flag_kernel, dim3(1), dim3(THREADS), 0, stream,
+                           (const unsigned long long*)err, d_result, zero, zero_words);
+        if (zero && done) *done |= HGK_MERGE_ZEROED;
+    } else
         hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)w.e0,
-                           (const unsigned long long*)w.err, w.heads, d_out, cap, d_result,
+                           (const unsigned long long*)err, w.heads, d_out, cap, d_result,
                            (const uint64_t*)nullptr, (uint64_t)0);
     return HG_LAUNCH_STATUS();
 }
@@ -2422,8 +2432,10 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
                 return HG_HIP_FAIL;
             dstart = w.ep;
         }
+        // the epochs run only after an order violation: the loop runs unconditionally
         hipLaunchKernelGGL(merge_exact_kernel, dim3(1), dim3(64), 0, stream, a, (const MEnt*)w.e0,
-                           (const unsigned long long*)w.err, w.heads, d_out, cap, d_result, dstart, n0);
+                           (const unsigned long long*)nullptr, w.heads, d_out, cap, d_result, dstart,
+                           n0);
         int r2 = HG_LAUNCH_STATUS();
         if (r2 != HG_OK) return r2;
         return sync_copy(h_result, d_result, sizeof(hg_merge_result), hipMemcpyDeviceToHost, stream);

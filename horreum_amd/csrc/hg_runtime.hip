@@ -12,6 +12,7 @@
 #include <mutex>
 #include <new>
 #include <thread>
+#include <utility>
 #include <vector>
 
 
@@ -1007,8 +1008,8 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
                 hg_pair* d_out, uint64_t cap, hg_merge_result* d_result, int defer,
                 const uint64_t* kp = nullptr, uint32_t kp_tag = 0,
                 const unsigned long long* d_err_pre = nullptr,
-                const hgk_merge_records* rec = nullptr, int* rec_emitted = nullptr) {
-    if (rec_emitted) *rec_emitted = 0;
+                const hgk_merge_records* rec = nullptr, int* done = nullptr) {
+    if (done) *done = 0;
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
@@ -1036,7 +1037,7 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
             return HG_HIP_FAIL;
         r = hgk_merge_launch(d_arena, arena_len, ntables, table_off, d_spans, counts, d_out, cap,
                              d_result, c->mws.p, c->mstage.p, c->stream, defer, kp, kp_tag, d_err_pre,
-                             rec, rec_emitted);
+                             rec, done);
         if (r != HG_OK) return r;
     }
     if (hipEventRecord(c->mstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
@@ -1241,13 +1242,24 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     // pairs + encode vs 1.226-1.231, 8 x 1 GiB 8.95-9.01 vs 9.02-9.05 ms;
     // profiles/r5_ab_compact_records.log): the fused round's gather runs at 5
     // waves/SIMD behind a look-back per tile, the record gather at 8.
-    hgk_merge_records rec{d_out, cap, d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr, dres_e};
-    const bool rec_mode = hgk_knob("HG_COMPACT_RECORDS", 0) == 1 && hgk_knob("HG_COMPACT_ENCODE", 0) != 1;
-    int emitted = 0;
+    const bool enc_records = hgk_knob("HG_COMPACT_ENCODE", 0) != 1;
+    const bool rec_mode = hgk_knob("HG_COMPACT_RECORDS", 0) == 1 && enc_records;
+    // the records encode's group sums are cleared by the merge's flag kernel
+    // (c->ws holds them: sized for the encode of nm pairs above)
+    uint64_t gs_first = 0, gs_words = 0;
+    hgk_encode_group_sums(nm, &gs_first, &gs_words);
+    hgk_merge_records rec{rec_mode ? d_out : nullptr,
+                          cap,
+                          d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr,
+                          dres_e,
+                          enc_records && nm ? static_cast<uint64_t*>(c->ws.p) + gs_first : nullptr,
+                          gs_words};
+    int done = 0;
     r = merge_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm, dres_m,
-                    1, kp.empty() ? nullptr : kp.data(), kp_tag, prebuilt_err, rec_mode ? &rec : nullptr,
-                    &emitted);
+                    1, kp.empty() ? nullptr : kp.data(), kp_tag, prebuilt_err, &rec, &done);
     if (r != HG_OK) return r;
+    const bool emitted = (done & HGK_MERGE_EMITTED) != 0;
+    bool zeroed = (done & HGK_MERGE_ZEROED) != 0;  // for the first encode only
     auto encode = [&]() -> int {
         if (nm == 0)
             return hipMemsetAsync(dres_e, 0, sizeof(hg_encode_result), c->stream) == hipSuccess
@@ -1263,7 +1275,8 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
         return hgk_encode_launch_records(arena, arena_len, pairs, nm, &dres_m->n_out, d_out, cap,
                                          d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr,
                                          block_stride, d_blk, dres_e,
-                                         reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+                                         reinterpret_cast<unsigned long long*>(c->ws.p), c->stream,
+                                         std::exchange(zeroed, false));
     };
     if (!emitted) {
         if ((r = encode()) != HG_OK) return r;
