@@ -11,9 +11,10 @@ collectives are the timing barrier and the max-over-ranks reduction).
 Prints ONE JSON line (rank 0).  `roofline` prices one decode call against
 HBM: algorithmic bytes = L + 16 n (read the table once, write 16-byte spans),
 divided by the call's duration measured with HIP events on the stream its
-kernels run on.  A decode call is a short pipeline (status memset,
-decode_spec_kernel, decode_kernel -- the latter writes the spans of the
-pre-pass's resolved prefix and runs the general engine on the rest); the
+kernels run on.  A decode call is a short pipeline (decode_spec_kernel,
+decode_kernel -- the latter writes the spans of the pre-pass's resolved
+prefix and runs the general engine on the rest; the statuses are cleared by
+the previous call's pre-pass, so repeated calls launch no memset); the
 stride pre-pass dominates (profiles/).  `cpu_baseline` times the oracle
 (the C restatement of the reference's Rust decode, with its per-record
 ownership pattern) on one host core over the same bytes.
@@ -423,7 +424,7 @@ def main(argv=None):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "decode call: status memset + decode_spec_kernel (dominant) + "
+                         "kernel": "decode call: decode_spec_kernel (dominant) + "
                                    "decode_kernel (prefix spans + general engine)",
                          "alg_bytes_per_launch": alg_bytes,
                          "mean_launch_ms": round(mean_launch_ms, 5)},

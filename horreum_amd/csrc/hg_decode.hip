@@ -40,6 +40,8 @@
 //     batch exactly from X_b (pieces re-read), emitting directly.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "hg_device.hpp"
 #include "hg_knobs.hpp"
 
@@ -135,6 +137,10 @@ struct DecodeArgs {
     uint32_t q;                  // pre-pass batches per general batch (bp / sbp)
     uint32_t hop_wide;           // hop batches with at most this many piece-0 run ends walk
                                  // wide segments (HOP_WIDE_CAND, or 0: see hop_wide_cand)
+    // the NEXT call's control region (hgk_decode_launch_ctl; null otherwise):
+    // decode_spec_kernel zeroes its first zero_next_n16 x 16 bytes
+    uint4* zero_next;
+    uint32_t zero_next_n16;
 };
 
 // The piece tags (decode_layout: right after the piece records).
@@ -3428,6 +3434,13 @@ __device__ void lw_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint3
 
 __global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, SpecBatch* sb,
                                                               SpecPiece* sp) {
+    // the other half of a double-buffered control region, cleared for the
+    // next call (no workgroup of this call reads it): that call then needs no
+    // memset launch ahead of its pre-pass (hgk_decode_launch_ctl)
+    if (a.zero_next)
+        for (uint32_t i = blockIdx.x * THREADS + threadIdx.x; i < a.zero_next_n16;
+             i += gridDim.x * THREADS)
+            a.zero_next[i] = make_uint4(0u, 0u, 0u, 0u);
 #ifdef HG_SPEC_SWAP_PAIRS  // diagnostics: workgroup b takes batch b ^ 1 (XCD vs address)
     spec_body<false>(a, sb, sp, (blockIdx.x ^ 1u) < a.nspec ? blockIdx.x ^ 1u : blockIdx.x);
 #else
@@ -3800,7 +3813,7 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
                           hg_decode_result* d_result, void* d_ws, uint32_t* d_diag, uint32_t bp,
                           uint32_t sbp, uint64_t& zero_bytes, uint64_t begin = 0,
                           uint64_t stop = ~0ull, uint64_t entry = 0, bool range = false,
-                          uint64_t rlen = ~0ull, uint32_t kpre_tag = 0) {
+                          uint64_t rlen = ~0ull, uint32_t kpre_tag = 0, void* d_ctl = nullptr) {
     using namespace hgk;
     if (stop > len) stop = len;
     if (rlen > len) rlen = len;
@@ -3825,11 +3838,14 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     a.cap = cap;
     a.result = d_result;
     char* ws = static_cast<char*>(d_ws);
-    DecodeCtl* ctl = static_cast<DecodeCtl*>(d_ws);
+    // the control region [0, scratch_off) lives at the workspace start, or in
+    // a separate buffer (d_ctl, hgk_decode_launch_ctl)
+    char* cr = d_ctl ? static_cast<char*>(d_ctl) : ws;
+    DecodeCtl* ctl = reinterpret_cast<DecodeCtl*>(cr);
     a.ctl = ctl;
-    a.gsum = reinterpret_cast<unsigned long long*>(ws + l.gsum_off);
-    a.link = reinterpret_cast<unsigned long long*>(ws + l.link_off);
-    a.status = reinterpret_cast<unsigned long long*>(ws + l.status_off);
+    a.gsum = reinterpret_cast<unsigned long long*>(cr + l.gsum_off);
+    a.link = reinterpret_cast<unsigned long long*>(cr + l.link_off);
+    a.status = reinterpret_cast<unsigned long long*>(cr + l.status_off);
     a.ticket = &ctl->ticket;
     a.scratch = reinterpret_cast<hg_span*>(ws + l.scratch_off);
     a.bp = bp;
@@ -3846,6 +3862,8 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     a.nspec = (uint32_t)((l.npieces + a.sbp - 1) / a.sbp);
     a.q = a.bp / a.sbp;
     a.hop_wide = HOP_WIDE_CAND;
+    a.zero_next = nullptr;
+    a.zero_next_n16 = 0;
     zero_bytes = (l.status_off + 2 * (uint64_t)a.nbatches * 8 + 7) & ~7ull;
     const uint64_t ll[8] = {l.sbatch_off, l.spiece_off, a.nspec, a.sbp, a.bp, a.nbatches,
                             l.status_off, 0};
@@ -3867,9 +3885,18 @@ __global__ void decode_const_result(hg_decode_result* r, uint64_t off) {
     *r = v;
 }
 
+// ctl (nullable): the double-buffered control region of hgk_decode_launch_ctl.
+struct CtlPair {
+    void* cur;            // this call's control region
+    uint64_t cur_clean;   // bytes of it known to be zero
+    void* next;           // the next call's, cleared by the pre-pass
+    uint64_t next_bytes;  // room in it
+    uint64_t* zeroed;     // out: bytes of `next` cleared
+};
 int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t cap,
                   hg_decode_result* d_result, void* d_ws, uint32_t* d_diag, hipStream_t stream,
-                  uint64_t begin, uint64_t stop, uint64_t entry, bool range, uint64_t rlen) {
+                  uint64_t begin, uint64_t stop, uint64_t entry, bool range, uint64_t rlen,
+                  const CtlPair* ctl = nullptr) {
     using namespace hgk;
     if (stop > len) stop = len;
     if (entry >= stop) {  // no record starts in the range: 0 records, exit = entry
@@ -3884,9 +3911,21 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
     const uint32_t sbp = spec_pieces(bp, npieces, device_cus());
     uint64_t zero_bytes = 0;
     DecodeArgs a = make_args(d_sst, len, d_spans, cap, d_result, d_ws, d_diag, bp, sbp,
-                             zero_bytes, begin, stop, entry, range, rlen);
+                             zero_bytes, begin, stop, entry, range, rlen, 0u,
+                             ctl ? ctl->cur : nullptr);
     a.hop_wide = hop_wide_cand(a.nspec, resident_workgroups(decode_spec_kernel, 3));
-    if (hipMemsetAsync(d_ws, 0, zero_bytes, stream) != hipSuccess) return HG_HIP_FAIL;
+    if (!ctl || ctl->cur_clean < zero_bytes) {
+        if (hipMemsetAsync(ctl ? ctl->cur : d_ws, 0, zero_bytes, stream) != hipSuccess)
+            return HG_HIP_FAIL;
+    }
+    if (ctl) {
+        // the next call of the same geometry finds its region clear (one of
+        // this size or smaller; another pays the memset)
+        const uint64_t z16 = std::min((zero_bytes + 15) / 16, ctl->next_bytes / 16);
+        a.zero_next = static_cast<uint4*>(ctl->next);
+        a.zero_next_n16 = (uint32_t)z16;
+        *ctl->zeroed = z16 * 16;
+    }
     // 1. pre-pass (stride runs, hop walks): verifies, links neighbours, sums records per group
     // 2. decode_kernel: spans of the resolved prefix, then the general engine
     //    from the first unresolved batch on (exits at once if there is none)
@@ -3947,6 +3986,24 @@ extern "C" int hgk_decode_launch(const uint8_t* d_sst, uint64_t len, hg_span* d_
                                  uint64_t cap, hg_decode_result* d_result, void* d_ws,
                                  hipStream_t stream) {
     return hgk_decode_launch_diag(d_sst, len, d_spans, cap, d_result, d_ws, nullptr, stream);
+}
+
+// Bytes of a table's control region (statuses, links, group sums, ticket):
+// the part of the workspace zeroed before every call.
+extern "C" uint64_t hgk_decode_ctl_bytes(uint64_t len) { return decode_layout(len).scratch_off; }
+
+// hgk_decode_launch with the control region in d_ctl (hgk_decode_ctl_bytes(len)
+// bytes) instead of the workspace start, `clean` bytes of it known to be zero
+// (no memset launch when that covers this call's), and d_next (next_bytes) the
+// next call's region: the pre-pass clears it; *zeroed = the bytes cleared.
+extern "C" int hgk_decode_launch_ctl(const uint8_t* d_sst, uint64_t len, hg_span* d_spans,
+                                     uint64_t cap, hg_decode_result* d_result, void* d_ws,
+                                     void* d_ctl, uint64_t clean, void* d_next,
+                                     uint64_t next_bytes, uint64_t* zeroed, hipStream_t stream) {
+    *zeroed = 0;
+    const CtlPair cp{d_ctl, clean, d_next, next_bytes, zeroed};
+    return launch_decode(d_sst, len, d_spans, cap, d_result, d_ws, nullptr, stream, 0, len, 0,
+                         false, len, &cp);
 }
 
 // Many tables, three launches in all (zero, pre-pass, decode).  Batch

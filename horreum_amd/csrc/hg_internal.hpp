@@ -9,6 +9,11 @@
 #include "../../include/horreum_gpu.h"
 #include "hg_err.hpp"
 
+extern "C" uint64_t hgk_decode_ctl_bytes(uint64_t len);
+extern "C" int hgk_decode_launch_ctl(const uint8_t*, uint64_t, hg_span*, uint64_t,
+                                     hg_decode_result*, void* d_ws, void* d_ctl, uint64_t clean,
+                                     void* d_next, uint64_t next_bytes, uint64_t* zeroed,
+                                     hipStream_t);
 extern "C" int hgk_decode_launch(const uint8_t*, uint64_t, hg_span*, uint64_t, hg_decode_result*,
                                  void*, hipStream_t);
 extern "C" int hgk_decode_range_launch(const uint8_t*, uint64_t, uint64_t, uint64_t, uint64_t,
@@ -93,6 +98,12 @@ struct hg_ctx {
     hipStream_t own = nullptr;
     hipStream_t stream = nullptr;
     hgi::DevBuf ws;        // decode statuses / encode tile statuses
+    // single-table decode: two control regions used in turn, each call's
+    // pre-pass clearing the other's (hgk_decode_launch_ctl); dctl_clean:
+    // bytes of each known to be zero
+    hgi::DevBuf dctl;
+    uint64_t dctl_clean[2] = {0, 0};
+    int dctl_cur = 0;
     hgi::DevBuf recoff;    // encode record offsets when blocks are wanted w/o rec_off
     hgi::DevBuf results;   // hg_decode_result + hg_encode_result
     hgi::PinBuf hres;      // pinned mirror of `results`

@@ -124,6 +124,13 @@ extern "C" {
 // Diagnostics only (not in include/horreum_gpu.h): the decode workspace and a
 // blocking device->host copy, for tools/spec_diag.py.
 void* hgk_ctx_workspace(hg_ctx* c) { return c ? c->ws.p : nullptr; }
+// the control region (DecodeCtl, group sums, links, statuses) of the last
+// single-table decode (hg_decode_dev_async: two regions used in turn)
+void* hgk_ctx_decode_ctl(hg_ctx* c) {
+    if (!c || !c->dctl.p) return nullptr;
+    const uint64_t half = c->dctl.bytes / 2 & ~(uint64_t)255;
+    return static_cast<char*>(c->dctl.p) + (1 - c->dctl_cur) * half;
+}
 int hgk_debug_d2h(void* dst, const void* src, uint64_t n) {
     return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }
@@ -235,7 +242,7 @@ int hg_ctx_destroy(hg_ctx* c) {
     if (!c) return HG_ERR_INVALID_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->ws, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
+    for (DevBuf* b : {&c->ws, &c->dctl, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
                       &c->bws, &c->bstage_d, &c->x_res, &c->x_aux, &c->x_arena, &c->x_spans})
         if (b->p) hipFree(b->p);
@@ -259,7 +266,8 @@ int hg_ctx_trim(hg_ctx* c) {
     if (!c) return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return HG_HIP_FAIL;
-    for (DevBuf* b : {&c->ws, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
+    c->dctl_clean[0] = c->dctl_clean[1] = 0;
+    for (DevBuf* b : {&c->ws, &c->dctl, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res, &c->bws,
                       &c->x_aux, &c->x_arena, &c->x_spans}) {
         if (b->p) hipFree(b->p);
@@ -294,12 +302,22 @@ int hg_ctx_synchronize(hg_ctx* c) {
     return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }
 
+// The single-table decode's two control regions (hg_ctx::dctl) for a table
+// of len bytes; a new allocation holds nothing known to be zero.
+static int ensure_dctl(hg_ctx* c, uint64_t len) {
+    const uint64_t need = 2 * ((hgk_decode_ctl_bytes(len) + 255) & ~(uint64_t)255);
+    if (c->dctl.bytes >= need) return HG_OK;
+    c->dctl_clean[0] = c->dctl_clean[1] = 0;
+    return ensure(c, c->dctl, need);
+}
+
 int hg_ctx_reserve(hg_ctx* c, uint64_t max_sst_bytes, uint64_t max_pairs) {
     if (!c) return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     size_t need = std::max(hgk_decode_workspace_bytes(max_sst_bytes),
                            hgk_encode_workspace_bytes(max_pairs));
     int r = ensure(c, c->ws, need);
+    if (r == HG_OK && max_sst_bytes) r = ensure_dctl(c, max_sst_bytes);
     if (r == HG_OK && max_pairs) r = ensure(c, c->recoff, max_pairs * sizeof(uint64_t));
     return r;
 }
@@ -320,7 +338,18 @@ int hg_decode_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* 
                    : HG_HIP_FAIL;
     int r = ensure(c, c->ws, hgk_decode_workspace_bytes(len));
     if (r != HG_OK) return r;
-    return hgk_decode_launch(d_sst, len, d_spans, cap, d_result, c->ws.p, c->stream);
+    if ((r = ensure_dctl(c, len)) != HG_OK) return r;
+    const uint64_t half = c->dctl.bytes / 2 & ~(uint64_t)255;
+    char* base = static_cast<char*>(c->dctl.p);
+    const int cur = c->dctl_cur;
+    uint64_t zeroed = 0;
+    r = hgk_decode_launch_ctl(d_sst, len, d_spans, cap, d_result, c->ws.p, base + cur * half,
+                              c->dctl_clean[cur], base + (1 - cur) * half, half, &zeroed,
+                              c->stream);
+    c->dctl_clean[cur] = 0;  // this call's statuses
+    c->dctl_clean[1 - cur] = r == HG_OK ? zeroed : 0;
+    c->dctl_cur = 1 - cur;
+    return r;
 }
 
 static int finish_decode(const hg_decode_result& res, uint64_t cap, uint64_t* n_out,

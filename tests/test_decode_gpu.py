@@ -570,13 +570,21 @@ def test_one_lane_chunk_walk_errors(engine):
         assert_same(engine, data[:o + 7])
 
 
-def _ctl_repairs(engine):
+def _ctl_words(engine):
+    """DecodeCtl of the last single-table decode (ticket, bad_rev, progress,
+    repairs): its control region is one of two the context uses in turn."""
     import ctypes
     lib = engine.lib
+    lib.hgk_ctx_decode_ctl.restype = ctypes.c_void_p
+    lib.hgk_ctx_decode_ctl.argtypes = [ctypes.c_void_p]
+    lib.hgk_debug_d2h.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     ctl = np.zeros(4, np.uint32)
-    ws = lib.hgk_ctx_workspace(engine.ctx)
-    lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws), 16)
-    return int(ctl[3])
+    lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(lib.hgk_ctx_decode_ctl(engine.ctx)), 16)
+    return ctl
+
+
+def _ctl_repairs(engine):
+    return int(_ctl_words(engine)[3])
 
 
 @pytest.mark.parametrize("fake_every", [1, 3])
@@ -632,8 +640,7 @@ def _prepass_links(engine, sst):
     sbd = np.dtype([("x0", "<u8"), ("exit", "<u8"), ("count", "<u4"), ("ok", "<u4"), ("pad", "<u8")])
     sb = np.zeros(nspec, sbd)
     lib.hgk_debug_d2h(sb.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws + sb_off), sb.nbytes)
-    ctl = np.zeros(4, np.uint32)
-    lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws), 16)
+    ctl = _ctl_words(engine)
     links = int(np.sum(sb["x0"][1:] != sb["exit"][:-1]))
     return out, nspec - int(ctl[1]), links, int(ctl[3]), sb["pad"] & 0xFF, nspec
 
@@ -703,3 +710,26 @@ def test_one_stride_two_shapes(engine, split):
     pairs["vlen"][sel] = 96
     data = oracle.encode(arena, pairs)[0]
     assert_same(engine, data)
+
+
+def test_control_region_reuse(engine):
+    """hg_decode_dev_async keeps two control regions and each call's pre-pass
+    clears the next call's, so a call whose region is already clear skips the
+    memset.  Calls of growing, shrinking and repeated sizes, a corrupt table
+    and a stride table in between, on one context: every result bit-exact vs
+    the oracle (a stale status, link or ticket would misplace spans)."""
+    big = _shape_table(400_000, (0, 24), (0, 64), seed=11)
+    small = _shape_table(30_000, (8, 65), (64, 513), seed=12)
+    bad = big[: big.size // 2].copy()
+    bad[bad.size // 3 + 8:bad.size // 3 + 16] = 0xFF  # a length field past the end
+    stride = _shape_table(200_000, (16, 17), (100, 101), seed=13)
+    tables = {"big": big, "small": small, "bad": bad, "stride": stride, "tiny": big[:100]}
+    want = {k: oracle.decode(v) for k, v in tables.items()}
+    dev = {k: engine.to_device(v) for k, v in tables.items()}
+    for name in ["big", "big", "small", "big", "bad", "big", "small", "small", "stride",
+                 "stride", "tiny", "big", "bad", "bad", "small", "big"]:
+        ws, wn, wk, wo, _ = want[name]
+        out = engine.decode_dev(dev[name], tables[name].size)
+        spans = engine.spans_to_numpy(out.spans, min(out.n, tables[name].size // 16))
+        assert (out.n, out.kind, out.offset) == (wn, wk, wo), name
+        assert np.array_equal(spans, ws), name

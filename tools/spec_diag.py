@@ -55,8 +55,11 @@ def main():
         sb = np.zeros(nspec, SB)
         lib.hgk_debug_d2h(sb.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws + sb_off),
                           sb.nbytes)
-        ctl = np.zeros(4, np.uint32)
-        lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ws), 16)
+        ctl = np.zeros(4, np.uint32)  # the last call's control region (one of two in turn)
+        lib.hgk_ctx_decode_ctl.restype = ctypes.c_void_p
+        lib.hgk_ctx_decode_ctl.argtypes = [ctypes.c_void_p]
+        lib.hgk_debug_d2h(ctl.ctypes.data_as(ctypes.c_void_p),
+                          ctypes.c_void_p(lib.hgk_ctx_decode_ctl(eng.ctx)), 16)
         fb = nspec - int(ctl[1])
         codes = Counter(int(c) & 0xFF for c in sb["pad"])
         why = Counter((int(c) >> 8) & 0xFF for c in sb["pad"] if (int(c) >> 8) & 0xFF)
