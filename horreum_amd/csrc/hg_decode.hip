@@ -1225,6 +1225,32 @@ __device__ uint64_t spec_base(const DecodeArgs& a, uint32_t e) {
 #endif
 constexpr uint32_t EMIT_U = HG_EMIT_U;  // scratch spans in flight per thread (emit_spec_range)
 
+// Wave 0 (all 64 lanes): piece record p of lane (< n) into LDS with its
+// record base g0 + the counts before it (one DPP scan; a serial loop of
+// thread 0 over 64 pieces was ~3 us of dependent LDS reads per workgroup,
+// with no span store in flight meanwhile), then the batch's end and whether
+// any piece was hop-walked.
+__device__ __forceinline__ void stage_pieces(SpecPiece* pc, uint64_t* pbase, const SpecPiece& p,
+                                             uint32_t n, uint64_t g0) {
+    const uint32_t lane = threadIdx.x;
+    const uint32_t cnt = lane < n ? p.count : 0u;
+    const uint32_t incl = dpp_sum_incl(cnt);  // n <= SPEC_BP = 64 counts of <= PIECE_RECS
+    const bool hop = lane < n && p.pad == SP_HOP;
+    if (lane < n) {
+        pc[lane] = p;
+        pbase[lane] = g0 + incl - cnt;
+    }
+    const uint32_t tot = __builtin_amdgcn_readlane(incl, 63);
+    const uint64_t hb = __ballot(hop);
+    if (lane == 0) {
+        pbase[SPEC_BP] = g0 + tot;
+        pbase[SPEC_BP + 1] = hb != 0;
+    }
+}
+
+__device__ uint64_t emit_staged(DecodeSmem& s, const DecodeArgs& a, uint32_t q0, uint32_t n,
+                                uint64_t g0);
+
 // Spans of pieces [q0, q0 + n) (n <= SPEC_BP) from their pre-pass summaries
 // (stride arithmetic, or the hop walk's scratch), record base g0.  All
 // threads; returns the record index after the last piece.
@@ -1234,20 +1260,42 @@ __device__ uint64_t emit_spec_range(DecodeSmem& s, const DecodeArgs& a, uint32_t
     SpecPiece* pc = reinterpret_cast<SpecPiece*>(s.data64);  // LDS scratch
     uint64_t* pbase = reinterpret_cast<uint64_t*>(pc + SPEC_BP);
     __syncthreads();
-    if (tid < n) pc[tid] = a.spiece[q0 + tid];
-    __syncthreads();
-    if (tid == 0) {
-        uint64_t g = g0;
-        uint32_t hop = 0;
-        for (uint32_t i = 0; i < n; ++i) {
-            pbase[i] = g;
-            g += pc[i].count;
-            hop |= pc[i].pad == SP_HOP;
-        }
-        pbase[SPEC_BP] = g;
-        pbase[SPEC_BP + 1] = hop;
+    if (tid < 64) {
+        SpecPiece p{};
+        if (tid < n) p = a.spiece[q0 + tid];
+        stage_pieces(pc, pbase, p, n, g0);
     }
     __syncthreads();
+    return emit_staged(s, a, q0, n, g0);
+}
+
+__device__ uint64_t spec_base(const DecodeArgs& a, uint32_t e);
+
+// The same for pre-pass batch e (pieces [q0, q0 + n)) of the resolved prefix
+// at the start of decode_kernel: its record base (spec_base) is loaded by
+// wave 0 together with the piece records (one round of loads, one barrier).
+__device__ uint64_t emit_spec_batch(DecodeSmem& s, const DecodeArgs& a, uint32_t e, uint32_t q0,
+                                    uint32_t n) {
+    const uint32_t tid = threadIdx.x;
+    SpecPiece* pc = reinterpret_cast<SpecPiece*>(s.data64);
+    uint64_t* pbase = reinterpret_cast<uint64_t*>(pc + SPEC_BP);
+    if (tid < 64) {
+        SpecPiece p{};
+        if (tid < n) p = a.spiece[q0 + tid];
+        const uint64_t g0 = spec_base(a, e);
+        stage_pieces(pc, pbase, p, n, g0);
+        if (tid == 0) s.xk = g0;
+    }
+    __syncthreads();
+    return emit_staged(s, a, q0, n, uni(s.xk));
+}
+
+// emit_spec_range after the pieces were staged (all threads).
+__device__ uint64_t emit_staged(DecodeSmem& s, const DecodeArgs& a, uint32_t q0, uint32_t n,
+                                uint64_t g0) {
+    const uint32_t tid = threadIdx.x;
+    const SpecPiece* pc = reinterpret_cast<const SpecPiece*>(s.data64);
+    const uint64_t* pbase = reinterpret_cast<const uint64_t*>(pc + SPEC_BP);
     if (uni(pbase[SPEC_BP + 1])) {
         // Batches with walked pieces (hop / lane-walk spans in scratch): the
         // copies run over the batch's records flattened, EMIT_U per thread
@@ -1492,12 +1540,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         const uint32_t e = blk;
         const uint32_t ep0 = e * a.sbp;
         const uint32_t enp = min(a.sbp, a.npieces - ep0);
-        if (tid < 64) {
-            const uint64_t base = spec_base(a, e);
-            if (tid == 0) s.xk = base;
-        }
-        __syncthreads();
-        const uint64_t g = emit_spec_range(s, a, ep0, enp, uni(s.xk));
+        const uint64_t g = emit_spec_batch(s, a, e, ep0, enp);
         if (tid == 0 && e == a.nspec - 1) {  // the whole file resolved: report it
             hg_decode_result r;
             r.n_records = g;

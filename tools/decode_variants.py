@@ -107,7 +107,16 @@ def main():
         got = spans[: n * 16].cpu().numpy().view(oracle.SPAN_DTYPE)
         ok = kind == wkind and n == wn and np.array_equal(got, want)
         ms = float(np.median(times))
+        # back to back (the bench legs' timing): 20 calls in one event pair
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(20):
+            eng.decode_dev_async(sst, L, spans, cap, res)
+        e1.record()
+        torch.cuda.synchronize()
+        b2b = e0.elapsed_time(e1) / 20
         print(json.dumps({"workload": label, "bytes": L, "records": n, "ms": round(ms, 4),
+                          "b2b_ms": round(b2b, 4),
                           "GBps_alg": round((L + 16 * n) / ms / 1e6, 1), "parity": bool(ok)}),
               flush=True)
         del spans, sst

@@ -3,7 +3,7 @@
 for each decode_spec_kernel, its duration, the gap to the next hg kernel on
 the queue, that kernel's duration, and the span from the first op of the
 call (any op since the previous call's last hg kernel) to the last.
-Usage: trace_gaps.py <kernel_trace.csv> [grid filter]"""
+Usage: trace_gaps.py <kernel_trace.csv> [N: also print the ops around call N]"""
 import csv
 import sys
 
@@ -30,6 +30,13 @@ for i, (s, e, n, g) in enumerate(rows):
 by = {}
 for c in calls:
     by.setdefault(c["grid"], []).append(c)
+if len(sys.argv) > 2:  # print the ops around call N of the first grid
+    n = int(sys.argv[2])
+    idx = [i for i, r in enumerate(rows) if "decode_spec_kernel" in r[2]]
+    i = idx[min(n, len(idx) - 1)]
+    t0 = rows[i][0]
+    for s, e, nm, g in rows[max(0, i - 4):i + 6]:
+        print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:8.1f}  {nm[-40:]} grid {g}")
 for g, cs in by.items():
     cs = cs[2:] or cs  # skip warm-up calls
     med = lambda k: sorted(x[k] for x in cs if x[k] is not None)[len(cs) // 2]
