@@ -39,6 +39,7 @@
 //     spans[G_b + ...], publish INCL.  Guess wrong or a format error: redo the
 //     batch exactly from X_b (pieces re-read), emitting directly.
 #include <stdlib.h>
+#include <string.h>
 
 #include <algorithm>
 
@@ -173,7 +174,8 @@ struct SpecBatch {                // one per pre-pass batch
 // of a lattice table's spans then known from x0 and R) 0.203 -> 0.255 ms,
 // nontemporal stores 0.254 ms (profiles/r5_ab_tail_emit.log); a first form
 // of the latter that handed out span tickets from one counter 0.59 ms.
-// Control words of a decode call (zeroed with the statuses before launch).
+// Control words of a decode call (zero at launch, with the statuses: cleared
+// by the previous call's pre-pass or by a memset, launch_decode).
 struct DecodeCtl {
     uint32_t ticket;              // decode_kernel batch tickets
     uint32_t bad_rev;             // max over unresolved pre-pass batches b of nspec - b
@@ -3536,8 +3538,15 @@ __global__ __launch_bounds__(THREADS, 4) void decode_spec_multi(const DecodeArgs
                                                              const uint32_t* pre, uint32_t ntab) {
     const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
     const DecodeArgs a = tabs[t];
-    spec_body<KPRE>(a, a.sbatch, const_cast<SpecPiece*>(a.spiece),
-                    blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
+    const uint32_t blk = blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]);
+    // the table's region of the next call's control half (hgk_multi_ctl).
+    // Not in compaction mode: there the loop took the kernel from 114 to 122
+    // VGPRs and 223 to 438 us on the cfg 5 leg (its piece staging is that
+    // sensitive, see the round-4 notes); those calls keep the zero kernel.
+    if (!KPRE && a.zero_next)
+        for (uint32_t i = blk * THREADS + threadIdx.x; i < a.zero_next_n16; i += a.nspec * THREADS)
+            a.zero_next[i] = make_uint4(0u, 0u, 0u, 0u);
+    spec_body<KPRE>(a, a.sbatch, const_cast<SpecPiece*>(a.spiece), blk);
 }
 
 __global__ __launch_bounds__(THREADS, 4) void decode_lw_multi(const DecodeArgs* tabs,
@@ -4077,11 +4086,13 @@ MultiStage multi_stage(uint32_t ntab) {
 
 extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t ntab) { return multi_stage(ntab).bytes; }
 
+// mc (nullable): control regions and staging reuse across calls (hgk_multi_ctl).
 extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_tables,
                                        const uint64_t* lens, hg_span* const* d_spans,
                                        const uint64_t* caps, hg_decode_result* d_results,
                                        void* d_ws, const uint64_t* ws_off, void* h_stage,
-                                       void* d_stage, hipStream_t stream, uint32_t kpre_tag) {
+                                       void* d_stage, hipStream_t stream, uint32_t kpre_tag,
+                                       const hgk_multi_ctl* mc) {
     using namespace hgk;
     if (ntab == 0) return HG_OK;
     uint64_t total_pieces = 0;
@@ -4097,10 +4108,19 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
     uint32_t* pre_d = reinterpret_cast<uint32_t*>(hs + ms.pre_d);
     pre_s[0] = pre_d[0] = 0;
     uint64_t nspec_all = 0;
+    bool clean = mc && mc->cur_zero, empty = false;
     for (uint32_t i = 0; i < ntab; ++i) {
         args[i] = make_args(d_tables[i], lens[i], d_spans[i], caps[i], d_results + i,
                             static_cast<char*>(d_ws) + ws_off[i], nullptr, bp, sbp, zb[i], 0,
-                            ~0ull, 0, false, ~0ull, kpre_tag);
+                            ~0ull, 0, false, ~0ull, kpre_tag, mc ? mc->cur + mc->off[i] : nullptr);
+        empty |= lens[i] == 0;
+        if (clean && lens[i] && mc->cur_zero[i] < zb[i]) clean = false;
+        if (mc) {  // the pre-pass of a non-empty table clears its region of `next`
+            const uint64_t z16 = lens[i] && !kpre_tag ? (zb[i] + 15) / 16 : 0;
+            args[i].zero_next = reinterpret_cast<uint4*>(mc->next + mc->off[i]);
+            args[i].zero_next_n16 = (uint32_t)z16;
+            mc->next_zero[i] = z16 * 16;
+        }
         const uint32_t gs = lens[i] ? args[i].nspec : 0;
         nspec_all += gs;
         const uint32_t gd = lens[i] ? (args[i].nbatches > args[i].nspec ? args[i].nbatches
@@ -4115,14 +4135,24 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
         for (uint32_t i = 0; i < ntab; ++i) args[i].hop_wide = hw;
     }
     const uint64_t bytes = hgk_decode_multi_stage_bytes(ntab);
-    if (hipMemcpyAsync(d_stage, h_stage, bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
+    // the device staging already holds these argument bytes (same tables,
+    // buffers and geometry as the call that staged them): no copy
+    const bool same = mc && mc->shadow && mc->shadow_bytes == bytes &&
+                      memcmp(mc->shadow, h_stage, bytes) == 0;
+    if (mc) *mc->copied = same ? 0 : 1;
+    if (!same && hipMemcpyAsync(d_stage, h_stage, bytes, hipMemcpyHostToDevice, stream) != hipSuccess)
+        return HG_HIP_FAIL;
+    if (!same && mc && mc->stage_ev && hipEventRecord(mc->stage_ev, stream) != hipSuccess)
         return HG_HIP_FAIL;
     char* ds = static_cast<char*>(d_stage);
     const DecodeArgs* dargs = reinterpret_cast<const DecodeArgs*>(ds);
     const uint64_t* dzb = reinterpret_cast<const uint64_t*>(ds + ms.zb);
     const uint32_t* dpre_s = reinterpret_cast<const uint32_t*>(ds + ms.pre_s);
     const uint32_t* dpre_d = reinterpret_cast<const uint32_t*>(ds + ms.pre_d);
-    hipLaunchKernelGGL(decode_zero_multi, dim3(ntab), dim3(THREADS), 0, stream, dargs, dzb, ntab);
+    // control regions: zeroed here unless the previous call's pre-pass
+    // cleared them (empty tables' results are written here too)
+    if (!clean || empty)
+        hipLaunchKernelGGL(decode_zero_multi, dim3(ntab), dim3(THREADS), 0, stream, dargs, dzb, ntab);
     if (pre_s[ntab]) {
         if (kpre_tag)
             hipLaunchKernelGGL(decode_spec_multi<true>, dim3(pre_s[ntab]), dim3(THREADS), 0, stream,

@@ -7,6 +7,28 @@
 #include "../../include/horreum_gpu.h"
 #include "hg_err.hpp"
 
+// Batched decode (hgk_decode_launch_multi) across calls on one context: the
+// tables' control regions in two halves used in turn (cur / next, table i at
+// off[i] in each), each call's pre-pass clearing next; cur_zero (nullable):
+// bytes of each region of cur known to be zero (no zero kernel when they
+// cover the call's); next_zero (out): bytes cleared per region of next.
+// shadow (nullable): a host copy of what d_stage holds (shadow_bytes): the
+// staging copy is skipped when the call's arguments are the same bytes;
+// *copied (out) says whether it ran; stage_ev (nullable) is recorded right
+// after it, so the host may reuse h_stage once the copy -- not the whole
+// decode -- has passed.
+struct hgk_multi_ctl {
+    char* cur;
+    char* next;
+    const uint64_t* off;
+    const uint64_t* cur_zero;
+    uint64_t* next_zero;
+    const void* shadow;
+    uint64_t shadow_bytes;
+    int* copied;
+    hipEvent_t stage_ev;
+};
+
 // Compaction extras of a merge (hgk_merge_launch in hg_merge.hip).
 // out non-null: records mode -- the last round writes the live records' bytes
 // to out (cap bytes; rec_off, nullable: each record's output offset) and the

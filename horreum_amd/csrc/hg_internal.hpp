@@ -6,7 +6,10 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/horreum_gpu.h"
+#include "hg_device.hpp"  // hgk_multi_ctl, hgk_merge_records
 #include "hg_err.hpp"
 
 extern "C" uint64_t hgk_decode_ctl_bytes(uint64_t len);
@@ -25,7 +28,8 @@ extern "C" uint64_t hgk_decode_workspace_bytes(uint64_t);
 extern "C" uint64_t hgk_decode_multi_stage_bytes(uint32_t);
 extern "C" int hgk_decode_launch_multi(uint32_t, const uint8_t* const*, const uint64_t*,
                                        hg_span* const*, const uint64_t*, hg_decode_result*, void*,
-                                       const uint64_t*, void*, void*, hipStream_t, uint32_t);
+                                       const uint64_t*, void*, void*, hipStream_t, uint32_t,
+                                       const hgk_multi_ctl* mc);
 extern "C" int hgk_encode_launch(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
                                  uint64_t*, uint32_t, hg_block*, hg_encode_result*,
                                  unsigned long long*, hipStream_t);
@@ -60,7 +64,6 @@ extern "C" int hgk_decode_entries_launch(const void* d_stage, uint32_t ntab, uin
 extern "C" uint32_t hgk_decode_multi_geometry(const void* h_stage, uint32_t ntab);
 extern "C" uint64_t hgk_merge_workspace_bytes(uint32_t, uint64_t);
 extern "C" uint64_t hgk_merge_staging_bytes(uint32_t);
-#include "hg_device.hpp"  // hgk_merge_records
 extern "C" int hgk_merge_launch(const uint8_t*, uint64_t, uint32_t, const uint64_t*,
                                 const hg_span* const*, const uint64_t*, hg_pair*, uint64_t,
                                 hg_merge_result*, void*, void*, hipStream_t, int defer,
@@ -125,6 +128,13 @@ struct hg_ctx {
     // batched decode in one launch: all tables' workspaces, argument staging
     hgi::DevBuf bws, bstage_d;
     hgi::PinBuf bstage;
+    // its control regions in two halves used in turn (hgk_multi_ctl): per half
+    // the region offsets of the call that cleared it and the bytes cleared
+    hgi::DevBuf bctl;
+    int bctl_cur = 0;
+    std::vector<uint64_t> bctl_off[2], bctl_zero[2];
+    // what bstage_d holds (a host copy of the last staged arguments)
+    std::vector<uint8_t> bstage_shadow;
     hipEvent_t bstage_ev = nullptr;
     bool bstage_busy = false;
     // multi-context driver (hg_multi.hip): decode results, gathered offsets

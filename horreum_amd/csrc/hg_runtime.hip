@@ -242,7 +242,7 @@ int hg_ctx_destroy(hg_ctx* c) {
     if (!c) return HG_ERR_INVALID_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->ws, &c->dctl, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
+    for (DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
                       &c->bws, &c->bstage_d, &c->x_res, &c->x_aux, &c->x_arena, &c->x_spans})
         if (b->p) hipFree(b->p);
@@ -267,7 +267,10 @@ int hg_ctx_trim(hg_ctx* c) {
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return HG_HIP_FAIL;
     c->dctl_clean[0] = c->dctl_clean[1] = 0;
-    for (DevBuf* b : {&c->ws, &c->dctl, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
+    c->bctl_off[0].clear();
+    c->bctl_off[1].clear();
+    c->bstage_shadow.clear();
+    for (DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->bstage_d, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res, &c->bws,
                       &c->x_aux, &c->x_arena, &c->x_spans}) {
         if (b->p) hipFree(b->p);
@@ -411,7 +414,19 @@ static int batch_one_launch(hg_ctx* c, uint32_t ntables, const uint8_t* const* d
         total += (hgk_decode_workspace_bytes(lens[i]) + 255) & ~255ull;
     }
     const uint64_t sb = hgk_decode_multi_stage_bytes(ntables);
+    // the tables' control regions, in each half of c->bctl
+    std::vector<uint64_t> coff(ntables);
+    uint64_t ctot = 0;
+    for (uint32_t i = 0; i < ntables; ++i) {
+        coff[i] = ctot;
+        ctot += (hgk_decode_ctl_bytes(lens[i]) + 255) & ~255ull;
+    }
+    if (c->bctl.bytes < 2 * ctot) {  // a new allocation holds nothing known to be zero
+        for (int h = 0; h < 2; ++h) c->bctl_off[h].clear();
+    }
+    if (c->bstage_d.bytes < sb) c->bstage_shadow.clear();
     int r = ensure(c, c->bws, total ? total : 256);
+    if (r == HG_OK) r = ensure(c, c->bctl, 2 * (ctot ? ctot : 256));
     if (r == HG_OK) r = ensure(c, c->bstage_d, sb);
     if (r == HG_OK && !c->bstage_ev &&
         hipEventCreateWithFlags(&c->bstage_ev, hipEventDisableTiming) != hipSuccess)
@@ -420,12 +435,42 @@ static int batch_one_launch(hg_ctx* c, uint32_t ntables, const uint8_t* const* d
     if (r == HG_OK && c->bstage_busy && hipEventSynchronize(c->bstage_ev) != hipSuccess)
         r = HG_HIP_FAIL;
     if (r == HG_OK && ensure_pin(c->bstage, sb) != HG_OK) r = HG_HIP_FAIL;
+    const uint64_t half = c->bctl.bytes / 2 & ~(uint64_t)255;
+    const int cur = c->bctl_cur;
+    char* base = static_cast<char*>(c->bctl.p);
+    std::vector<uint64_t> next_zero(ntables, 0);
+    int copied = 1;
+    const hgk_multi_ctl mc{base + cur * half,
+                           base + (1 - cur) * half,
+                           coff.data(),
+                           c->bctl_off[cur] == coff ? c->bctl_zero[cur].data() : nullptr,
+                           next_zero.data(),
+                           c->bstage_shadow.empty() ? nullptr : c->bstage_shadow.data(),
+                           c->bstage_shadow.size(),
+                           &copied,
+                           c->bstage_ev};
     if (r == HG_OK)
         r = hgk_decode_launch_multi(ntables, d_tables, lens, d_spans, caps, d_results, c->bws.p,
-                                    off.data(), c->bstage.p, c->bstage_d.p, c->stream, kpre_tag);
+                                    off.data(), c->bstage.p, c->bstage_d.p, c->stream, kpre_tag,
+                                    &mc);
+    // this call dirtied its half; the other is clear where its pre-pass ran
+    c->bctl_off[cur].clear();
+    if (r == HG_OK) {
+        c->bctl_off[1 - cur] = coff;
+        c->bctl_zero[1 - cur] = std::move(next_zero);
+        if (copied) {
+            const uint8_t* hs = static_cast<const uint8_t*>(c->bstage.p);
+            c->bstage_shadow.assign(hs, hs + sb);
+        }
+    } else {
+        c->bctl_off[1 - cur].clear();
+        c->bstage_shadow.clear();
+    }
+    c->bctl_cur = 1 - cur;
     if (r != HG_OK) return r;
-    if (hipEventRecord(c->bstage_ev, c->stream) != hipSuccess) return HG_HIP_FAIL;
-    c->bstage_busy = true;
+    // bstage_ev was recorded behind the argument copy (if one ran): the next
+    // call's host staging waits for that copy only, not for this decode
+    c->bstage_busy = copied != 0;
     if (ws_off) *ws_off = std::move(off);
     return HG_OK;
 }
