@@ -106,8 +106,7 @@ struct DecodeArgs {
     uint64_t stop;               // records START in [entry, stop) (== len for a whole table)
     uint64_t entry;              // exact start of the first record (0 for a whole table)
     uint64_t obase;              // added to every span offset written to `spans`
-    uint32_t range;              // bit 0: a range decode (the result's err_offset on success =
-                                 // exit); bit 1: pre-pass batch statuses on (pst_of, lw_emit)
+    uint32_t range;              // a range decode: the result's err_offset on success = exit
     hg_span* spans;
     uint64_t cap;
     hg_decode_result* result;
@@ -1201,20 +1200,6 @@ __device__ int32_t piece_path(DecodeSmem& s, const DecodeArgs& a, uint32_t p, ui
 // workgroups around it (measured: 205 -> 755 us for the pre-pass).  Offsets
 // are < 2^40 (HG_ERR_TOO_LARGE), so the 48-bit sum is exact.
 constexpr uint64_t LINK_ONE = 1ull << 56, LINK_MASK = (1ull << 48) - 1;
-// Pre-pass batch statuses (DecodeArgs::pst): flag in the top two bits, then
-// the batch's record count (AGG) or the records up to and including it (INCL).
-constexpr unsigned long long PST_AGG = 1ull << 62, PST_INCL = 2ull << 62, PST_BAD = 3ull << 62,
-                             PST_VAL = (1ull << 62) - 1;
-constexpr uint64_t SB_EMITTED = 1ull << 48;  // SpecBatch.pad: the pre-pass wrote the batch's spans
-// The pre-pass batch statuses, or null when the launch turned them off
-// (DecodeArgs::range bit 1): nspec words right after the pair links in use
-// (decode_layout reserves room for the most pre-pass batches in the zeroed
-// control region; links are used below nspec only).
-__device__ __forceinline__ unsigned long long* pst_of(const DecodeArgs& a) {
-    return (a.range & 2u) ? reinterpret_cast<unsigned long long*>(
-                                (reinterpret_cast<uintptr_t>(a.link + a.nspec) + 255) & ~(uintptr_t)255)
-                          : nullptr;
-}
 __device__ __forceinline__ void mark_bad(DecodeCtl* c, uint32_t nspec, uint32_t j) {
     atomicMax(&c->bad_rev, nspec - j);
 }
@@ -1291,7 +1276,6 @@ __device__ uint64_t spec_base(const DecodeArgs& a, uint32_t e);
 // The same for pre-pass batch e (pieces [q0, q0 + n)) of the resolved prefix
 // at the start of decode_kernel: its record base (spec_base) is loaded by
 // wave 0 together with the piece records (one round of loads, one barrier).
-template <bool LWE>
 __device__ uint64_t emit_spec_batch(DecodeSmem& s, const DecodeArgs& a, uint32_t e, uint32_t q0,
                                     uint32_t n) {
     const uint32_t tid = threadIdx.x;
@@ -1302,14 +1286,9 @@ __device__ uint64_t emit_spec_batch(DecodeSmem& s, const DecodeArgs& a, uint32_t
         if (tid < n) p = a.spiece[q0 + tid];
         const uint64_t g0 = spec_base(a, e);
         stage_pieces(pc, pbase, p, n, g0);
-        if (tid == 0) {
-            s.xk = g0;
-            // a lane-walk batch whose pre-pass workgroup wrote its spans (lw_emit)
-            if (LWE && (a.sbatch[e].pad & SB_EMITTED)) pbase[SPEC_BP + 1] = 2;
-        }
+        if (tid == 0) s.xk = g0;
     }
     __syncthreads();
-    if (LWE && uni(pbase[SPEC_BP + 1]) == 2) return uni(pbase[SPEC_BP]);
     return emit_staged(s, a, q0, n, uni(s.xk));
 }
 
@@ -1543,10 +1522,7 @@ __device__ __noinline__ uint32_t splice_repair(SpliceArgs a, uint4* ebuf, uint32
     return count_e - before + E;
 }
 
-// LWE: the single-table kernel, where pre-pass workgroups may have written a
-// lane-walk batch's spans (lw_emit; decode_multi has it off: the check took
-// that kernel from 116 VGPRs to 128 with 32 spilled).
-template <bool DIAG, bool LWE = true>
+template <bool DIAG>
 __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
     __shared__ DecodeSmem s;
     const uint32_t tid = threadIdx.x;
@@ -1566,13 +1542,13 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         const uint32_t e = blk;
         const uint32_t ep0 = e * a.sbp;
         const uint32_t enp = min(a.sbp, a.npieces - ep0);
-        const uint64_t g = emit_spec_batch<LWE>(s, a, e, ep0, enp);
+        const uint64_t g = emit_spec_batch(s, a, e, ep0, enp);
         if (tid == 0 && e == a.nspec - 1) {  // the whole file resolved: report it
             hg_decode_result r;
             r.n_records = g;
             r.kind = HG_OK;
             r.reserved = 0;
-            r.err_offset = (a.range & 1u) ? a.obase + a.sbatch[e].exit : 0;
+            r.err_offset = a.range ? a.obase + a.sbatch[e].exit : 0;
             *a.result = r;
         }
     }
@@ -1681,7 +1657,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
                         r.n_records = gk0 + ptot;
                         r.kind = HG_OK;
                         r.reserved = 0;
-                        r.err_offset = (a.range & 1u) ? a.obase + pex : 0;
+                        r.err_offset = a.range ? a.obase + pex : 0;
                         *a.result = r;
                     }
                 }
@@ -1916,7 +1892,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         r.n_records = gk + total;
         r.kind = kind;
         r.reserved = 0;
-        r.err_offset = kind != HG_OK ? a.obase + errpos : ((a.range & 1u) ? a.obase + x : 0);
+        r.err_offset = kind != HG_OK ? a.obase + errpos : (a.range ? a.obase + x : 0);
         *a.result = r;
     }
 }
@@ -3182,108 +3158,6 @@ __device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const Decod
     return ok;
 }
 
-#ifndef HG_LW_EMIT
-#define HG_LW_EMIT 1  // 0: lane-walk batches leave their spans to decode_kernel (A/B)
-#endif
-constexpr uint32_t PST_SPIN_MAX = 1u << 16;  // idle polls (s_sleep 2 each) before giving up
-
-// Wave 0 (all 64 lanes): the records before pre-pass batch b, if batches
-// [0, b) are resolved and each entered at its predecessor's exit up to b
-// (their statuses and the pair links), else ~0.  A decoupled look-back:
-// 64 predecessors per poll, summing AGG counts back to the nearest INCL
-// (batch -1 reads as INCL 0; batch 0's own entry check is in its flag).
-__device__ uint64_t pst_lookback(const DecodeArgs& a, uint32_t b) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const unsigned long long* const pst = pst_of(a);
-    uint64_t acc = 0;
-    int64_t top = (int64_t)b - 1;
-    uint32_t idle = 0;
-    while (true) {
-        const int64_t j = top - (int64_t)lane;
-        unsigned long long w = PST_INCL, lk = 2 * LINK_ONE;
-        if (j >= 0) {
-            w = ld_agent(&pst[j]);
-            lk = ld_agent(&a.link[j + 1]);  // between j and j + 1
-        }
-        const uint32_t f = (uint32_t)(w >> 62);
-        const bool ready = f != 0 && (lk >> 56) >= 2;
-        const uint64_t nr = __ballot(!ready);
-        const uint64_t bm = __ballot(ready && (f == 3 || (lk & LINK_MASK) != 0));
-        const uint64_t im = __ballot(ready && f == 2);
-        const uint32_t fnr = nr ? (uint32_t)__ffsll((long long)nr) - 1 : 64u;
-        const uint32_t fi = im ? (uint32_t)__ffsll((long long)im) - 1 : 64u;
-        const uint32_t lim = fi < fnr ? fi + 1 : fnr;  // lanes [0, lim) are usable
-        const uint64_t lm = lim >= 64 ? ~0ull : ((1ull << lim) - 1);
-        if (bm & lm) return ~0ull;  // an unresolved or unlinked batch on the way
-        if (lim == 0) {
-            if (++idle > PST_SPIN_MAX) return ~0ull;
-            __builtin_amdgcn_s_sleep(2);
-            continue;
-        }
-        acc += wave_sum<uint64_t>(lane < lim ? (uint64_t)(w & PST_VAL) : 0ull);
-        if (fi < fnr) return acc;
-        top -= lim;
-        idle = 0;
-    }
-}
-
-// A resolved lane-walk batch b (pieces [p0, p0 + np), `total` records, its
-// AGG status published) writes its own final spans: look-back for its
-// record base, INCL published at once, then its pieces' scratch spans copied
-// to spans[base ...] (EMIT_U per thread in flight), and the batch marked so
-// decode_kernel skips it.  The 64 MB of span copies of small records then
-// run in the pre-pass tail next to other batches' lane walks (compute-bound)
-// instead of in a separate pass after them.  All threads.
-__device__ void lw_emit(SpecSmem& s, const DecodeArgs& a, SpecBatch* sb, uint32_t b, uint32_t p0,
-                        uint32_t np, uint64_t total) {
-    const uint32_t tid = threadIdx.x;
-    uint32_t* const pbase = reinterpret_cast<uint32_t*>(s.data64);  // batch-local record bases
-    uint64_t* const gb = reinterpret_cast<uint64_t*>(s.data64) + SPEC_BP;
-    __syncthreads();  // lw_batch's chunk buffers (data64) are free
-    if (tid < 64) {
-        const uint64_t base = pst_lookback(a, b);
-        if (tid == 0) {
-            if (base != ~0ull) st_agent(&pst_of(a)[b], PST_INCL | (base + total));
-            gb[0] = base;
-        }
-        const uint32_t q = (np + NW - 1) / NW;
-        const uint32_t cnt = tid < np ? s.lw_pc[tid / q][tid % q] : 0u;
-        const uint32_t incl = dpp_sum_incl(cnt);
-        if (tid < np) pbase[tid] = incl - cnt;
-        if (tid == 0) pbase[SPEC_BP] = __builtin_amdgcn_readlane(incl, 63);
-    }
-    __syncthreads();
-    const uint64_t base = uni(gb[0]);
-    if (base == ~0ull || uni(pbase[SPEC_BP]) != total) return;  // left to decode_kernel
-    for (uint64_t j0 = 0; j0 < total; j0 += (uint64_t)THREADS * EMIT_U) {
-        uint4 v[EMIT_U];
-#pragma unroll
-        for (uint32_t u = 0; u < EMIT_U; ++u) {
-            const uint32_t j = (uint32_t)min(j0 + u * THREADS + tid, total - 1);
-            uint32_t lo = 0, hi = np;  // the piece holding record j: last pbase <= j
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (pbase[mid] <= j) lo = mid;
-                else hi = mid;
-            }
-            v[u] = *reinterpret_cast<const uint4*>(a.scratch + (size_t)(p0 + lo) * MAX_REC_PIECE +
-                                                   (j - pbase[lo]));
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < EMIT_U; ++u) {
-            const uint64_t j = j0 + u * THREADS + tid;
-            const uint64_t gp = base + j;
-            if (j >= total || gp >= a.cap) continue;
-            const uint64_t off = (((uint64_t)v[u].y << 32) | v[u].x) + a.obase;
-            v[u].x = (uint32_t)off;
-            v[u].y = (uint32_t)(off >> 32);
-            *reinterpret_cast<uint4*>(a.spans + gp) = v[u];
-        }
-    }
-    __syncthreads();
-    if (tid == 0) sb[b].pad |= SB_EMITTED;
-}
-
 // Stride check of one staged piece without a barrier: the run's geometry
 // (entry, R, count) follows from the uniform header at X alone, so the exit
 // is known at once; the per-lane compares only decide whether the batch is
@@ -3322,9 +3196,6 @@ __device__ __forceinline__ bool stride_geom(const uint8_t* data, uint64_t base, 
 
 // Thread 0: publish batch b (read by decode_kernel after the kernel boundary),
 // count its records per group, then settle the two links it is part of.
-// PST: also its pre-pass status (pst_of; not in compaction mode, whose
-// pre-pass kernel went 114 -> 122 VGPRs with it).
-template <bool PST = true>
 __device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb, uint32_t b,
                                              uint64_t X0, uint64_t X, uint64_t total, bool ok,
                                              uint32_t code) {
@@ -3339,8 +3210,6 @@ __device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb,
     if (!ok || (b == 0 && X0 != a.entry)) mark_bad(a.ctl, a.nspec, b);
     if (b > 0) link_arrive(a, b, 0 - X0);
     if (b + 1 < a.nspec) link_arrive(a, b + 1, X);
-    if (PST && (a.range & 2u))
-        st_agent(&pst_of(a)[b], (!ok || (b == 0 && X0 != a.entry)) ? PST_BAD : (PST_AGG | total));
 }
 
 // KPRE (compaction mode, a.kpre_tag != 0): stride pieces also leave their
@@ -3560,8 +3429,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     if (HG_LW && !ok && hop && __builtin_amdgcn_readfirstlane(s.hcode) == SB_HOP_SMALL) {
         uint32_t why = 0;
         const bool lok = lw_batch(s, spec_alt, a, p0, np, sp, X0, X, total, why);
-        if (tid == 0) spec_publish<!KPRE>(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
-        if (!KPRE && HG_LW_EMIT && lok && (a.range & 2u) && total) lw_emit(s, a, sb, b, p0, np, total);
+        if (tid == 0) spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
         return;
     }
 #endif
@@ -3577,7 +3445,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             o.pad = SB_HOP_SMALL;
             sb[b] = o;
         } else {
-            spec_publish<!KPRE>(a, sb, b, X0, X, total, ok, code);
+            spec_publish(a, sb, b, X0, X, total, ok, code);
         }
     }
 }
@@ -3695,7 +3563,7 @@ __global__ __launch_bounds__(THREADS, HG_DEC_WAVES) void decode_multi(const Deco
                                                            const uint32_t* pre, uint32_t ntab) {
     const uint32_t t = __builtin_amdgcn_readfirstlane(find_table(pre, ntab, blockIdx.x));
     const DecodeArgs a = tabs[t];
-    decode_body<false, false>(a, blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
+    decode_body<false>(a, blockIdx.x - __builtin_amdgcn_readfirstlane(pre[t]));
 }
 
 // ---- compaction mode: merge entries ------------------------------------------------
@@ -3872,20 +3740,19 @@ __global__ __launch_bounds__(THREADS) void decode_entries_multi(const DecodeArgs
 namespace {
 struct DecodeLayout {
     uint64_t npieces, nbatches, status_words, scratch_off, nspec, sbatch_off, spiece_off, bytes;
-    uint64_t gsum_off, link_off, pst_off, status_off, ptag_off;
+    uint64_t gsum_off, link_off, status_off, ptag_off;
 };
 DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
     DecodeLayout l;
     l.npieces = (len + PIECE - 1) / PIECE;
     l.nbatches = (l.npieces + BATCH_MIN - 1) / BATCH_MIN;  // most batches any launch uses
-    // [DecodeCtl | group sums | pair links | pre-pass statuses | statuses] are zeroed per call
+    // [DecodeCtl | group sums | pair links | statuses] are zeroed per call
     // (up to the statuses in use), then the scratch and pre-pass records.
     l.nspec = (l.npieces + SPEC_BP_MIN - 1) / SPEC_BP_MIN;  // most pre-pass batches
     l.gsum_off = sizeof(DecodeCtl);
     l.link_off = l.gsum_off + ((l.nspec + SPEC_GROUP - 1) / SPEC_GROUP) * 8;
-    l.pst_off = (l.link_off + l.nspec * 8 + 255) & ~255ull;  // pre-pass batch statuses
-    l.status_off = (l.pst_off + l.nspec * 8 + 255) & ~255ull;
+    l.status_off = (l.link_off + l.nspec * 8 + 255) & ~255ull;
     l.status_words = 2 * l.nbatches;
     l.scratch_off = (l.status_off + l.status_words * 8 + 255) & ~255ull;
     l.sbatch_off = l.scratch_off + l.npieces * MAX_REC_PIECE * sizeof(hg_span);
@@ -4018,7 +3885,7 @@ hgk::DecodeArgs make_args(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, 
     a.stop = stop;
     a.entry = entry - begin;
     a.obase = begin;
-    a.range = (range ? 1u : 0u) | 2u;  // the launchers clear bit 1 where lw_emit may not wait
+    a.range = range ? 1u : 0u;
     a.spans = d_spans;
     a.cap = cap;
     a.result = d_result;
@@ -4099,9 +3966,6 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
                              zero_bytes, begin, stop, entry, range, rlen, 0u,
                              ctl ? ctl->cur : nullptr);
     a.hop_wide = hop_wide_cand(a.nspec, resident_workgroups(decode_spec_kernel, 3));
-    // lane-walk batches may wait for their predecessors (lw_emit): only while
-    // every pre-pass workgroup is resident at once
-    if (a.nspec > resident_workgroups(decode_spec_kernel, 3)) a.range &= ~2u;
     if (!ctl || ctl->cur_clean < zero_bytes) {
         if (hipMemsetAsync(ctl ? ctl->cur : d_ws, 0, zero_bytes, stream) != hipSuccess)
             return HG_HIP_FAIL;
@@ -4269,8 +4133,6 @@ extern "C" int hgk_decode_launch_multi(uint32_t ntab, const uint8_t* const* d_ta
         const uint32_t hw = hop_wide_cand(nspec_all, kpre_tag ? resident_workgroups(decode_spec_multi<true>, 4)
                                                              : resident_workgroups(decode_spec_multi<false>, 5));
         for (uint32_t i = 0; i < ntab; ++i) args[i].hop_wide = hw;
-        // no lw_emit in batched decodes (decode_multi does not check for it)
-        for (uint32_t i = 0; i < ntab; ++i) args[i].range &= ~2u;
     }
     const uint64_t bytes = hgk_decode_multi_stage_bytes(ntab);
     // the device staging already holds these argument bytes (same tables,
