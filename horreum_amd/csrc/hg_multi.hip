@@ -236,32 +236,98 @@ __device__ int dkey_cmp(const uint8_t* a, uint32_t al, const uint8_t* b, uint32_
     return al < bl ? -1 : (al > bl ? 1 : 0);
 }
 
-// For splitter key s: the first record with key >= s (lower bound), its byte
-// offset (the table length past the end), and whether the two records around
-// the cut are strictly increasing (a cut inside a run of equal or unordered
-// keys cannot be merged slice by slice).
-__global__ void split_points_kernel(const uint8_t* table, uint64_t len, const hg_span* spans,
-                                    uint64_t n, const uint8_t* keys, const uint64_t* koff,
-                                    const uint32_t* klen, uint32_t nsplit, uint64_t* out) {
-    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= nsplit) return;
+// A key's first 16 bytes as two big-endian words (zero past klen): two
+// unaligned 8-byte reads for keys of 16 bytes or more (no byte loop of
+// dependent reads), the key's own bytes otherwise.
+__device__ __forceinline__ void key_prefix16(const uint8_t* k, uint32_t kl, uint64_t& p0,
+                                             uint64_t& p1) {
+    uint64_t lo = 0, hi = 0;
+    if (kl >= 16) {
+        lo = *reinterpret_cast<const uint64_t*>(k);
+        hi = *reinterpret_cast<const uint64_t*>(k + 8);
+    } else {
+        for (uint32_t i = 0; i < kl; ++i) {
+            const uint64_t b = k[i];
+            if (i < 8) lo |= b << (8 * i);
+            else hi |= b << (8 * (i - 8));
+        }
+    }
+    p0 = __builtin_bswap64(lo);
+    p1 = __builtin_bswap64(hi);
+}
+
+// Vec<u8> Ord of a table key against splitter s (prefix words sp0 / sp1):
+// the prefixes decide unless they are equal; then both keys' bytes from 16 on.
+__device__ __forceinline__ int split_cmp(const uint8_t* k, uint32_t kl, uint64_t p0, uint64_t p1,
+                                         const uint8_t* sk, uint32_t sl, uint64_t sp0,
+                                         uint64_t sp1) {
+    if (p0 != sp0) return p0 < sp0 ? -1 : 1;
+    if (p1 != sp1) return p1 < sp1 ? -1 : 1;
+    if (kl <= 16 || sl <= 16) return kl < sl ? -1 : (kl > sl ? 1 : 0);
+    return dkey_cmp(k + 16, kl - 16, sk + 16, sl - 16);
+}
+
+struct SplitTab {  // one table of a context's cut search
+    const uint8_t* table;
+    const hg_span* spans;
+    uint64_t len, n;
+};
+
+// For splitter s of table t (one wave per pair, grid = tables x splitters):
+// the first record with key >= s (lower bound), its byte offset (the table
+// length past the end), and whether the two records around the cut are
+// strictly increasing (a cut inside a run of equal or unordered keys cannot
+// be merged slice by slice).  A 64-ary search: each step the 64 lanes probe
+// 64 evenly spaced records at once (about four dependent steps for a million
+// records, against ~20 for a binary search, each step one span read and one
+// key read).  On sorted input this is the exact lower bound; on unsorted input
+// it is some index, and the ok flag or the slice merges find the disorder.
+__global__ __launch_bounds__(256) void split_points_kernel(const SplitTab* tabs, uint32_t ntab,
+                                                           const uint8_t* keys,
+                                                           const uint64_t* koff,
+                                                           const uint32_t* klen,
+                                                           const uint64_t* kpre, uint32_t nsplit,
+                                                           uint64_t* out) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (w >= ntab * nsplit) return;
+    const uint32_t t = w / nsplit, s = w % nsplit;
+    const SplitTab tb = tabs[t];
     const uint8_t* key = keys + koff[s];
     const uint32_t kl = klen[s];
-    uint64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const uint64_t mid = lo + (hi - lo) / 2;
-        const hg_span sp = spans[mid];
-        if (dkey_cmp(table + sp.off + 16, sp.klen, key, kl) < 0) lo = mid + 1;
-        else hi = mid;
+    const uint64_t sp0 = kpre[2 * s], sp1 = kpre[2 * s + 1];
+    auto less = [&](uint64_t r) -> bool {  // key of record r < splitter
+        const hg_span sp = tb.spans[r];
+        uint64_t p0, p1;
+        key_prefix16(tb.table + sp.off + 16, sp.klen, p0, p1);
+        return split_cmp(tb.table + sp.off + 16, sp.klen, p0, p1, key, kl, sp0, sp1) < 0;
+    };
+    uint64_t lo = 0, hi = tb.n;  // the answer lies in [lo, hi]
+    while (hi - lo > 64) {
+        const uint64_t span = hi - lo;
+        const uint64_t pr = lo + span * (lane + 1) / 65;  // strictly increasing, in [lo, hi)
+        const uint64_t m = __ballot(less(pr));
+        const uint32_t c = (uint32_t)__popcll(m);
+        const uint64_t nlo = c ? lo + span * c / 65 + 1 : lo;
+        const uint64_t nhi = c < 64 ? lo + span * (c + 1) / 65 : hi;
+        lo = nlo;
+        hi = nhi;
     }
+    const uint64_t pr = lo + lane;
+    lo += (uint64_t)__popcll(__ballot(pr < hi && less(pr)));
+    if (lane != 0) return;
     uint64_t ok = 1;
-    if (lo > 0 && lo < n) {
-        const hg_span a = spans[lo - 1], b = spans[lo];
-        ok = dkey_cmp(table + a.off + 16, a.klen, table + b.off + 16, b.klen) < 0;
+    if (lo > 0 && lo < tb.n) {
+        const hg_span a = tb.spans[lo - 1], b = tb.spans[lo];
+        uint64_t a0, a1, b0, b1;
+        key_prefix16(tb.table + a.off + 16, a.klen, a0, a1);
+        key_prefix16(tb.table + b.off + 16, b.klen, b0, b1);
+        ok = split_cmp(tb.table + a.off + 16, a.klen, a0, a1, tb.table + b.off + 16, b.klen, b0, b1) < 0;
     }
-    out[3 * s] = lo;
-    out[3 * s + 1] = lo < n ? spans[lo].off : len;
-    out[3 * s + 2] = ok;
+    uint64_t* o = out + 3 * ((size_t)t * nsplit + s);
+    o[0] = lo;
+    o[1] = lo < tb.n ? tb.spans[lo].off : tb.len;
+    o[2] = ok;
 }
 
 int host_key_cmp(const std::vector<uint8_t>& a, const std::vector<uint8_t>& b) {
@@ -535,9 +601,16 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
             if (a.p1 != b.p1) return a.p1 < b.p1;
             return a.klen < b.klen;
         });
-        for (uint32_t g = 1; g < nctx; ++g) {  // the splitter's exact bytes from its owner
+        for (uint32_t g = 1; g < nctx; ++g) {  // the splitter's exact bytes
             const KeyRef& kr = all[all.size() * g / nctx];
-            const uint32_t o = ow.owner[kr.table];
+            if (kr.klen <= 16) {  // the sampled prefix holds the whole key (no round trip)
+                std::vector<uint8_t> k(kr.klen);
+                for (uint32_t i = 0; i < kr.klen; ++i)
+                    k[i] = (uint8_t)((i < 8 ? kr.p0 >> (56 - 8 * i) : kr.p1 >> (56 - 8 * (i - 8))) & 0xFF);
+                keys.push_back(std::move(k));
+                continue;
+            }
+            const uint32_t o = ow.owner[kr.table];  // longer keys: from the table's owner
             hg_ctx* c = ctxs[o];
             if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
             hg_span sp;
@@ -585,31 +658,46 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
             }
         }
         if (!nsplit) return (int)HG_OK;
+        // one stream-ordered upload from a pageable host blob laid out as on
+        // the device: splitter bytes, offsets, lengths, 16-byte big-endian
+        // prefixes, then this context's tables; one launch for all of them
+        const uint32_t nt = (uint32_t)s.ids.size();
         const size_t kb = (kbytes.size() + 255) & ~(size_t)255;
-        const size_t need = kb + 16 * (nsplit + 1) + 256 + 24 * (size_t)(nsplit + 1) * s.ids.size();
-        int rr = ensure(c, c->x_aux, need);
+        const size_t o_ko = kb, o_kl = o_ko + 8 * (nsplit + 1), o_kp = (o_kl + 4 * nsplit + 15) & ~(size_t)15;
+        const size_t o_tb = (o_kp + 16 * (size_t)nsplit + 255) & ~(size_t)255;
+        const size_t o_out = (o_tb + sizeof(SplitTab) * nt + 255) & ~(size_t)255;
+        int rr = ensure(c, c->x_aux, o_out + 24 * (size_t)nsplit * nt);
         if (rr != HG_OK) return rr;
         char* d = static_cast<char*>(c->x_aux.p);
-        uint8_t* dk = reinterpret_cast<uint8_t*>(d);
-        uint64_t* dko = reinterpret_cast<uint64_t*>(d + kb);
-        uint32_t* dkl = reinterpret_cast<uint32_t*>(d + kb + 8 * (nsplit + 1));
-        uint64_t* dout = reinterpret_cast<uint64_t*>(d + kb + 16 * (nsplit + 1) + 256);
-        // stream-ordered uploads from pageable host vectors (the runtime stages them)
-        if ((!kbytes.empty() && hipMemcpyAsync(dk, kbytes.data(), kbytes.size(),
-                                               hipMemcpyHostToDevice, c->stream) != hipSuccess) ||
-            hipMemcpyAsync(dko, kofs.data(), 8 * (nsplit + 1), hipMemcpyHostToDevice, c->stream) !=
-                hipSuccess ||
-            hipMemcpyAsync(dkl, kls.data(), 4 * nsplit, hipMemcpyHostToDevice, c->stream) !=
-                hipSuccess)
-            return (int)HG_HIP_FAIL;
-        for (size_t j = 0; j < s.ids.size(); ++j) {
-            hipLaunchKernelGGL(split_points_kernel, dim3((nsplit + 63) / 64), dim3(64), 0, c->stream,
-                               ow.dptr[s.ids[j]], lens[s.ids[j]],
-                               static_cast<const hg_span*>(c->mspans.p) + s.soff[j],
-                               s.res[j].n_records, (const uint8_t*)dk, (const uint64_t*)dko,
-                               (const uint32_t*)dkl, nsplit, dout + 3 * (size_t)nsplit * j);
-            if ((rr = HG_LAUNCH_STATUS()) != HG_OK) return rr;
+        std::vector<uint8_t> blob(o_out, 0);
+        if (!kbytes.empty()) memcpy(blob.data(), kbytes.data(), kbytes.size());
+        memcpy(blob.data() + o_ko, kofs.data(), 8 * (nsplit + 1));
+        memcpy(blob.data() + o_kl, kls.data(), 4 * (size_t)nsplit);
+        uint64_t* kp = reinterpret_cast<uint64_t*>(blob.data() + o_kp);
+        for (uint32_t q = 0; q < nsplit; ++q) {  // prefix words as split_cmp compares them
+            uint64_t w0 = 0, w1 = 0;
+            for (uint32_t i = 0; i < 16; ++i) {
+                const uint64_t b = i < kls[q] ? kbytes[kofs[q] + i] : 0;
+                if (i < 8) w0 = (w0 << 8) | b;
+                else w1 = (w1 << 8) | b;
+            }
+            kp[2 * q] = w0;
+            kp[2 * q + 1] = w1;
         }
+        SplitTab* tb = reinterpret_cast<SplitTab*>(blob.data() + o_tb);
+        for (uint32_t j = 0; j < nt; ++j)
+            tb[j] = SplitTab{ow.dptr[s.ids[j]], static_cast<const hg_span*>(c->mspans.p) + s.soff[j],
+                             lens[s.ids[j]], s.res[j].n_records};
+        if (hipMemcpyAsync(d, blob.data(), blob.size(), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            return (int)HG_HIP_FAIL;
+        uint64_t* dout = reinterpret_cast<uint64_t*>(d + o_out);
+        const uint32_t waves = nt * nsplit;
+        hipLaunchKernelGGL(split_points_kernel, dim3((waves + 3) / 4), dim3(256), 0, c->stream,
+                           reinterpret_cast<const SplitTab*>(d + o_tb), nt,
+                           reinterpret_cast<const uint8_t*>(d), reinterpret_cast<const uint64_t*>(d + o_ko),
+                           reinterpret_cast<const uint32_t*>(d + o_kl),
+                           reinterpret_cast<const uint64_t*>(d + o_kp), nsplit, dout);
+        if ((rr = HG_LAUNCH_STATUS()) != HG_OK) return rr;
         std::vector<uint64_t> h(3 * (size_t)nsplit * s.ids.size());
         if ((rr = sync_d2h(c, h.data(), dout, 8 * h.size())) != HG_OK) return rr;
         for (size_t j = 0; j < s.ids.size(); ++j) {

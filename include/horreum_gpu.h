@@ -370,7 +370,7 @@ int hg_host_is_pinned(const void* h_ptr);
  * Many tables (SSTableManager::new opening a directory, manager.rs:47-55;
  * BASELINE config 4): table i goes to context i % nctx; each context uploads
  * its tables and decodes them in one batched launch chain per group of tables
- * under a device byte budget (HG_DECODE_GROUP_BYTES, default 40 % of the free
+ * under a device byte budget (knob HG_DECODE_GROUP_BYTES, default 40 % of the free
  * device memory; tables plus span capacity), so a directory larger than HBM
  * opens group by group.  spans of table i
  * to h_spans[i] (capacity caps[i]), n_out[i] records, errs[i] its format
