@@ -214,18 +214,30 @@ __device__ __forceinline__ void key_prefix(const uint8_t* k, uint32_t kl, uint64
     }
 }
 
-__global__ void sample_keys_kernel(const uint8_t* table, const hg_span* spans, uint64_t n,
-                                   uint64_t step, uint32_t tid, KeyRef* out, uint64_t m) {
-    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= m) return;
-    const uint64_t rec = j * step < n ? j * step : n - 1;
-    const hg_span sp = spans[rec];
+// Up to kSampleTabs tables' samples in one launch (by value: no upload);
+// block y = table, m <= blockDim.x samples each.
+constexpr uint32_t kSampleTabs = 32;
+struct SampleArgs {
+    struct Tab {
+        const uint8_t* table;
+        const hg_span* spans;
+        uint64_t n, step, at;
+        uint32_t m, id;
+    } t[kSampleTabs];
+};
+
+__global__ void sample_keys_kernel(SampleArgs sa, KeyRef* out) {
+    const SampleArgs::Tab& tb = sa.t[blockIdx.x];
+    const uint32_t j = threadIdx.x;
+    if (j >= tb.m) return;
+    const uint64_t rec = j * tb.step < tb.n ? j * tb.step : tb.n - 1;
+    const hg_span sp = tb.spans[rec];
     KeyRef r;
-    key_prefix(table + sp.off + 16, sp.klen, r.p0, r.p1);
+    key_prefix(tb.table + sp.off + 16, sp.klen, r.p0, r.p1);
     r.klen = sp.klen;
-    r.table = tid;
+    r.table = tb.id;
     r.rec = rec;
-    out[j] = r;
+    out[tb.at + j] = r;
 }
 
 // Vec<u8> Ord (shorter first on a common prefix).
@@ -576,18 +588,25 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
         if (rr != HG_OK) return rr;
         KeyRef* d = static_cast<KeyRef*>(c->x_aux.p);
         uint64_t at = 0;
+        SampleArgs sa{};
+        uint32_t k = 0;
+        auto launch = [&]() -> int {  // the tables gathered so far, one launch
+            if (!k) return (int)HG_OK;
+            hipLaunchKernelGGL(sample_keys_kernel, dim3(k), dim3(kSamples), 0, c->stream, sa, d);
+            k = 0;
+            return HG_LAUNCH_STATUS();
+        };
         for (size_t j = 0; j < s.ids.size(); ++j) {
             const uint64_t n = s.res[j].n_records;
             if (!n) continue;
             const uint64_t m = std::min<uint64_t>(kSamples, n);
-            const uint64_t step = (n + m - 1) / m;
-            hipLaunchKernelGGL(sample_keys_kernel, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0,
-                               c->stream, ow.dptr[s.ids[j]],
-                               static_cast<const hg_span*>(c->mspans.p) + s.soff[j], n, step,
-                               s.ids[j], d + at, m);
-            if ((rr = HG_LAUNCH_STATUS()) != HG_OK) return rr;
+            sa.t[k++] = SampleArgs::Tab{ow.dptr[s.ids[j]],
+                                        static_cast<const hg_span*>(c->mspans.p) + s.soff[j], n,
+                                        (n + m - 1) / m, at, (uint32_t)m, s.ids[j]};
             at += m;
+            if (k == kSampleTabs && (rr = launch()) != HG_OK) return rr;
         }
+        if ((rr = launch()) != HG_OK) return rr;
         samples[ci].resize(m_tot);
         return sync_d2h(c, samples[ci].data(), d, m_tot * sizeof(KeyRef));
     });
