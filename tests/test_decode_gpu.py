@@ -783,3 +783,42 @@ def test_batch_control_region_reuse(engine):
     run(dc, c)
     run(da, a)
     run(da, a)
+
+
+@pytest.mark.parametrize("where", ["clean", "bad_header_in_tail", "stride_change_in_tail",
+                                   "stride_change_at_tail", "tombstones"])
+def test_stride_batch_tails(engine, where):
+    """A 528 MB fixed-stride table (pre-pass batches of 32+ pieces) with the
+    damage placed in the last pieces of full batches -- the region a tail-task
+    scheme would hand to another workgroup (measured in round 5, not kept):
+    clean, a broken header, a stride change inside the last eight pieces or
+    exactly at their start, and tombstones (vlen 0: other record sizes) there;
+    every result bit-exact vs the oracle."""
+    import ctypes
+    from horreum_amd import synth
+    rec = 132
+    host = synth.fixed_sst(4_000_000, 16, 100, seed=5, device="cpu").numpy().copy()
+    assert_same(engine, host)
+    lay = (ctypes.c_uint64 * 8)()
+    engine.lib.hgk_decode_last_layout(lay)
+    sbp = int(lay[3])
+    assert sbp > 16, sbp  # long batches
+    tails = 8
+    for b in (3, 11, 40):
+        t0 = (b * sbp + sbp - tails) * CHUNK  # first byte of batch b's tail task
+        if where == "clean":
+            continue
+        if where == "bad_header_in_tail":
+            r = (t0 + 3 * CHUNK + rec - 1) // rec * rec
+            host[r + 8:r + 16] = np.frombuffer((1 << 33).to_bytes(8, "little"), np.uint8)
+            break  # one error: the oracle stops there
+        if where == "tombstones":
+            for k in range(5):
+                r = (t0 + k * CHUNK + 7 * rec) // rec * rec
+                host[r + 8:r + 16] = 0  # vlen 0: a 32-byte record, then 100 bytes read as records
+            continue
+        cut = (t0 + (CHUNK * 2 + 50 if where == "stride_change_in_tail" else 0) + rec - 1) // rec * rec
+        suffix = oracle.encode(*corpus.fixed((host.size - cut) // 76, 16, 44, seed=9))[0]
+        host = np.concatenate([host[:cut], suffix])
+        break
+    assert_same(engine, host)
