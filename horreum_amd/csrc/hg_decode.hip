@@ -106,8 +106,7 @@ struct DecodeArgs {
     uint64_t stop;               // records START in [entry, stop) (== len for a whole table)
     uint64_t entry;              // exact start of the first record (0 for a whole table)
     uint64_t obase;              // added to every span offset written to `spans`
-    uint32_t range;              // bit 0: a range decode (the result's err_offset on success =
-                                 // exit); bit 1: the pre-pass's tail tasks on (spec_tails)
+    uint32_t range;              // a range decode: the result's err_offset on success = exit
     hg_span* spans;
     uint64_t cap;
     hg_decode_result* result;
@@ -184,6 +183,7 @@ struct DecodeCtl {
                                   // waits restart their budget whenever it moves
     uint32_t repairs;             // pre-pass batches spliced onto their predecessor's exit
 };
+// (the group sums follow it: 8-byte atomics, which fault when misaligned)
 static_assert(sizeof(DecodeCtl) % 8 == 0, "DecodeCtl keeps the group sums 8-byte aligned");
 constexpr uint32_t SPEC_GROUP = 64;  // pre-pass batches per group sum
 __device__ __forceinline__ uint32_t first_bad(const DecodeCtl* c, uint32_t nspec) {
@@ -1550,7 +1550,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
             r.n_records = g;
             r.kind = HG_OK;
             r.reserved = 0;
-            r.err_offset = (a.range & 1u) ? a.obase + a.sbatch[e].exit : 0;
+            r.err_offset = a.range ? a.obase + a.sbatch[e].exit : 0;
             *a.result = r;
         }
     }
@@ -1659,7 +1659,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
                         r.n_records = gk0 + ptot;
                         r.kind = HG_OK;
                         r.reserved = 0;
-                        r.err_offset = (a.range & 1u) ? a.obase + pex : 0;
+                        r.err_offset = a.range ? a.obase + pex : 0;
                         *a.result = r;
                     }
                 }
@@ -1894,7 +1894,7 @@ __device__ void decode_body(const DecodeArgs& a, uint32_t blk) {
         r.n_records = gk + total;
         r.kind = kind;
         r.reserved = 0;
-        r.err_offset = kind != HG_OK ? a.obase + errpos : ((a.range & 1u) ? a.obase + x : 0);
+        r.err_offset = kind != HG_OK ? a.obase + errpos : (a.range ? a.obase + x : 0);
         *a.result = r;
     }
 }
@@ -2012,9 +2012,6 @@ struct SpecSmem {
     uint32_t lw_pc[NW][SPEC_BP / NW];
     uint32_t lw_prof[8];      // diagnostics (a.sdiag): cycles per lane-walk phase, see LW_STAMP
     uint64_t lw_last;
-    uint32_t task;            // spec_tails: the tail task examined next,
-    uint32_t t_got;           // whether task_claim got it,
-    uint64_t t_l0, t_l1;      // and its batch's lattice words
 };
 
 // Span of the HOP_CHECK records after the (valid) record at p, or 0 if one
@@ -3268,174 +3265,8 @@ __device__ __forceinline__ void raw_barrier() {
     __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// ---- tail tasks: the pre-pass's straggler tail -------------------------------
-// Workgroups stream their batches at rates that differ by 5-15 % (per XCD,
-// not fixed to one; profiles/r4_prepass_timeline.log), so the last one ends
-// ~20 us after the median.  A full batch of a fixed-stride table streams its
-// first sbp - HG_TAILS pieces itself and offers the last HG_TAILS pieces as a
-// TAIL TASK: the lattice (entry x0 and record length R, published by the
-// owner after piece 0) gives the task's exact entry -- the first lattice point
-// in its first piece -- so the task needs nothing else from the owner.
-// Whoever claims the task's state word first (compare-and-swap) decodes it:
-// the owner when it reaches its tail, or a workgroup done with its own batch
-// that finds it open among its partners' (spec_tails).  Nobody ever
-// waits for another workgroup, so this holds with any number of workgroups
-// resident.  Each part adds its records (the task also its exit) into the
-// batch's combine word; the part that completes it publishes the batch
-// (spec_publish).  The owner checks that its exit is the task's entry; a
-// broken run in either part leaves the batch unresolved (decode_kernel's
-// engine decodes it, as any unresolved batch).  decode_spec_kernel only.
-#ifndef HG_TAILS
-#define HG_TAILS 8  // pieces per full pre-pass batch offered as a tail task (0: off)
-#endif
-constexpr uint32_t TAILS = HG_TAILS;
-constexpr unsigned long long LAT_VALID = 1ull << 63, LAT_NOSPLIT = 1ull << 62;
-constexpr unsigned long long CMB_PART = 1ull << 62, CMB_BAD = 1ull << 57, CMB_M40 = (1ull << 40) - 1;
-// Tail words of pre-pass batch b: [0] x0 | LAT_VALID, or LAT_NOSPLIT (the
-// owner decodes the whole batch); [1] R | kl << 34; [2] the combine word
-// (2 bits parts, 2 bits bad parts, 17 bits records, 40 bits the task's exit);
-// [3] the task's state (0 open, 1 claimed).  They follow the pair links in
-// use (decode_layout reserves 4 words for the most pre-pass batches in the
-// zeroed control region).
-__device__ __forceinline__ unsigned long long* tail_of(const DecodeArgs& a, uint32_t b) {
-    return reinterpret_cast<unsigned long long*>(
-               (reinterpret_cast<uintptr_t>(a.link + a.nspec) + 255) & ~(uintptr_t)255) +
-           4 * (size_t)b;
-}
-__device__ __forceinline__ bool split_batch(const DecodeArgs& a, uint32_t np) {
-    return TAILS && (a.range & 2u) && np == a.sbp && np > 2 * TAILS;
-}
-// The first record start of the lattice (x0, R) at or after byte q > x0.
-__device__ __forceinline__ uint64_t lattice_at(uint64_t x0, uint64_t R, uint64_t q) {
-    return x0 + (q - x0 + R - 1) / R * R;
-}
-// Thread 0: add one part of batch b; the part that completes it publishes.
-__device__ __forceinline__ void tail_combine(const DecodeArgs& a, SpecBatch* sb, uint32_t b,
-                                             uint64_t x0, unsigned long long part) {
-    const unsigned long long full = atomicAdd(&tail_of(a, b)[2], part) + part;
-    if ((full >> 62) != 2) return;
-    spec_publish(a, sb, b, x0, full & CMB_M40, (full >> 40) & 0x1FFFFull, ((full >> 57) & 3) == 0,
-                 SB_STRIDE);
-}
 
-// The tail task of batch t (its lattice x0, R), claimed by this workgroup:
-// its TAILS pieces staged by LDS-DMA two buffers deep like the owner's, each
-// verified as a stride run of the lattice, then the task's part combined.
-// All threads.
-__device__ __forceinline__ void spec_task(SpecSmem& s, const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp,
-                          uint8_t* buf0, uint8_t* buf1, uint32_t t, uint64_t x0, uint64_t R) {
-    const uint32_t tid = threadIdx.x;
-    const uint32_t q0 = t * a.sbp + a.sbp - TAILS;
-    uint64_t X = lattice_at(x0, R, (uint64_t)q0 * PIECE), cnt = 0;
-    int bad = 0;
-    __syncthreads();  // the caller is done with the buffers and s.halo
-    if (tid < TAILS) s.halo[tid] = load16(a, (uint64_t)(q0 + tid + 1) * PIECE);
-    bool dma_cur = spec_dma(a, q0, buf0);
-    for (uint32_t i = 0; i < TAILS; ++i) {
-        const uint32_t p = q0 + i;
-        const uint64_t base = (uint64_t)p * PIECE;
-        const uint32_t clen = piece_clen(a, base);
-        uint8_t* const cur = (i & 1) ? buf1 : buf0;
-        raw_barrier();  // (A)
-        const bool dma_next = i + 1 < TAILS && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
-        lw_wait_vm(dma_next ? GPT : 0);
-        if (!dma_cur) {
-#pragma unroll
-            for (uint32_t q = 0; q < GPT; ++q)
-                *reinterpret_cast<uint4*>(cur + (q * THREADS + tid) * 16) =
-                    load16(a, base + (q * THREADS + tid) * 16);
-        }
-        if (tid < 4)
-            *reinterpret_cast<uint4*>(cur + PIECE + tid * 16) = tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
-        raw_barrier();  // (B)
-        dma_cur = dma_next;
-        PieceSum ps;
-        if (!stride_geom(cur, base, a.len, clen, X, ps, bad) || (ps.kind == PK_STRIDE && ps.R != R)) {
-            bad = 1;
-            break;
-        }
-        if (tid == 0) {
-            SpecPiece o;
-            o.x = ps.x;
-            o.R = ps.R;
-            o.kl = ps.kl;
-            o.vl = ps.vl;
-            o.count = ps.count;
-            o.pad = 0;
-            sp[p] = o;
-        }
-        cnt += ps.count;
-        X = ps.kind == PK_EMPTY ? X : X + (uint64_t)ps.count * ps.R;
-    }
-    lw_wait_vm(0);  // a break leaves the next piece's DMA in flight
-    const bool tbad = __syncthreads_or(bad);
-    if (tid == 0) tail_combine(a, sb, t, x0, CMB_PART | (X & CMB_M40) | (cnt << 40) | (tbad ? CMB_BAD : 0));
-}
-
-// Claim the tail task of batch t if its lattice is published and nobody took
-// it (thread 0; the result and the lattice go to LDS).  No waiting.
-__device__ __forceinline__ bool task_claim(SpecSmem& s, const DecodeArgs& a, uint32_t t) {
-    if (threadIdx.x == 0) {
-        uint32_t got = 0;
-        if (t < a.nspec && split_batch(a, min(a.sbp, a.npieces - t * a.sbp))) {
-            unsigned long long* tw = tail_of(a, t);
-            const unsigned long long l0 = ld_agent(&tw[0]), l1 = ld_agent(&tw[1]);
-            if ((l0 & LAT_VALID) && l1 && ld_agent(&tw[3]) == 0 && atomicCAS(&tw[3], 0ull, 1ull) == 0) {
-                got = 1;
-                s.t_l0 = l0;
-                s.t_l1 = l1;
-            }
-        }
-        s.t_got = got;  // (not s.task: other waves may still be reading it)
-    }
-    __syncthreads();
-    return uni(s.t_got) != 0;
-}
-
-// A workgroup done with its own batch: the tail tasks of its PARTNER_TASKS
-// successors (batches b + 1 ... -- with workgroups dealt round-robin over
-// the XCDs, one on each other XCD), examined by one wave in one round of
-// loads; the first open one whose lattice is published is claimed and
-// decoded, then the partners are examined again; none open: done.  (A global
-// task counter instead made every shape 30-100 % slower: same-address atomics
-// from every XCD serialise.)
-constexpr uint32_t PARTNER_TASKS = 7;
-__device__ __forceinline__ void spec_tails(SpecSmem& s, const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp,
-                           uint8_t* buf0, uint8_t* buf1, uint32_t b) {
-    const uint32_t tid = threadIdx.x;
-    for (uint32_t round = 0; round < 2 * PARTNER_TASKS; ++round) {
-        __syncthreads();  // s.t_* of the previous round, the buffers
-        if (tid < 64) {
-            const uint32_t t = (b + 1 + tid) % a.nspec;
-            bool cand = false;
-            if (tid < PARTNER_TASKS && t != b && split_batch(a, min(a.sbp, a.npieces - t * a.sbp))) {
-                const unsigned long long* tw = tail_of(a, t);
-                cand = (ld_agent(&tw[0]) & LAT_VALID) && ld_agent(&tw[3]) == 0;
-            }
-            const uint64_t m = __ballot(cand);
-            const uint32_t fl = m ? (uint32_t)__ffsll((long long)m) - 1 : 64u;
-            if (tid == (fl < 64 ? fl : 0u)) {
-                uint32_t got = 0;
-                if (fl < 64) {
-                    unsigned long long* tw = tail_of(a, t);
-                    if (atomicCAS(&tw[3], 0ull, 1ull) == 0) {
-                        got = 1;
-                        s.task = t;
-                        s.t_l0 = ld_agent(&tw[0]);
-                        s.t_l1 = ld_agent(&tw[1]);
-                    }
-                }
-                s.t_got = got;
-            }
-        }
-        __syncthreads();
-        if (!uni(s.t_got)) return;
-        spec_task(s, a, sb, sp, buf0, buf1, uni(s.task), uni(s.t_l0) & CMB_M40,
-                  uni(s.t_l1) & ((1ull << 34) - 1));
-    }
-}
-
-template <bool KPRE, bool TAILS_ON = false>
+template <bool KPRE>
 __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uint32_t blk) {
     __shared__ SpecSmem s;
     const uint32_t tid = threadIdx.x;
@@ -3464,12 +3295,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     uint64_t X = 0, X0 = 0, total = 0;
     bool ok = true, hop = false;
     int bad = 0;
-    // tail task (spec_tails): the batch's last TAILS pieces are left to any
-    // workgroup once the lattice is known after piece 0 (F: pieces streamed here)
-    const bool split = TAILS_ON && split_batch(a, np);
-    uint32_t F = np;
-    uint64_t lat_R = 0;
-    bool lat_pub = false;  // the tail words say VALID or NOSPLIT
     constexpr uint32_t KPT = KPRE ? MAX_REC_PIECE / THREADS : 1;  // prefixes per thread
     uint4 pf[KPT];
     uint32_t pf_n = 0, pf_piece = 0;  // the pending prefixes (KPRE)
@@ -3492,7 +3317,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     };
     // Two barriers per piece: (A) the previous piece is done with LDS; stage
     // v and the halo and put the next piece's loads in flight before (B).
-    for (uint32_t i = 0; i < F; ++i) {
+    for (uint32_t i = 0; i < np; ++i) {
         const uint32_t p = p0 + i;
         const uint64_t base = (uint64_t)p * PIECE;
         const uint64_t rem = a.len - base;
@@ -3501,7 +3326,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         uint8_t* const cur = (i & 1) ? buf1 : buf0;
         data = cur;
         raw_barrier();  // (A) every wave is done with the other buffer (piece i - 1)
-        const bool dma_next = i + 1 < F && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
+        const bool dma_next = i + 1 < np && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
         lw_wait_vm(dma_next ? GPT : 0);  // (and every store before the DMA)
         flush_prefixes();
 #ifdef HG_SPEC_TIMELINE
@@ -3566,23 +3391,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             o.pad = 0;
             sp[p] = o;
         }
-        if (split && i == 0) {  // the lattice for the tail task, or the whole batch here
-            const bool lat = ps.kind == PK_STRIDE && ps.kl < (1u << 30);
-            lat_pub = true;
-            if (lat) {
-                F = np - TAILS;
-                lat_R = ps.R;
-            }
-            if (tid == 0) {
-                unsigned long long* tw = tail_of(a, b);
-                if (lat) {
-                    st_agent(&tw[1], ps.R | ((unsigned long long)ps.kl << 34));
-                    st_agent(&tw[0], X0 | LAT_VALID);
-                } else {
-                    st_agent(&tw[0], LAT_NOSPLIT);
-                }
-            }
-        }
         if (KPRE && ps.kind == PK_STRIDE) {  // compaction mode: key prefixes from LDS
             const uint32_t xr = (uint32_t)(X - base), R = (uint32_t)ps.R;
 #pragma unroll
@@ -3609,8 +3417,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
 #if HG_SPEC_GLDS
     lw_wait_vm(0);  // a break leaves the next piece's DMA in flight
 #endif
-    if (split && !lat_pub && tid == 0)  // left at piece 0: no tail task for this batch
-        st_agent(&tail_of(a, b)[0], LAT_NOSPLIT);
     flush_prefixes();
     if (hop) {
         bad = 0;
@@ -3626,7 +3432,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         uint32_t why = 0;
         const bool lok = lw_batch(s, spec_alt, a, p0, np, sp, X0, X, total, why);
         if (tid == 0) spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
-        if (TAILS_ON && (a.range & 2u)) spec_tails(s, a, sb, sp, buf0, buf1, b);
         return;
     }
 #endif
@@ -3641,20 +3446,10 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             o.ok = 0;
             o.pad = SB_HOP_SMALL;
             sb[b] = o;
-        } else if (lat_R) {  // the owner's part of a batch split with its tail task
-            const bool pok = ok && X == lattice_at(X0, lat_R, (uint64_t)(p0 + F) * PIECE);
-            tail_combine(a, sb, b, X0, CMB_PART | ((unsigned long long)total << 40) | (pok ? 0ull : CMB_BAD));
         } else {
             spec_publish(a, sb, b, X0, X, total, ok, code);
         }
     }
-#if HG_SPEC_GLDS
-    if (TAILS_ON && (a.range & 2u)) {
-        // its own task first, unless another workgroup took it
-        if (uni(lat_R) && task_claim(s, a, b)) spec_task(s, a, sb, sp, buf0, buf1, b, X0, lat_R);
-        spec_tails(s, a, sb, sp, buf0, buf1, b);
-    }
-#endif
 }
 
 // The lane-walk mode as its own launch between the pre-pass and decode_kernel:
@@ -3694,9 +3489,9 @@ __global__ __launch_bounds__(THREADS, 4) void decode_spec_kernel(DecodeArgs a, S
              i += gridDim.x * THREADS)
             a.zero_next[i] = make_uint4(0u, 0u, 0u, 0u);
 #ifdef HG_SPEC_SWAP_PAIRS  // diagnostics: workgroup b takes batch b ^ 1 (XCD vs address)
-    spec_body<false, true>(a, sb, sp, (blockIdx.x ^ 1u) < a.nspec ? blockIdx.x ^ 1u : blockIdx.x);
+    spec_body<false>(a, sb, sp, (blockIdx.x ^ 1u) < a.nspec ? blockIdx.x ^ 1u : blockIdx.x);
 #else
-    spec_body<false, true>(a, sb, sp, blockIdx.x);
+    spec_body<false>(a, sb, sp, blockIdx.x);
 #endif
 }
 
@@ -3947,20 +3742,19 @@ __global__ __launch_bounds__(THREADS) void decode_entries_multi(const DecodeArgs
 namespace {
 struct DecodeLayout {
     uint64_t npieces, nbatches, status_words, scratch_off, nspec, sbatch_off, spiece_off, bytes;
-    uint64_t gsum_off, link_off, tail_off, status_off, ptag_off;
+    uint64_t gsum_off, link_off, status_off, ptag_off;
 };
 DecodeLayout decode_layout(uint64_t len) {
     using namespace hgk;
     DecodeLayout l;
     l.npieces = (len + PIECE - 1) / PIECE;
     l.nbatches = (l.npieces + BATCH_MIN - 1) / BATCH_MIN;  // most batches any launch uses
-    // [DecodeCtl | group sums | pair links | tail words | statuses] are zeroed per call
+    // [DecodeCtl | group sums | pair links | statuses] are zeroed per call
     // (up to the statuses in use), then the scratch and pre-pass records.
     l.nspec = (l.npieces + SPEC_BP_MIN - 1) / SPEC_BP_MIN;  // most pre-pass batches
-    l.gsum_off = (sizeof(DecodeCtl) + 63) & ~63ull;
+    l.gsum_off = sizeof(DecodeCtl);
     l.link_off = l.gsum_off + ((l.nspec + SPEC_GROUP - 1) / SPEC_GROUP) * 8;
-    l.tail_off = (l.link_off + l.nspec * 8 + 255) & ~255ull;  // 4 words per pre-pass batch (tail_of)
-    l.status_off = (l.tail_off + 4 * l.nspec * 8 + 255) & ~255ull;
+    l.status_off = (l.link_off + l.nspec * 8 + 255) & ~255ull;
     l.status_words = 2 * l.nbatches;
     l.scratch_off = (l.status_off + l.status_words * 8 + 255) & ~255ull;
     l.sbatch_off = l.scratch_off + l.npieces * MAX_REC_PIECE * sizeof(hg_span);
@@ -4174,8 +3968,6 @@ int launch_decode(const uint8_t* d_sst, uint64_t len, hg_span* d_spans, uint64_t
                              zero_bytes, begin, stop, entry, range, rlen, 0u,
                              ctl ? ctl->cur : nullptr);
     a.hop_wide = hop_wide_cand(a.nspec, resident_workgroups(decode_spec_kernel, 3));
-    // tail tasks (spec_tails; nobody waits for another workgroup)
-    if (TAILS && !range) a.range |= 2u;
     if (!ctl || ctl->cur_clean < zero_bytes) {
         if (hipMemsetAsync(ctl ? ctl->cur : d_ws, 0, zero_bytes, stream) != hipSuccess)
             return HG_HIP_FAIL;
