@@ -790,3 +790,32 @@ def test_compact_records_mode(engine, knobs, shape, stride):
             assert np.array_equal(s2[: want.size - short], want[: want.size - short]), (mode, short)
             assert (s2[want.size - short:] == 0xCD).all(), (mode, short)
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("prebuild", [1, 0])
+def test_compact_large_values_prebuild(engine, knobs, prebuild):
+    """the compaction prebuilds merge entries into a
+    workspace sized for every record the tables could hold (lens / 16), so
+    with large values that bound is far above the real record count.  8
+    tables of 16-64 KiB values (lens / 16 ~ 100x the records): both with
+    the prebuild (knob HG_COMPACT_PREBUILD 1, the default: taken when the
+    bound fits, else the merge builds its entries after the counts) and
+    without it, the output is the oracle's compacted table byte for byte --
+    twice on one context, so a workspace grown by the first call is reused."""
+    rng = np.random.default_rng(77)
+    knobs("HG_COMPACT_PREBUILD", prebuild)
+    tables = []
+    for t in range(8):
+        ks = sorted({rng.integers(0, 256, 16, dtype=np.uint8).tobytes() for _ in range(60)})
+        tables.append([(k, None if rng.random() < 0.05 else
+                        rng.integers(0, 256, int(rng.integers(16 << 10, 64 << 10)), dtype=np.uint8).tobytes())
+                       for k in ks])
+    datas = encode_tables(tables)
+    assert sum(d.size for d in datas) // 16 > 50 * sum(len(t) for t in tables)
+    want, _, wn = oracle.compacted_table(datas)
+    arena, offs = _arena(engine, datas)
+    for _ in range(2):
+        out = engine.empty(want.size + 64)
+        c = engine.compact_dev(arena, offs, [d.size for d in datas], out)
+        assert c.status == 0 and c.kind == 0 and c.n == wn, c
+        assert np.array_equal(out.cpu().numpy()[:want.size], want)
