@@ -594,11 +594,16 @@ __global__ __launch_bounds__(ENC_THREADS) void encode_sums_kernel(const hg_pair*
 // a contiguous chunk, loaded 8 at a time so the loads overlap) and the call's
 // result: out_len = total bytes, HG_ERR_CAPACITY if they exceed cap.
 constexpr uint32_t BASES_THREADS = 1024;
+// zero_next / zero_words (nullable): the next call's group sums (the other
+// half of a double buffer, hgk_encode_launch_ctl), cleared here.
 __global__ __launch_bounds__(BASES_THREADS) void encode_bases_kernel(uint64_t* gsum, uint64_t ng,
                                                                      uint64_t cap,
-                                                                     hg_encode_result* result) {
+                                                                     hg_encode_result* result,
+                                                                     uint64_t* zero_next,
+                                                                     uint64_t zero_words) {
     __shared__ uint64_t part[BASES_THREADS / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    for (uint64_t i = tid; i < zero_words; i += BASES_THREADS) zero_next[i] = 0;
     const uint64_t chunk = (ng + BASES_THREADS - 1) / BASES_THREADS;
     const uint64_t lo = min(ng, (uint64_t)tid * chunk), hi = min(ng, lo + chunk);
     uint64_t sum = 0;
@@ -687,12 +692,14 @@ int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t 
                        const uint64_t* d_n, int mode, uint64_t rec_arena_len, uint8_t* d_out,
                        uint64_t cap, uint64_t* d_rec_off, uint64_t rec_base,
                        uint32_t block_stride, hg_block* d_blocks, hg_encode_result* d_result,
-                       unsigned long long* d_status, hipStream_t stream, bool gsum_zeroed = false) {
+                       unsigned long long* d_status, hipStream_t stream, bool gsum_zeroed = false,
+                       uint64_t* gsum_ext = nullptr, uint64_t* zero_next = nullptr,
+                       uint64_t zero_words = 0) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
     uint64_t* tsum = reinterpret_cast<uint64_t*>(d_status);
-    uint64_t* gsum = tsum + nt;
+    uint64_t* gsum = gsum_ext ? gsum_ext : tsum + nt;  // (gsum_ext: a double-buffered half)
     if (nt == 0) {
         if (hipMemsetAsync(d_result, 0, sizeof(hg_encode_result), stream) != hipSuccess)
             return HG_HIP_FAIL;
@@ -704,7 +711,7 @@ int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t 
                        d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum), d_n);
     if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng, cap,
-                       d_result);
+                       d_result, zero_next, zero_words);
     if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
     EncodeArgs a;
     a.arena = d_arena;
@@ -758,6 +765,26 @@ extern "C" int hgk_encode_launch_records(const uint8_t* d_arena, uint64_t arena_
                                          hipStream_t stream, int gsum_zeroed) {
     return encode_launch_mode(d_arena, d_pairs, n, d_n, 2, arena_len, d_out, cap, d_rec_off, 0,
                               block_stride, d_blocks, d_result, d_status, stream, gsum_zeroed != 0);
+}
+
+// hgk_encode_launch_ex with its group sums in gs_cur (clean: words of it
+// known to be zero; no memset launch when they cover the call's) and the
+// next call's in gs_next (next_words of room), cleared by encode_bases_kernel;
+// *zeroed = the words cleared.
+extern "C" int hgk_encode_launch_ctl(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,
+                                     uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
+                                     uint32_t block_stride, hg_block* d_blocks,
+                                     hg_encode_result* d_result, unsigned long long* d_status,
+                                     uint64_t* gs_cur, uint64_t clean, uint64_t* gs_next,
+                                     uint64_t next_words, uint64_t* zeroed, hipStream_t stream) {
+    using namespace hgk;
+    const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
+    const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
+    const uint64_t z = ng < next_words ? ng : next_words;
+    *zeroed = nt ? z : 0;
+    return encode_launch_mode(d_arena, d_pairs, n, nullptr, 0, 0, d_out, cap, d_rec_off, 0,
+                              block_stride, d_blocks, d_result, d_status, stream, clean >= ng,
+                              gs_cur, gs_next, z);
 }
 
 // The group sums an encode of n pairs accumulates into (words from d_status):
@@ -838,7 +865,7 @@ extern "C" int hgk_encode_size_launch(const hg_pair* d_pairs, uint64_t n,
                        d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum),
                        (const uint64_t*)nullptr);
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng,
-                       ~0ull, d_result);
+                       ~0ull, d_result, (uint64_t*)nullptr, (uint64_t)0);
     return HG_LAUNCH_STATUS();
 }
 

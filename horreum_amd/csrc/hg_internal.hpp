@@ -45,6 +45,11 @@ extern "C" int hgk_encode_launch_records(const uint8_t*, uint64_t, const hg_pair
                                          hg_block*, hg_encode_result*, unsigned long long*,
                                          hipStream_t, int gsum_zeroed);
 extern "C" void hgk_encode_group_sums(uint64_t n, uint64_t* first_word, uint64_t* words);
+extern "C" int hgk_encode_launch_ctl(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
+                                     uint64_t*, uint32_t, hg_block*, hg_encode_result*,
+                                     unsigned long long*, uint64_t* gs_cur, uint64_t clean,
+                                     uint64_t* gs_next, uint64_t next_words, uint64_t* zeroed,
+                                     hipStream_t);
 extern "C" int hgk_encode_blocks_launch(const uint64_t*, uint64_t, uint32_t, uint64_t, hg_block*,
                                         hipStream_t);
 extern "C" int hgk_encode_size_launch(const hg_pair*, uint64_t, hg_encode_result*, unsigned long long*,
@@ -107,6 +112,11 @@ struct hg_ctx {
     hgi::DevBuf dctl;
     uint64_t dctl_clean[2] = {0, 0};
     int dctl_cur = 0;
+    // device-pair encode: its group sums in two halves used in turn, each
+    // call's bases kernel clearing the other's (hgk_encode_launch_ctl)
+    hgi::DevBuf egs;
+    uint64_t egs_clean[2] = {0, 0};
+    int egs_cur = 0;
     hgi::DevBuf recoff;    // encode record offsets when blocks are wanted w/o rec_off
     hgi::DevBuf results;   // hg_decode_result + hg_encode_result
     hgi::PinBuf hres;      // pinned mirror of `results`

@@ -242,7 +242,7 @@ int hg_ctx_destroy(hg_ctx* c) {
     if (!c) return HG_ERR_INVALID_ARG;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    for (DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
+    for (DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->egs, &c->recoff, &c->results, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mres, &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res,
                       &c->bws, &c->bstage_d, &c->x_res, &c->x_aux, &c->x_arena, &c->x_spans})
         if (b->p) hipFree(b->p);
@@ -267,10 +267,11 @@ int hg_ctx_trim(hg_ctx* c) {
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
     if (c->stream && hipStreamSynchronize(c->stream) != hipSuccess) return HG_HIP_FAIL;
     c->dctl_clean[0] = c->dctl_clean[1] = 0;
+    c->egs_clean[0] = c->egs_clean[1] = 0;
     c->bctl_off[0].clear();
     c->bctl_off[1].clear();
     c->bstage_shadow.clear();
-    for (DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->bstage_d, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
+    for (DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->egs, &c->bstage_d, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res, &c->bws,
                       &c->x_aux, &c->x_arena, &c->x_spans}) {
         if (b->p) hipFree(b->p);
@@ -889,9 +890,32 @@ static int encode_dev_async_ex(hg_ctx* c, const uint8_t* d_arena, const hg_pair*
         if ((r = ensure(c, c->recoff, n * sizeof(uint64_t))) != HG_OK) return r;
         d_rec_off = static_cast<uint64_t*>(c->recoff.p);
     }
-    return hgk_encode_launch_ex(d_arena, d_pairs, n, nullptr, gather, d_out, cap, d_rec_off, 0,
-                                block_stride, d_blocks, d_result,
-                                reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+    if (gather)
+        return hgk_encode_launch_ex(d_arena, d_pairs, n, nullptr, gather, d_out, cap, d_rec_off, 0,
+                                    block_stride, d_blocks, d_result,
+                                    reinterpret_cast<unsigned long long*>(c->ws.p), c->stream);
+    // group sums double-buffered: this call's were cleared by the previous
+    // call's bases kernel when they are big enough (no memset launch)
+    uint64_t first = 0, ng = 0;
+    hgk_encode_group_sums(n, &first, &ng);
+    const uint64_t need = 2 * ((ng * 8 + 255) & ~(uint64_t)255);
+    if (c->egs.bytes < need) {
+        c->egs_clean[0] = c->egs_clean[1] = 0;
+        if ((r = ensure(c, c->egs, need)) != HG_OK) return r;
+    }
+    const uint64_t half = c->egs.bytes / 2 & ~(uint64_t)255;
+    char* base = static_cast<char*>(c->egs.p);
+    const int cur = c->egs_cur;
+    uint64_t zeroed = 0;
+    r = hgk_encode_launch_ctl(d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride, d_blocks,
+                              d_result, reinterpret_cast<unsigned long long*>(c->ws.p),
+                              reinterpret_cast<uint64_t*>(base + cur * half), c->egs_clean[cur],
+                              reinterpret_cast<uint64_t*>(base + (1 - cur) * half), half / 8,
+                              &zeroed, c->stream);
+    c->egs_clean[cur] = 0;
+    c->egs_clean[1 - cur] = r == HG_OK ? zeroed : 0;
+    c->egs_cur = 1 - cur;
+    return r;
 }
 
 int hg_encode_dev_async(hg_ctx* c, const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t n,

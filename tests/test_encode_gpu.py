@@ -213,3 +213,20 @@ def test_host_encode_page_locked_chunks(engine, shuffled, chunk_mb, knobs):
     assert got.out_len == want.size
     assert np.array_equal(got.data, want)
     assert np.array_equal(got.rec_off, wrec) and np.array_equal(got.blocks, wblk)
+
+
+def test_group_sums_reuse(engine):
+    """hg_encode_dev keeps its group sums in two halves used in turn (each
+    call's bases kernel clears the other, so a call no bigger than the last
+    launches no memset): encodes of growing, shrinking and repeated sizes
+    on one context, every output and record offset bit-exact vs the oracle
+    (a stale group sum would shift a whole group of tiles)."""
+    cases = {"big": corpus.mixed(300_000, 24, 96, seed=51), "small": corpus.mixed(3_000, 8, 40, seed=52),
+             "mid": corpus.fixed(90_000, 16, 100, seed=53), "one": corpus.fixed(1, 4, 4, seed=54)}
+    want = {k: oracle.encode(*v) for k, v in cases.items()}
+    for name in ["big", "big", "small", "big", "mid", "mid", "one", "small", "big"]:
+        arena, pairs = cases[name]
+        data, rec_off, _, _ = want[name]
+        got, rec, _ = gpu_encode_dev(engine, arena, pairs)
+        assert np.array_equal(got, data), name
+        assert np.array_equal(rec, rec_off.astype(np.uint64)), name
