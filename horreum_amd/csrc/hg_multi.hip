@@ -23,6 +23,8 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -36,12 +38,83 @@ namespace {
 
 constexpr uint64_t kPiece = 16384;  // hg_decode.hip PIECE
 
-// Run fn(i) for i in [0, n) on one host thread each; the first failing code.
+// Persistent host workers for fan_out: a split compaction runs four steps
+// over every context, and spawning and joining a thread per context per step
+// cost more than a context's share of the work on eight GPUs.  One fan_out
+// uses the pool at a time (busy); a second, concurrent one (another host
+// thread's call) spawns its own threads as before.
+class FanPool {
+  public:
+    ~FanPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (std::thread& t : workers_) t.join();
+    }
+    std::mutex busy;
+    // fn(i) for i in [0, n) on the workers (the caller only waits: its
+    // current HIP device stays its own); returns when all ran
+    void run(uint32_t n, const std::function<void(uint32_t)>& fn) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            // (a new worker starts from the generation before this job's)
+            while (workers_.size() < n && workers_.size() < 64)
+                workers_.emplace_back([this, g = gen_] { work(g); });
+            job_ = &fn;
+            njobs_ = n;
+            next_ = 0;
+            pending_ = n;
+            ++gen_;
+        }
+        cv_.notify_all();
+        std::unique_lock<std::mutex> lk(m_);
+        done_.wait(lk, [this] { return pending_ == 0; });
+        job_ = nullptr;
+    }
+
+  private:
+    void take(std::unique_lock<std::mutex>& lk) {  // run indices until none is left
+        while (next_ < njobs_) {
+            const uint32_t i = next_++;
+            const std::function<void(uint32_t)>* f = job_;
+            lk.unlock();
+            (*f)(i);
+            lk.lock();
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    void work(uint64_t seen) {
+        std::unique_lock<std::mutex> lk(m_);
+        while (true) {
+            cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+            if (stop_) return;
+            seen = gen_;
+            take(lk);
+        }
+    }
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> workers_;
+    const std::function<void(uint32_t)>* job_ = nullptr;
+    uint32_t njobs_ = 0, next_ = 0, pending_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+FanPool g_pool;
+
+// Run fn(i) for i in [0, n) on host threads (a worker per index while the
+// pool has room; more than 64 share them); the first failing code.
 template <typename F>
 int fan_out(uint32_t n, F fn) {
     std::vector<int> rc(n, HG_OK);
     if (n == 1) {
         rc[0] = fn(0u);
+    } else if (g_pool.busy.try_lock()) {
+        const std::function<void(uint32_t)> job = [&rc, &fn](uint32_t i) { rc[i] = fn(i); };
+        g_pool.run(n, job);
+        g_pool.busy.unlock();
     } else {
         std::vector<std::thread> th;
         th.reserve(n);
