@@ -143,8 +143,11 @@ struct hg_ctx {
     hgi::DevBuf bctl;
     int bctl_cur = 0;
     std::vector<uint64_t> bctl_off[2], bctl_zero[2];
-    // what bstage_d holds (a host copy of the last staged arguments)
-    std::vector<uint8_t> bstage_shadow;
+    // bstage_d in two halves used with the control halves (the arguments
+    // point at the call's control half, so a call's bytes repeat two calls
+    // later); what each half holds (a host copy), and the last call's half
+    std::vector<uint8_t> bstage_shadow[2];
+    void* bstage_last = nullptr;
     hipEvent_t bstage_ev = nullptr;
     bool bstage_busy = false;
     // multi-context driver (hg_multi.hip): decode results, gathered offsets

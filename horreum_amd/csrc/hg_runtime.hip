@@ -270,7 +270,8 @@ int hg_ctx_trim(hg_ctx* c) {
     c->egs_clean[0] = c->egs_clean[1] = 0;
     c->bctl_off[0].clear();
     c->bctl_off[1].clear();
-    c->bstage_shadow.clear();
+    c->bstage_shadow[0].clear();
+    c->bstage_shadow[1].clear();
     for (DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->egs, &c->bstage_d, &c->recoff, &c->d_in, &c->d_out, &c->d_aux, &c->d_blk, &c->mws,
                       &c->mspans, &c->mpairs, &c->lk_index, &c->lk_keys, &c->lk_res, &c->bws,
                       &c->x_aux, &c->x_arena, &c->x_spans}) {
@@ -425,10 +426,11 @@ static int batch_one_launch(hg_ctx* c, uint32_t ntables, const uint8_t* const* d
     if (c->bctl.bytes < 2 * ctot) {  // a new allocation holds nothing known to be zero
         for (int h = 0; h < 2; ++h) c->bctl_off[h].clear();
     }
-    if (c->bstage_d.bytes < sb) c->bstage_shadow.clear();
+    const uint64_t sbh = (sb + 255) & ~(uint64_t)255;
+    if (c->bstage_d.bytes < 2 * sbh) c->bstage_shadow[0].clear(), c->bstage_shadow[1].clear();
     int r = ensure(c, c->bws, total ? total : 256);
     if (r == HG_OK) r = ensure(c, c->bctl, 2 * (ctot ? ctot : 256));
-    if (r == HG_OK) r = ensure(c, c->bstage_d, sb);
+    if (r == HG_OK) r = ensure(c, c->bstage_d, 2 * sbh);
     if (r == HG_OK && !c->bstage_ev &&
         hipEventCreateWithFlags(&c->bstage_ev, hipEventDisableTiming) != hipSuccess)
         r = HG_HIP_FAIL;
@@ -441,19 +443,21 @@ static int batch_one_launch(hg_ctx* c, uint32_t ntables, const uint8_t* const* d
     char* base = static_cast<char*>(c->bctl.p);
     std::vector<uint64_t> next_zero(ntables, 0);
     int copied = 1;
+    std::vector<uint8_t>& shadow = c->bstage_shadow[cur];
+    void* const d_stage = static_cast<char*>(c->bstage_d.p) + cur * sbh;
     const hgk_multi_ctl mc{base + cur * half,
                            base + (1 - cur) * half,
                            coff.data(),
                            c->bctl_off[cur] == coff ? c->bctl_zero[cur].data() : nullptr,
                            next_zero.data(),
-                           c->bstage_shadow.empty() ? nullptr : c->bstage_shadow.data(),
-                           c->bstage_shadow.size(),
+                           shadow.empty() ? nullptr : shadow.data(),
+                           shadow.size(),
                            &copied,
                            c->bstage_ev};
     if (r == HG_OK)
         r = hgk_decode_launch_multi(ntables, d_tables, lens, d_spans, caps, d_results, c->bws.p,
-                                    off.data(), c->bstage.p, c->bstage_d.p, c->stream, kpre_tag,
-                                    &mc);
+                                    off.data(), c->bstage.p, d_stage, c->stream, kpre_tag, &mc);
+    c->bstage_last = d_stage;
     // this call dirtied its half; the other is clear where its pre-pass ran
     c->bctl_off[cur].clear();
     if (r == HG_OK) {
@@ -461,11 +465,11 @@ static int batch_one_launch(hg_ctx* c, uint32_t ntables, const uint8_t* const* d
         c->bctl_zero[1 - cur] = std::move(next_zero);
         if (copied) {
             const uint8_t* hs = static_cast<const uint8_t*>(c->bstage.p);
-            c->bstage_shadow.assign(hs, hs + sb);
+            shadow.assign(hs, hs + sb);
         }
     } else {
         c->bctl_off[1 - cur].clear();
-        c->bstage_shadow.clear();
+        shadow.clear();
     }
     c->bctl_cur = 1 - cur;
     if (r != HG_OK) return r;
@@ -1272,7 +1276,7 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
                 }
                 // the decode's device staging (its DecodeArgs and pre-pass grid)
                 // for the per-batch entry builder (hgk_decode_entries_launch)
-                kp[3 * (size_t)ntables] = reinterpret_cast<uint64_t>(c->bstage_d.p);
+                kp[3 * (size_t)ntables] = reinterpret_cast<uint64_t>(c->bstage_last);
                 kp[3 * (size_t)ntables + 1] = hgk_decode_multi_geometry(c->bstage.p, ntables);
             }
         } else {
