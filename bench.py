@@ -301,6 +301,15 @@ def cpu_extras(host_sample, seconds=1.0):
     return out
 
 
+_T0 = time.time()
+
+
+def progress(rank, what):
+    """One stderr line per finished leg (stdout carries only the JSON line):
+    a long run -- the N > 1 rehearsals share one card -- shows it is alive."""
+    print(f"[bench rank {rank}] {what} done at {time.time() - _T0:.1f} s", file=sys.stderr, flush=True)
+
+
 def main(argv=None):
     args = parse(argv)
     rank, world, local = dist_env()
@@ -337,6 +346,7 @@ def main(argv=None):
         eng.decode_dev_async(sst, L, spans, n, res)
 
     wall, launch_ms = time_async(torch, step, args.steps, args.warmup, world, device)
+    progress(rank, "headline decode")
 
     # correctness of what was timed (outside the timed region)
     r = res[:24].cpu().numpy()
@@ -357,23 +367,29 @@ def main(argv=None):
     extra = {}
     if not args.no_encode:
         extra["encode_cfg3"] = encode_leg(torch, eng, device, args, world, rank)
+        progress(rank, "encode")
     if not args.no_extra:
         del spans
         torch.cuda.empty_cache()
         extra["multi_table_decode_cfg4"] = multi_table_leg(torch, eng, device, args, world, rank,
                                                            host=not args.no_host and world == 1)
+        progress(rank, "cfg 4 batched decode")
         extra["compaction_cfg5_scaled"] = compaction_leg(torch, eng, device, world, rank,
                                                          host=not args.no_host and world == 1,
                                                          exact=True)
+        progress(rank, "compaction (scaled)")
         extra["compaction_cfg5_share"] = compaction_leg(torch, eng, device, world, rank,
                                                         per_table=8_134_407, exact=True,
                                                         pmc_name=f"{PMC_TAG}_pmc_compaction_share.json")
+        progress(rank, "compaction (share)")
 
     if not args.no_extra:
         extra["decode_general"] = general_legs(torch, eng, device, world)
         extra["lookups"] = lookup_leg(torch, eng, sst, n, k, v)
+        progress(rank, "general shapes + lookups")
     if not args.no_host and world == 1:
         extra["host_inclusive"] = host_leg(torch, eng, sst, n, world)
+        progress(rank, "host-inclusive")
 
     if not args.no_extra:
         # the split across GPUs (§8e) from rank 0 over contexts on devices
@@ -399,6 +415,8 @@ def main(argv=None):
 
     cpu = (cpu_baseline(sst, n, args.cpu_sample_mb, args.cpu_seconds)
            if (rank == 0 and world == 1) else None)
+    if cpu is not None:
+        progress(rank, "CPU baseline")
     if rank == 0:
         line = {
             "metric": "GiB/s SSTable bytes encoded+decoded, device-resident, 1/2/4/8 MI355X",
