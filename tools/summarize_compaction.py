@@ -48,6 +48,18 @@ def main():
         k = res["kernels"].setdefault(short(r["Name"]), {})
         k["avg_us"] = round(float(r["AverageNs"]) / 1e3, 2)
         k["dispatches_per_call"] = int(r["Calls"]) // CALLS
+    # the three timed calls alone (the warm-up call's first dispatches pay
+    # first-use costs: decode_multi 131 us there against 26 us after)
+    trace = newest_run(glob.glob(os.path.join(out, f"{tag}_ctrace", "**", "*kernel_trace.csv"),
+                                 recursive=True))
+    durs = defaultdict(list)
+    for r in (csv.DictReader(open(trace[0])) if trace else []):
+        if r["Kernel_Name"].startswith(OURS):
+            durs[short(r["Kernel_Name"])].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    for name, d in durs.items():
+        per = len(d) // CALLS
+        if name in res["kernels"] and per:
+            res["kernels"][name]["timed_avg_us"] = round(sum(d[per:]) / len(d[per:]), 2)
     for cnt, sub, scale, key in (("FETCH_SIZE", "cfetch", 2.0, "hbm_read_bytes"),
                                  ("WRITE_SIZE", "cwrite", 1.0, "hbm_write_bytes")):
         tot = defaultdict(float)
