@@ -63,14 +63,19 @@ __global__ __launch_bounds__(256) void sweep_kernel(const uint8_t* src, uint32_t
 // wave per 16 KiB piece) into NBUF LDS buffers, NBUF - 1 pieces in flight,
 // counted vmcnt + raw s_barrier (a __syncthreads() would drain every DMA),
 // nontemporal (aux 2) or default policy.
-template <int NBUF, int AUX>
+// ROT (round 5): workgroup b streams its pieces starting at piece
+// (b * ROT) % ppb and wrapping, so the grid's streams do not walk the same
+// offsets (mod the batch size) in lockstep -- is the lockstep costing
+// anything in the HBM channel interleave?
+template <int NBUF, int AUX, int ROT = 0>
 __global__ __launch_bounds__(256) void glds_sweep_kernel(const uint8_t* src, uint32_t ppb,
                                                          unsigned long long* out) {
     extern __shared__ u32x4 buf[];  // NBUF * PIECE bytes
     const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
     const uint64_t base = (uint64_t)blockIdx.x * ppb * PIECE;
+    const uint32_t rot = ROT ? (blockIdx.x * (uint32_t)ROT) % ppb : 0u;
     auto issue = [&](uint32_t k) {
-        const uint8_t* s = src + base + (uint64_t)k * PIECE;
+        const uint8_t* s = src + base + (uint64_t)((k + rot) % ppb) * PIECE;
         uint8_t* d = reinterpret_cast<uint8_t*>(buf) + (k % NBUF) * PIECE;
 #pragma unroll
         for (uint32_t q = 0; q < GPT; ++q) {
@@ -101,23 +106,23 @@ __global__ __launch_bounds__(256) void glds_sweep_kernel(const uint8_t* src, uin
     if (acc == 0x12345678u) out[0] = acc;
 }
 
-template <int NBUF, int AUX>
+template <int NBUF, int AUX, int ROT = 0>
 void run_glds(const uint8_t* d, uint64_t len, uint32_t ppb, unsigned long long* out, const char* name,
               size_t pad = 0) {
     const uint32_t npieces = (uint32_t)(len / PIECE);
     const uint32_t grid = npieces / ppb;
     const size_t lds = (size_t)NBUF * PIECE + pad;  // pad: extra LDS to cap occupancy
-    CHECK(hipFuncSetAttribute((const void*)glds_sweep_kernel<NBUF, AUX>,
+    CHECK(hipFuncSetAttribute((const void*)glds_sweep_kernel<NBUF, AUX, ROT>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int occ = 0;
-    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, glds_sweep_kernel<NBUF, AUX>, 256, lds));
+    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, glds_sweep_kernel<NBUF, AUX, ROT>, 256, lds));
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
     float best = 1e9f;
     for (int r = 0; r < 8; ++r) {
         CHECK(hipEventRecord(e0));
-        glds_sweep_kernel<NBUF, AUX><<<grid, 256, lds>>>(d, ppb, out);
+        glds_sweep_kernel<NBUF, AUX, ROT><<<grid, 256, lds>>>(d, ppb, out);
         CHECK(hipEventRecord(e1));
         CHECK(hipEventSynchronize(e1));
         float ms;
@@ -188,6 +193,15 @@ int main() {
             if (r > 0 && ms < best) best = ms;
         }
         printf("flat grid-stride           grid=%6d  %.4f ms  %.0f GB/s\n", g, best, len / best / 1e6);
+    }
+    if (getenv("SWEEP_ROT")) {  // the pre-pass geometry (64 pieces, 40 KB), lockstep vs rotated
+        for (int rep = 0; rep < 3; ++rep) {
+            run_glds<2, 2>(d, len, 64, out, "glds x2 nt 40KB", 40960 - 2 * PIECE);
+            run_glds<2, 2, 1>(d, len, 64, out, "glds x2 nt 40KB rot1", 40960 - 2 * PIECE);
+            run_glds<2, 2, 37>(d, len, 64, out, "glds x2 nt 40KB rot37", 40960 - 2 * PIECE);
+            run_glds<2, 2, 32>(d, len, 64, out, "glds x2 nt 40KB rot32", 40960 - 2 * PIECE);
+        }
+        return 0;
     }
     for (uint32_t ppb : {16u, 32u, 64u}) {
         run_glds<2, 2>(d, len, ppb, out, "glds x2 nt");
