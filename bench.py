@@ -49,6 +49,8 @@ def parse(argv=None):
                    help="skip the config-4 / config-5 (scaled) legs")
     p.add_argument("--no-host", action="store_true",
                    help="skip the host-inclusive (H2D + kernel + D2H) legs")
+    p.add_argument("--multi-split-child", default=None, metavar="DEVICES",
+                   help=argparse.SUPPRESS)  # internal: the cross-GPU leg's own process
     return p.parse_args(argv)
 
 
@@ -310,8 +312,47 @@ def progress(rank, what):
     print(f"[bench rank {rank}] {what} done at {time.time() - _T0:.1f} s", file=sys.stderr, flush=True)
 
 
+def multi_split_isolated(devices, timeout_s=600):
+    """multi_split_leg in a child process (rank 0 waits on it): the leg drives
+    every GPU of the node from one process, through the peer-copy branch, and
+    a fault there must not cost the bench line the driver's N > 1 runs
+    record.  Returns the child's JSON object, or an error record."""
+    import subprocess
+    cmd = [sys.executable, os.path.abspath(__file__), "--multi-split-child",
+           ",".join(str(d) for d in devices)]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK",
+                        "ROLE_RANK", "TORCHELASTIC_RUN_ID")}
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s, env=env)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout_s} s"}
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"error": f"exit {p.returncode}", "stderr_tail": p.stderr[-600:]}
+    out = json.loads(lines[-1])
+    out["process"] = "child of rank 0 (isolated from the bench line)"
+    return out
+
+
+def multi_split_child(devs):
+    import torch
+    from horreum_amd.engine import Engine
+    devices = [int(x) for x in devs.split(",")]
+    torch.cuda.set_device(devices[0])
+    eng = Engine(devices[0])
+    try:
+        out = multi_split_leg(torch, eng, devices)
+    except Exception as e:  # noqa: BLE001 -- reported, not raised
+        out = {"error": repr(e)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.multi_split_child:
+        return multi_split_child(args.multi_split_child)
     rank, world, local = dist_env()
     import torch
     if os.environ.get("HG_BENCH_SHARE_GPU") == "1":
@@ -407,10 +448,8 @@ def main(argv=None):
         if devices is None:
             extra["multi_gpu_split"] = {"skipped": "one GPU and HG_BENCH_MULTI_CTX unset"}
         elif rank == 0:
-            try:
-                extra["multi_gpu_split"] = multi_split_leg(torch, eng, devices)
-            except Exception as e:  # noqa: BLE001 -- a failed leg must not lose the bench line
-                extra["multi_gpu_split"] = {"error": repr(e)}
+            extra["multi_gpu_split"] = multi_split_isolated(devices)
+            progress(rank, "cross-GPU split")
         side_barrier(world)
 
     cpu = (cpu_baseline(sst, n, args.cpu_sample_mb, args.cpu_seconds)
