@@ -76,6 +76,10 @@ int ensure(hg_ctx* c, DevBuf& b, size_t bytes) {
     size_t want = std::max(bytes, (size_t)256);
     if (hipMalloc(&b.p, want) != hipSuccess) return HG_HIP_FAIL;
     b.bytes = want;
+    // diagnostics knob: new buffers hold 0xA5 bytes, so a read of memory no
+    // call wrote shows up whatever the allocator hands back
+    if (hgk_knob("HG_DEBUG_POISON", 0) == 1 && hipMemsetAsync(b.p, 0xA5, want, c->stream) != hipSuccess)
+        return HG_HIP_FAIL;
     return HG_OK;
 }
 
@@ -95,6 +99,7 @@ bool try_grow(hg_ctx* c, DevBuf& b, size_t bytes) {
     if (b.p) (void)hipFree(b.p);
     b.p = p;
     b.bytes = bytes;
+    if (hgk_knob("HG_DEBUG_POISON", 0) == 1) (void)hipMemsetAsync(b.p, 0xA5, bytes, c->stream);
     return true;
 }
 
@@ -165,6 +170,7 @@ Knob g_knobs[] = {
     {"HG_MERGE_SERIAL", 0, false},       // 1: the reference loop (rank path), 2: the round-2 loop
     {"HG_MERGE_TEST_EPOCH_FAIL", 0, false},  // test hook: epoch k reports a failure
     {"HG_RANK_NOPACK", 0, false},        // 1: rank path with plain ranks at any size
+    {"HG_DEBUG_POISON", 0, false},       // 1: new device buffers filled with 0xA5 (diagnostics)
 };
 std::mutex g_knob_mu;
 Knob* find_knob(const char* name) {
@@ -444,7 +450,11 @@ static int batch_one_launch(hg_ctx* c, uint32_t ntables, const uint8_t* const* d
     std::vector<uint64_t> next_zero(ntables, 0);
     int copied = 1;
     std::vector<uint8_t>& shadow = c->bstage_shadow[cur];
-    void* const d_stage = static_cast<char*>(c->bstage_d.p) + cur * sbh;
+    // the staging halves split the buffer, not this call's size: a half's
+    // place must not move with the table count, or a smaller call's second
+    // half would land in the first half's bytes (whose shadow then lies)
+    const uint64_t shalf = c->bstage_d.bytes / 2 & ~(uint64_t)255;
+    void* const d_stage = static_cast<char*>(c->bstage_d.p) + cur * shalf;
     const hgk_multi_ctl mc{base + cur * half,
                            base + (1 - cur) * half,
                            coff.data(),

@@ -785,6 +785,43 @@ def test_batch_control_region_reuse(engine):
     run(da, a)
 
 
+def test_batch_staging_halves_with_varying_table_counts(engine):
+    """The argument staging of hg_decode_batch_dev_async alternates between
+    two halves of one device buffer, and a call whose staged bytes equal the
+    half's last ones skips the copy.  Calls of different table counts in turn
+    (3, 1, 3, 2, 3 ... tables): a half's place must not depend on the count,
+    or a one-table call's second half overwrites the three-table arguments
+    that the next identical call then reuses without a copy (found in round
+    5: the next call decoded the previous tables).  Every result bit-exact."""
+    import torch
+
+    outs = {}
+
+    def run(key, devs, datas):
+        caps = [max(d.size // 16, 1) for d in datas]
+        if key not in outs:
+            outs[key] = ([engine.empty(c * 16) for c in caps], engine.empty(24 * len(datas)))
+        spans, res = outs[key]
+        res.fill_(0xEE)
+        engine.decode_batch_dev_async(devs, [d.size for d in datas], spans, caps, res)
+        torch.cuda.synchronize()
+        r = res.cpu().numpy()
+        for i, d in enumerate(datas):
+            ws, wn, wk, wo, _ = oracle.decode(d)
+            n = int(r[24 * i:24 * i + 8].view("<u8")[0])
+            kind = int(r[24 * i + 8:24 * i + 12].view("<i4")[0])
+            assert (n, kind) == (wn, wk), (key, i)
+            assert np.array_equal(engine.spans_to_numpy(spans[i], min(n, caps[i])), ws), (key, i)
+
+    sets = {}
+    for key, seeds in (("three", (91, 92, 93)), ("one", (94,)), ("two", (95, 96))):
+        datas = [oracle.encode(*_large_mixed(2000 + 300 * j, seed=s))[0] for j, s in enumerate(seeds)]
+        sets[key] = ([engine.to_device(d) for d in datas], datas)
+    for key in ("three", "one", "three", "two", "three", "one", "one", "three", "three", "two", "two",
+                "three"):
+        run(key, *sets[key])
+
+
 @pytest.mark.parametrize("where", ["clean", "bad_header_in_tail", "stride_change_in_tail",
                                    "stride_change_at_tail", "tombstones"])
 def test_stride_batch_tails(engine, where):

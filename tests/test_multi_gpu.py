@@ -356,3 +356,71 @@ def test_decode_tables_across_devices_keeps_caller_device():
     finally:
         torch.cuda.set_device(0)
         m.close()
+
+
+# ---- the library's host worker pool (hg_multi.hip FanPool) ---------------------------------
+def _pool_case(engine):
+    tables = sorted_tables(6, 12000, 0.4, 51)
+    datas = [d.tobytes() for d in encode_tables(tables)]
+    single = engine.compact_host(datas, block_stride=5)
+    assert single.status == 0
+    dec_tables = []
+    for t in range(9):
+        arena, pairs = corpus.mixed(300 + 40 * t, 16, 2048, seed=60 + t, kmin=8, vmin=0)
+        dec_tables.append(oracle.encode(arena, pairs)[0])
+    want = [oracle.decode(d) for d in dec_tables]
+
+    def one_pass(m):
+        outs = m.decode_tables(dec_tables)
+        for (w, wn, wk, wo, _), o in zip(want, outs):
+            assert (o.n, o.kind, o.offset) == (wn, wk, wo)
+            assert np.array_equal(o.spans[:wn], w[:wn])
+        got = m.compact(datas, block_stride=5)
+        assert got.status == 0 and np.array_equal(got.data, single.data)
+        assert np.array_equal(got.blocks, single.blocks)
+    return one_pass
+
+
+def test_worker_pool_growth_sequential(engine, multi2):
+    """The multi-context driver runs its per-context steps on persistent host
+    workers: a five-context driver grows the pool past the two- and
+    three-context drivers' workers, then the two-context driver runs on the
+    same pool again; decodes and compactions alternate on both, every result
+    byte-identical to the oracle / the single-context engine."""
+    from horreum_amd.multi import MultiEngine
+    one_pass = _pool_case(engine)
+    m5 = MultiEngine([0] * 5)
+    try:
+        for _ in range(2):
+            one_pass(m5)
+            one_pass(multi2)
+    finally:
+        m5.close()
+
+
+def test_worker_pool_concurrent_drivers(engine, multi2):
+    """Two multi-context drivers used at once from two Python threads: one
+    holds the library's worker pool, the other runs its steps on threads of
+    its own (include/horreum_gpu.h: distinct contexts may be used from
+    distinct threads); both stay byte-identical throughout."""
+    from horreum_amd.multi import MultiEngine
+    one_pass = _pool_case(engine)
+    m5 = MultiEngine([0] * 5)
+    errors = []
+
+    def run(m, reps):
+        try:
+            for _ in range(reps):
+                one_pass(m)
+        except Exception as e:  # noqa: BLE001 -- reported by the main thread
+            errors.append(e)
+
+    try:
+        th = [threading.Thread(target=run, args=(m, 3)) for m in (m5, multi2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errors, errors
+    finally:
+        m5.close()
