@@ -22,6 +22,11 @@ def golden():
 @pytest.fixture(scope="session")
 def engine():
     from horreum_amd.engine import Engine
+    if os.environ.get("HG_TEST_POISON") == "1":
+        # every new device buffer of the library filled with 0xA5: a read of
+        # memory no call wrote cannot pass on zero-filled fresh pages
+        from horreum_amd import abi
+        abi.set_knob("HG_DEBUG_POISON", 1)
     e = Engine(0)
     yield e
     e.close()
