@@ -42,10 +42,18 @@ struct hgk_merge_records {
     hg_encode_result* enc_result;
     uint64_t* zero;
     uint64_t zero_words;
+    // (nullable) the encode's tile sums (enc_nt words) and group sums after
+    // them, accumulated by the merge's last round: the encode then skips its
+    // sums pass over the pairs.  Tiles of 2^enc_tile_log2 records, groups of
+    // 2^enc_group_log2 tiles (hgk_encode_tile_geometry).
+    uint64_t* enc_sums;
+    uint64_t enc_nt, enc_words;
+    uint32_t enc_tile_log2, enc_group_log2;
 };
 // hgk_merge_launch's done flags
 constexpr int HGK_MERGE_EMITTED = 1;  // records mode wrote the records
 constexpr int HGK_MERGE_ZEROED = 2;   // the flag kernel cleared rec->zero
+constexpr int HGK_MERGE_SUMS = 4;     // the last round accumulated rec->enc_sums
 
 namespace hgk {
 

@@ -694,7 +694,7 @@ int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t 
                        uint32_t block_stride, hg_block* d_blocks, hg_encode_result* d_result,
                        unsigned long long* d_status, hipStream_t stream, bool gsum_zeroed = false,
                        uint64_t* gsum_ext = nullptr, uint64_t* zero_next = nullptr,
-                       uint64_t zero_words = 0) {
+                       uint64_t zero_words = 0, bool sums_ready = false) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;
     const uint64_t ng = (nt + ENC_GROUP - 1) / ENC_GROUP;
@@ -705,11 +705,14 @@ int encode_launch_mode(const uint8_t* d_arena, const hg_pair* d_pairs, uint64_t 
             return HG_HIP_FAIL;
         return HG_OK;
     }
-    if (!gsum_zeroed && hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess)
+    // sums_ready: the merge's last round accumulated tsum / gsum (no pass here)
+    if (!sums_ready && !gsum_zeroed && hipMemsetAsync(gsum, 0, ng * sizeof(uint64_t), stream) != hipSuccess)
         return HG_HIP_FAIL;
-    hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
-                       d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum), d_n);
-    if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
+    if (!sums_ready) {
+        hipLaunchKernelGGL(encode_sums_kernel, dim3((uint32_t)nt), dim3(ENC_THREADS), 0, stream,
+                           d_pairs, n, tsum, reinterpret_cast<unsigned long long*>(gsum), d_n);
+        if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
+    }
     hipLaunchKernelGGL(encode_bases_kernel, dim3(1), dim3(BASES_THREADS), 0, stream, gsum, ng, cap,
                        d_result, zero_next, zero_words);
     if (HG_LAUNCH_STATUS() != HG_OK) return HG_ERR_HIP;
@@ -762,9 +765,10 @@ extern "C" int hgk_encode_launch_records(const uint8_t* d_arena, uint64_t arena_
                                          uint8_t* d_out, uint64_t cap, uint64_t* d_rec_off,
                                          uint32_t block_stride, hg_block* d_blocks,
                                          hg_encode_result* d_result, unsigned long long* d_status,
-                                         hipStream_t stream, int gsum_zeroed) {
+                                         hipStream_t stream, int gsum_zeroed, int sums_ready) {
     return encode_launch_mode(d_arena, d_pairs, n, d_n, 2, arena_len, d_out, cap, d_rec_off, 0,
-                              block_stride, d_blocks, d_result, d_status, stream, gsum_zeroed != 0);
+                              block_stride, d_blocks, d_result, d_status, stream, gsum_zeroed != 0,
+                              nullptr, nullptr, 0, sums_ready != 0);
 }
 
 // hgk_encode_launch_ex with its group sums in gs_cur (clean: words of it
@@ -790,6 +794,14 @@ extern "C" int hgk_encode_launch_ctl(const uint8_t* d_arena, const hg_pair* d_pa
 // The group sums an encode of n pairs accumulates into (words from d_status):
 // cleared by the launch unless its caller had them cleared earlier on the
 // stream (gsum_zeroed; the compaction's merge flag kernel does).
+extern "C" void hgk_encode_tile_geometry(uint32_t* tile_log2, uint32_t* group_log2) {
+    using namespace hgk;
+    static_assert((ENC_TILE & (ENC_TILE - 1)) == 0 && (ENC_GROUP & (ENC_GROUP - 1)) == 0,
+                  "encode tiles and groups are powers of two");
+    *tile_log2 = (uint32_t)__builtin_ctz(ENC_TILE);
+    *group_log2 = (uint32_t)__builtin_ctz(ENC_GROUP);
+}
+
 extern "C" void hgk_encode_group_sums(uint64_t n, uint64_t* first_word, uint64_t* words) {
     using namespace hgk;
     const uint64_t nt = (n + ENC_TILE - 1) / ENC_TILE;

@@ -43,8 +43,9 @@ extern "C" int hgk_encode_launch_ex(const uint8_t*, const hg_pair*, uint64_t, co
 extern "C" int hgk_encode_launch_records(const uint8_t*, uint64_t, const hg_pair*, uint64_t,
                                          const uint64_t*, uint8_t*, uint64_t, uint64_t*, uint32_t,
                                          hg_block*, hg_encode_result*, unsigned long long*,
-                                         hipStream_t, int gsum_zeroed);
+                                         hipStream_t, int gsum_zeroed, int sums_ready);
 extern "C" void hgk_encode_group_sums(uint64_t n, uint64_t* first_word, uint64_t* words);
+extern "C" void hgk_encode_tile_geometry(uint32_t* tile_log2, uint32_t* group_log2);
 extern "C" int hgk_encode_launch_ctl(const uint8_t*, const hg_pair*, uint64_t, uint8_t*, uint64_t,
                                      uint64_t*, uint32_t, hg_block*, hg_encode_result*,
                                      unsigned long long*, uint64_t* gs_cur, uint64_t clean,

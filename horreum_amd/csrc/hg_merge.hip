@@ -363,9 +363,13 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
                                                               const MEnt* in, uint64_t* split,
                                                               uint64_t nb_tiles,
                                                               const unsigned long long* err,
-                                                              unsigned long long* zst) {
+                                                              unsigned long long* zst,
+                                                              unsigned long long* zsum = nullptr,
+                                                              uint64_t zsum_words = 0) {
     const uint32_t lane = threadIdx.x & 63u, j = lane % SPLIT_G, gsh = lane - j;
-    const uint64_t t = ((uint64_t)blockIdx.x * THREADS + threadIdx.x) / SPLIT_G;
+    const uint64_t gt = (uint64_t)blockIdx.x * THREADS + threadIdx.x;
+    if (gt < zsum_words) zsum[gt] = 0;  // the last round's encode sums (FinalArgs::enc_sums)
+    const uint64_t t = gt / SPLIT_G;
     if (t > nb_tiles) return;  // the whole group
     uint64_t i = 0;
     if (*err == ~0ull) {
@@ -425,7 +429,13 @@ struct FinalArgs {
     uint64_t rec_cap;
     uint64_t* rec_off;             // nullable: each record's output offset (block index)
     hg_encode_result* enc_result;  // out_len, HG_ERR_CAPACITY past rec_cap
+    // pairs mode (MODE 1), nullable: the encode's tile sums [enc_nt] and group
+    // sums after them, accumulated here (zeroed by the round's split kernel)
+    unsigned long long* enc_sums;
+    uint64_t enc_nt, enc_words;  // tile sums; all words (tile + group sums)
+    uint32_t enc_tile_log2, enc_group_log2;
 };
+constexpr uint32_t FIN_ENC_SLOTS = 17;  // encode tiles one merge tile's pairs can touch (>= 64 records each)
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INCL = 2ull << 62;
 constexpr unsigned long long LB_VAL = (1ull << 62) - 1;
 
@@ -624,6 +634,7 @@ __global__ __launch_bounds__(THREADS, MODE == 1 ? 6 : MODE == 2 ? HG_REC_WAVES :
     __shared__ LevelSmem s;
     __shared__ uint32_t fin_tmp[THREADS / 64];
     __shared__ uint64_t fin_base, fin_bbase, fin_tmp64[THREADS / 64];
+    __shared__ unsigned long long fin_esum[FIN_ENC_SLOTS];  // MODE 1: this tile's bytes per encode tile
     // FINAL: the tables' run offsets, span arrays and arena offsets in LDS
     // (up to FIN_LDS_TABLES tables), so a live record's span lookup is one
     // HBM load after an LDS search instead of a chain of dependent loads
@@ -637,6 +648,7 @@ __global__ __launch_bounds__(THREADS, MODE == 1 ? 6 : MODE == 2 ? HG_REC_WAVES :
     const uint64_t t0 = (uint64_t)bx * TILE;
     if (t0 >= a.n) return;
     const bool fin_lds = FINAL && a.ntables <= FIN_LDS_TABLES;
+    if (MODE == 1 && tid < FIN_ENC_SLOTS) fin_esum[tid] = 0;  // read after later barriers
     if (fin_lds) {  // read after the segment staging's barrier
         if (tid <= a.ntables) fin_roff[tid] = a.run_off[tid];
         if (tid < a.ntables) {
@@ -844,6 +856,23 @@ __global__ __launch_bounds__(THREADS, MODE == 1 ? 6 : MODE == 2 ? HG_REC_WAVES :
                     uint64_t* o8 = reinterpret_cast<uint64_t*>(f.out);
                     for (uint32_t i = tid; i < 3 * ftot; i += THREADS)
                         if (w0 + i < wcap) o8[w0 + i] = s8[i];
+                    if (f.enc_sums) {
+                        // the encode's record sizes per tile of its output
+                        // (pair q in encode tile q >> tile_log2): into LDS,
+                        // then one atomic per touched tile and group
+                        const uint64_t T0 = fin_base >> f.enc_tile_log2;
+                        for (uint32_t i = tid; i < ftot; i += THREADS) {
+                            const hg_pair& p = lp[i];
+                            atomicAdd(&fin_esum[((fin_base + i) >> f.enc_tile_log2) - T0],
+                                      16ull + p.klen + p.vlen);
+                        }
+                        __syncthreads();
+                        if (tid < FIN_ENC_SLOTS && fin_esum[tid]) {
+                            const uint64_t T = T0 + tid;
+                            atomicAdd(f.enc_sums + T, fin_esum[tid]);
+                            atomicAdd(f.enc_sums + f.enc_nt + (T >> f.enc_group_log2), fin_esum[tid]);
+                        }
+                    }
                 } else {
                     // records mode: each live record's source (its header in
                     // the arena) and output offset in the tile go to LDS --
@@ -2086,10 +2115,18 @@ int launch_rounds(const hgm::MergeArgs& a, const uint64_t* roff, uint64_t nr, hg
             l.uw = l.un = 0;
             // tile_base is free in the rounds: the round's splits
             const uint32_t gs = (uint32_t)(((ntiles + 1) * SPLIT_G + THREADS - 1) / THREADS);
+            // the last round's split kernel also clears the encode sums that
+            // round accumulates (when its grid covers them)
+            const bool sums = nr == 2 && !fa.rec_out && fa.enc_sums &&
+                              fa.enc_words <= (uint64_t)gs * THREADS;
             hipLaunchKernelGGL(merge_split_kernel, dim3(gs), dim3(THREADS), 0, stream, a, l,
                                (const MEnt*)cur, w.tile_base, ntiles, (const unsigned long long*)err,
-                               first ? w.lb_status : (unsigned long long*)nullptr);
+                               first ? w.lb_status : (unsigned long long*)nullptr,
+                               sums ? fa.enc_sums : (unsigned long long*)nullptr,
+                               sums ? fa.enc_words : (uint64_t)0);
             first = false;
+            if (nr == 2 && !sums) fa.enc_sums = nullptr;
+            if (sums && done) *done |= HGK_MERGE_SUMS;
             if (nr == 2)  // the last round emits the pairs
                 if (fa.rec_out) {  // compaction: the records themselves
                     hipLaunchKernelGGL(merge_level_kernel<2>, dim3((uint32_t)ntiles), dim3(THREADS), 0,
@@ -2352,14 +2389,25 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
         fa.rec_cap = rec->cap;
         fa.rec_off = rec->rec_off;
         fa.enc_result = rec->enc_result;
+    } else if (rec && rec->enc_sums && defer) {
+        // pairs mode: the last round also sums the encode's tiles (defer only:
+        // otherwise the exact loop may rewrite the pairs after it)
+        fa.enc_sums = reinterpret_cast<unsigned long long*>(rec->enc_sums);
+        fa.enc_nt = rec->enc_nt;
+        fa.enc_words = rec->enc_words;
+        fa.enc_tile_log2 = rec->enc_tile_log2;
+        fa.enc_group_log2 = rec->enc_group_log2;
     }
     // the rounds ping-pong between e1 and e2, so e0 keeps the entries for the
     // exact loop / the epochs (the first round reads e0)
+    int dl = 0;
     int rc = launch_rounds(a, a.run_off + ntables + 1, nruns0, w.e0, w.e1, w.e2, w, err, fa,
-                           stream, r0, done);
+                           stream, r0, &dl);
+    if (done) *done |= dl;
     if (rc != HG_OK) return rc;
     if (defer) {
-        uint64_t* const zero = rec ? rec->zero : nullptr;
+        // (not the group sums the last round accumulated)
+        uint64_t* const zero = rec && !(dl & HGK_MERGE_SUMS) ? rec->zero : nullptr;
         const uint64_t zero_words = zero ? rec->zero_words : 0;
         hipLaunchKernelGGL(merge_flag_kernel, dim3(1), dim3(THREADS), 0, stream,
                            (const unsigned long long*)err, d_result, zero, zero_words);

@@ -165,6 +165,7 @@ Knob g_knobs[] = {
     {"HG_COMPACT_PREBUILD", 0, false},   // 0: merge entries built after the host has the counts
     {"HG_COMPACT_ENCODE", 0, false},     // 1: compaction encode by the general pair gather
     {"HG_COMPACT_RECORDS", 0, false},    // 1: compaction merge writes the records (no pairs, no encode pass)
+    {"HG_COMPACT_MERGE_SUMS", 0, false}, // 0: the records encode sums its tiles itself (not the merge)
     {"HG_MERGE_KENT", 0, false},         // 0: merge entries by merge_prep_kernel
     {"HG_MERGE_KWAY", 0, false},         // 1: the one-pass k-way merge (3..KW_MAX runs)
     {"HG_MERGE_SERIAL", 0, false},       // 1: the reference loop (rank path), 2: the round-2 loop
@@ -1360,18 +1361,29 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
     // (c->ws holds them: sized for the encode of nm pairs above)
     uint64_t gs_first = 0, gs_words = 0;
     hgk_encode_group_sums(nm, &gs_first, &gs_words);
+    // (pairs mode: the merge's last round also accumulates the records
+    // encode's tile sums, c->ws [0, gs_first), and group sums after them)
+    uint32_t tl2 = 0, gl2 = 0;
+    hgk_encode_tile_geometry(&tl2, &gl2);
+    const bool merge_sums = enc_records && !rec_mode && nm && hgk_knob("HG_COMPACT_MERGE_SUMS", 1) != 0;
     hgk_merge_records rec{rec_mode ? d_out : nullptr,
                           cap,
                           d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr,
                           dres_e,
                           enc_records && nm ? static_cast<uint64_t*>(c->ws.p) + gs_first : nullptr,
-                          gs_words};
+                          gs_words,
+                          merge_sums ? static_cast<uint64_t*>(c->ws.p) : nullptr,
+                          gs_first,
+                          gs_first + gs_words,
+                          tl2,
+                          gl2};
     int done = 0;
     r = merge_async(c, ntables, arena, arena_len, toff, sp.data(), counts.data(), pairs, nm, dres_m,
                     1, kp.empty() ? nullptr : kp.data(), kp_tag, prebuilt_err, &rec, &done);
     if (r != HG_OK) return r;
     const bool emitted = (done & HGK_MERGE_EMITTED) != 0;
     bool zeroed = (done & HGK_MERGE_ZEROED) != 0;  // for the first encode only
+    bool sums = (done & HGK_MERGE_SUMS) != 0;      // (likewise)
     auto encode = [&]() -> int {
         if (nm == 0)
             return hipMemsetAsync(dres_e, 0, sizeof(hg_encode_result), c->stream) == hipSuccess
@@ -1388,7 +1400,7 @@ static int compact_core(hg_ctx* c, uint32_t ntables, const uint8_t* arena, uint6
                                          d_blk ? static_cast<uint64_t*>(c->recoff.p) : nullptr,
                                          block_stride, d_blk, dres_e,
                                          reinterpret_cast<unsigned long long*>(c->ws.p), c->stream,
-                                         std::exchange(zeroed, false));
+                                         std::exchange(zeroed, false), std::exchange(sums, false));
     };
     if (!emitted) {
         if ((r = encode()) != HG_OK) return r;
