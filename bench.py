@@ -206,47 +206,64 @@ def host_cores():
 
 def cpu_all_cores(host_sample, seconds=2.0):
     """The optimised multi-threaded CPU codec (oracle/cpu_opt.c: byte ranges
-    with guessed entries handed over in order, spans not owned copies;
-    sizes / prefix / copy for encode) on every host core this job may use:
-    cfg 2 decode of the same sample, cfg 3 encode of a 1 M-pair sample."""
+    with guessed entries handed over in order, spans placed in parallel, not
+    owned copies; sizes / prefix / copy for encode; workers started at a
+    barrier, as a pool would hold them) on EVERY core this process may run
+    on (its CPU affinity, capped at the codec's 256 threads), and beside it
+    on the job's OMP_NUM_THREADS share: cfg 2 decode of the same sample,
+    cfg 3 encode of a 1 M-pair sample, and a memcpy of the sample (the
+    CPU's streaming ceiling)."""
     from horreum_amd import synth
     from oracle import oracle
-    threads, nproc, aff = host_cores()
+    share, nproc, aff = host_cores()
     want_n = host_sample.size // (16 + CFG2["k"] + CFG2["v"])
-    spans = np.zeros(host_sample.size // 16 + 1, dtype=oracle.SPAN_DTYPE)
-    scratch = np.empty(host_sample.size // 16 + 2 * threads + 2, dtype=oracle.SPAN_DTYPE)
-    tot, k = 0.0, 0
-    while k == 0 or tot < seconds:
-        _, n, t = oracle.mt_decode(host_sample, threads, spans, scratch)
-        assert n == want_n, (n, want_n)
-        tot += t
-        k += 1
-    dec = k * host_sample.size / tot / GIB
     arena, pairs = synth.fixed_arena(1_000_000, 32, 256, seed=3, device="cpu")
     a, p = arena.numpy(), pairs.numpy().view(oracle.PAIR_DTYPE)
     out = np.empty(304_000_000, dtype=np.uint8)
-    tot, k = 0.0, 0
-    while k == 0 or tot < seconds:
-        got, t = oracle.mt_encode(a, p, threads, out)
-        assert got.size == 304_000_000
-        tot += t
-        k += 1
-    enc = k * 304_000_000 / tot / GIB
-    cp = np.empty_like(host_sample)  # the CPU roofline: memcpy on the same threads
-    tot, k = 0.0, 0
-    while k == 0 or tot < seconds:
-        tot += oracle.mt_memcpy(cp, host_sample, threads)
-        k += 1
-    mcp = k * host_sample.size / tot / GIB
+    cp = np.empty_like(host_sample)
+    spans = np.zeros(host_sample.size // 16 + 1, dtype=oracle.SPAN_DTYPE)
+
+    def rate(fn, nbytes):
+        tot, k = 0.0, 0
+        while k == 0 or tot < seconds:
+            tot += fn()
+            k += 1
+        return k * nbytes / tot / GIB
+
+    def measure(threads):
+        scratch = np.empty(host_sample.size // 16 + 2 * threads + 2, dtype=oracle.SPAN_DTYPE)
+
+        def dec():
+            _, n, t = oracle.mt_decode(host_sample, threads, spans, scratch)
+            assert n == want_n, (n, want_n)
+            return t
+
+        def enc():
+            got, t = oracle.mt_encode(a, p, threads, out)
+            assert got.size == 304_000_000
+            return t
+        return {"threads": threads,
+                "decode_cfg2_GiB_s": round(rate(dec, host_sample.size), 3),
+                "encode_cfg3_1M_GiB_s": round(rate(enc, 304_000_000), 3),
+                "memcpy_GiB_s": round(rate(lambda: oracle.mt_memcpy(cp, host_sample, threads),
+                                           host_sample.size), 3)}
+    whole = measure(min(aff, 256))
     ok = bool(np.array_equal(spans[:1000], oracle.decode(host_sample[:132000])[0])
               and np.array_equal(cp[:4096], host_sample[:4096]))
+    job = measure(share) if share != whole["threads"] else None
     del cp
-    return {"cores": threads, "nproc": nproc, "affinity": aff, "kind": "port (tuned)",
-            "decode_cfg2_GiB_s": round(dec, 3), "encode_cfg3_1M_GiB_s": round(enc, 3),
-            "memcpy_GiB_s": round(mcp, 3),
-            "sample": f"decode: the same {host_sample.size} B cfg 2 sample; encode: 1 M pairs of "
-                      f"32 B / 256 B; hgo_mt_decode / hgo_mt_encode, >= {seconds} s each",
-            "parity_spot": ok}
+    out_d = {"cores": whole["threads"], "nproc": nproc, "affinity": aff, "kind": "port (tuned)",
+             "decode_cfg2_GiB_s": whole["decode_cfg2_GiB_s"],
+             "encode_cfg3_1M_GiB_s": whole["encode_cfg3_1M_GiB_s"],
+             "memcpy_GiB_s": whole["memcpy_GiB_s"],
+             "sample": f"decode: the same {host_sample.size} B cfg 2 sample; encode: 1 M pairs of "
+                       f"32 B / 256 B; hgo_mt_decode / hgo_mt_encode, >= {seconds} s each, on "
+                       f"every core of the process's affinity",
+             "parity_spot": ok}
+    if job is not None:
+        out_d["job_share"] = dict(job, note="the OMP_NUM_THREADS share the GPU box gives one "
+                                            "GPU's job")
+    return out_d
 
 
 def cpu_extras(host_sample, seconds=1.0):
@@ -421,7 +438,9 @@ def main(argv=None):
         progress(rank, "compaction (scaled)")
         extra["compaction_cfg5_share"] = compaction_leg(torch, eng, device, world, rank,
                                                         per_table=8_134_407, exact=True,
-                                                        pmc_name=f"{PMC_TAG}_pmc_compaction_share.json")
+                                                        pmc_name=f"{PMC_TAG}_pmc_compaction_share.json",
+                                                        host=not args.no_host and world == 1,
+                                                        pinned=True)
         progress(rank, "compaction (share)")
 
     if not args.no_extra:
@@ -969,7 +988,7 @@ def cfg5_value_seed(rank, t):
 
 
 def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000, host=False,
-                   pmc_name=f"{PMC_TAG}_pmc_compaction.json", exact=False):
+                   pmc_name=f"{PMC_TAG}_pmc_compaction.json", exact=False, pinned=False):
     """BASELINE config 5 on this GPU's key range: 8 sorted tables of
     `per_table` records each (16 B keys / 100 B values, 132 B records), 25 %
     of each table's keys shared by all tables.  The global dataset is 8
@@ -1019,9 +1038,12 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
         del bufs
     out = eng.empty(total)
 
+    paths = []  # the merge path of every call (hg_merge_result table / index)
+
     def run():
         c = eng.compact_dev(arena, offs_b, sizes, out)
         assert c.status == 0, c
+        paths.append([int(c.table), int(c.index)])
         return c, c.data.numel()
 
     run()
@@ -1051,6 +1073,11 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
             exact_ok = torch.equal(out[i * 132:j * 132], rows.index_select(0, want_rows[i:j]).view(-1))
         exact_ok = bool(exact_ok)
         del rows, want_rows
+    want_first = want_last = None
+    if hosts is not None:  # the host leg's parity spot: both ends of the device output
+        mib = min(1 << 20, int(out_len))
+        want_first = out[:mib].cpu().numpy()
+        want_last = out[int(out_len) - mib:int(out_len)].cpu().numpy()
     del out
     torch.cuda.empty_cache()
     line = {"value": round(world * in_bytes / wall / GIB, 3), "unit": "GiB/s of input tables",
@@ -1058,6 +1085,10 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
             "merged_records": int(m.n), "merged_bytes": int(out_len),
             "ms": round(wall * 1e3, 3), "times_ms": [round(t * 1e3, 3) for t in times],
             "status": int(m.status), "api": "hg_compact_dev", "input_records": n_in,
+            # per call (warm-up first): [0, 0] the parallel merge; [3, k] redone
+            # k times after a look-back wait over its budget; [1|2, ..] the
+            # reference loop (unsorted input: never here)
+            "merge_paths": paths,
             "split": f"key range {rank} of {world} (no data movement between GPUs)",
             # newest wins over sorted unique tables: one record per distinct key
             "parity_count_ok": int(m.n) == n_distinct, "parity_bytes_ok": exact_ok}
@@ -1077,16 +1108,35 @@ def compaction_leg(torch, eng, device, world, rank, ntab=8, per_table=1_000_000,
     line["traffic_source"] = src
     if hosts is not None:
         hout = np.empty(in_bytes, dtype=np.uint8)  # caller-owned output, reused
-        eng.compact_host(hosts, out=hout)  # warm-up (staging buffers, workspaces)
-        ht = []
-        for _ in range(3):
-            t0 = time.perf_counter()
-            c = eng.compact_host(hosts, out=hout)
-            ht.append(time.perf_counter() - t0)
-        t = sorted(ht)[1]
+        reg = []
+        if pinned:  # page-locked in and out: DMA straight from / to them
+            for h in hosts + [hout]:
+                eng.host_register(h)
+                reg.append(h)
+        try:
+            hpaths = []
+            eng.compact_host(hosts, out=hout)  # warm-up (staging buffers, workspaces)
+            ht = []
+            for _ in range(3):
+                t0 = time.perf_counter()
+                c = eng.compact_host(hosts, out=hout)
+                ht.append(time.perf_counter() - t0)
+                hpaths.append([int(c.table), int(c.index)])
+            t = sorted(ht)[1]
+            # parity spot: the output's first and last MiB against the device run's
+            spot = bool(c.status == 0 and c.n == m.n and c.data.size == out_len)
+            if spot and want_first is not None:
+                spot = (np.array_equal(hout[:want_first.size], want_first)
+                        and np.array_equal(hout[out_len - want_last.size:out_len], want_last))
+        finally:
+            for h in reg:
+                eng.host_unregister(h)
         line["host_inclusive"] = {"ms": round(t * 1e3, 2), "GiB_s": round(in_bytes / t / GIB, 3),
-                                  "parity_spot": bool(c.status == 0 and c.n == m.n
-                                                      and c.data.size == out_len)}
+                                  "times_ms": [round(x * 1e3, 2) for x in ht],
+                                  "input": "pinned (hipHostRegister)" if pinned else "pageable",
+                                  "api": "hg_compact_host: H2D of every table, decode, merge, "
+                                         "encode, D2H of the compacted table",
+                                  "merge_paths": hpaths, "parity_spot": spot}
         del hosts
     return line
 

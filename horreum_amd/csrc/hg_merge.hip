@@ -408,6 +408,7 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
             zst[t] = 0;
             zst[nb_tiles + t] = 0;
         }
+        if (zst && t == nb_tiles) zst[2 * nb_tiles] = 0;  // the FINAL round's tile ticket
     }
 }
 
@@ -417,7 +418,8 @@ __global__ __launch_bounds__(THREADS) void merge_split_kernel(MergeArgs a, Level
 // its pairs at their final positions; the last tile writes the result.
 struct FinalArgs {
     unsigned long long* st;  // [ntiles] look-back status (zeroed): flag << 62 | live count
-                             // (records mode: then [ntiles] of output bytes, same flags)
+                             // (records mode: then [ntiles] of output bytes, same flags;
+                             // st[2 ntiles]: the tile ticket, zeroed with them)
     hg_pair* out;
     uint64_t cap;
     hg_merge_result* result;
@@ -434,6 +436,9 @@ struct FinalArgs {
     unsigned long long* enc_sums;
     uint64_t enc_nt, enc_words;  // tile sums; all words (tile + group sums)
     uint32_t enc_tile_log2, enc_group_log2;
+    // test hook (knob HG_MERGE_TEST_LB_EXPIRE): this tile's look-back acts
+    // as if its wait ran over the budget (~0u: none)
+    uint32_t test_expire = ~0u;
 };
 constexpr uint32_t FIN_ENC_SLOTS = 17;  // encode tiles one merge tile's pairs can touch (>= 64 records each)
 constexpr unsigned long long LB_AGG = 1ull << 62, LB_INCL = 2ull << 62;
@@ -456,6 +461,13 @@ __device__ uint64_t final_lookback(const FinalArgs& f, uint32_t t, uint64_t agg,
     const uint32_t lane = threadIdx.x & 63u;
     if (t == 0) {
         if (lane == 0) final_publish(f, 0, LB_INCL | agg);
+        return 0;
+    }
+    if (t == f.test_expire) {  // test hook: a wait over the budget
+        if (lane == 0) {
+            atomicMin(err, 0ull);
+            final_publish(f, t, LB_INCL | agg);
+        }
         return 0;
     }
     if (lane == 0) hgk::st_agent(&f.st[t], LB_AGG | agg);
@@ -512,9 +524,17 @@ __device__ void final_lookback2(const FinalArgs& f, uint32_t t, uint64_t agg_c, 
         }
         return;
     }
-    if (lane == 0) {
+    if (lane == 0 && t != f.test_expire) {
         hgk::st_agent(&f.st[t], LB_AGG | agg_c);
         hgk::st_agent(&stb[t], LB_AGG | agg_b);
+    }
+    if (t == f.test_expire) {  // test hook: a wait over the budget
+        if (lane == 0) {
+            atomicMin(err, 0ull);
+            hgk::st_agent(&f.st[t], LB_INCL | agg_c);
+            hgk::st_agent(&stb[t], LB_INCL | agg_b);
+        }
+        return;
     }
     uint64_t acc_c = 0, acc_b = 0;
     int64_t j0 = (int64_t)t - 1;
@@ -644,7 +664,19 @@ __global__ __launch_bounds__(THREADS, MODE == 1 ? 6 : MODE == 2 ? HG_REC_WAVES :
     // (tiles in blockIdx order: an XCD-contiguous deal of the tiles, measured
     // round 4, made the non-final rounds 87 -> 94 us and the record gather
     // 368 -> 376 us on the cfg 5 leg)
-    const uint32_t bx = blockIdx.x;
+    // The FINAL round's look-back waits on the tiles before it, so its tile
+    // index is a ticket drawn when the workgroup starts: every tile it waits
+    // on is then already resident and running.  By blockIdx a later tile
+    // could occupy a CU while an earlier one still waits for dispatch -- on
+    // a GPU shared with another process (whose waves hold the earlier
+    // tile's XCD) that wait ran out the spin budget and the merge went to a
+    // redo, 4-125 s per compaction (profiles/r5_bench_n2_shared_gpu_rehearsal.json).
+    __shared__ uint32_t fin_ticket;
+    if (FINAL) {
+        if (tid == 0) fin_ticket = atomicAdd(reinterpret_cast<unsigned int*>(f.st + 2 * (uint64_t)f.ntiles), 1u);
+        __syncthreads();
+    }
+    const uint32_t bx = FINAL ? fin_ticket : blockIdx.x;
     const uint64_t t0 = (uint64_t)bx * TILE;
     if (t0 >= a.n) return;
     const bool fin_lds = FINAL && a.ntables <= FIN_LDS_TABLES;
@@ -2384,6 +2416,7 @@ extern "C" int hgk_merge_launch(const uint8_t* d_arena, uint64_t arena_len, uint
     fa.out = d_out;
     fa.cap = cap;
     fa.result = d_result;
+    fa.test_expire = (uint32_t)hgk_knob("HG_MERGE_TEST_LB_EXPIRE", -1);  // test hook (unset: ~0u)
     if (rec && rec->out) {  // records mode: the last round writes the records (no pairs)
         fa.rec_out = rec->out;
         fa.rec_cap = rec->cap;
@@ -2490,7 +2523,8 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
     };
     // D == 0: the tables are strictly increasing after all -- the error word
     // came from a look-back wait over its budget (contention), not from the
-    // order check -- and the one epoch below is the whole merge again.
+    // order check -- and the one epoch below is the whole merge again, by
+    // the parallel rounds (result table 3, index = the redos).
     // an epoch costs a few launches and host round trips (~0.1-0.2 ms): many
     // disorder points -> the serial loop
     if (D > EPOCH_MAX_DISORDER || D > n / 128 + 1 || serial_knob) return serial(nullptr, 0);
@@ -2515,6 +2549,13 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
     uint64_t* dhi = w.ep + 2 * (uint64_t)ntables;
     uint64_t* du = w.ep + 3 * (uint64_t)ntables;
     unsigned long long* ep_err = w.dis_count + 1;
+    // An epoch's sub-runs are strictly increasing, so its error word can only
+    // come from a look-back wait over the budget: the epoch is merged again
+    // by the parallel rounds (up to EPOCH_REDOS times in all) before the
+    // serial loop takes over -- a serial loop over millions of records is
+    // thousands of times slower than a redo.
+    constexpr uint32_t EPOCH_REDOS = 4;
+    uint32_t redos = 0;
     for (;;) {
         uint32_t nc = 0;
         bool left = false;
@@ -2575,15 +2616,22 @@ extern "C" int hgk_merge_epochs(const uint8_t* d_arena, uint64_t arena_len, uint
         if ((rc = sync_copy(&er.r, w.ep_res, sizeof er.r, hipMemcpyDeviceToHost, stream)) != HG_OK ||
             (rc = sync_copy(&er.e, ep_err, 8, hipMemcpyDeviceToHost, stream)) != HG_OK)
             return rc;
-        // a look-back wait over its budget (a stalled or shared GPU) or any
-        // other failure of the epoch: the serial loop takes over from its
-        // heads, overwriting whatever pairs the epoch left past N
-        if (er.e != ~0ull || er.r.kind != HG_OK || (long)epochs == fail_at) return serial(hd.data(), N);
+        // a look-back wait over its budget (a stalled or shared GPU): the
+        // epoch again; any other failure of the epoch (or too many redos):
+        // the serial loop takes over from its heads, overwriting whatever
+        // pairs the epoch left past N
+        if ((long)epochs == fail_at) return serial(hd.data(), N);
+        if (er.e == 0 && er.r.kind == HG_OK && redos < EPOCH_REDOS) {
+            ++redos;
+            continue;  // hd unchanged: the same cuts, merged again
+        }
+        if (er.e != ~0ull || er.r.kind != HG_OK) return serial(hd.data(), N);
         N += er.r.n_out;
         for (uint32_t t = 0; t < ntables; ++t) hd[t] = u[t];
         ++epochs;
     }
     // table = 2: the epochs produced the output (index = their number); D == 0
-    // (a look-back over its budget, sorted input): the one epoch was a plain redo
-    return finish(hg_merge_result{N, HG_OK, D ? 2u : 0u, D ? epochs : 0});
+    // (a look-back over its budget, sorted input): the one epoch was a plain
+    // redo of the parallel merge (table 3, index = the redos, >= 1)
+    return finish(hg_merge_result{N, HG_OK, D ? 2u : 3u, D ? epochs : (uint64_t)redos + 1});
 }

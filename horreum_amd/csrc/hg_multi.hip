@@ -632,8 +632,17 @@ struct Owned {
 
 struct RangeOut {
     uint64_t n = 0, bytes = 0;
-    uint32_t exact = 0;
+    uint32_t exact = 0;  // the slice's merge followed the reference loop (unsorted input)
+    uint64_t redos = 0;  // merges redone after a look-back wait over its budget (table 3)
 };
+
+// The merge path of a split compaction for hg_merge_result: 0, or 3 with the
+// redos of every range summed (the output is the same either way).
+hg_merge_result split_result(const std::vector<RangeOut>& O, uint64_t nrec) {
+    uint64_t redos = 0;
+    for (const RangeOut& o : O) redos += o.redos;
+    return hg_merge_result{nrec, HG_OK, redos ? 3u : 0u, redos};
+}
 
 // Steps 2-5 of a split compaction over decoded tables: samples -> splitters ->
 // cut points -> every range on its context (slices gathered by device copies,
@@ -895,9 +904,12 @@ int split_compact(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables, const ui
                           static_cast<hg_pair*>(c->mpairs.p), nb, &mr);
         if (rr != HG_OK) return rr;
         O[g].n = mr.n_out;
-        O[g].exact = mr.table;
+        // table 3: sorted input, the parallel merge redone after a look-back
+        // wait over its budget -- the slice is good
+        O[g].exact = mr.table == 1 || mr.table == 2;
+        O[g].redos = mr.table == 3 ? mr.index : 0;
         stamp(g, 2);
-        if (mr.table) return (int)HG_OK;  // not range-separable: decided after the join
+        if (O[g].exact) return (int)HG_OK;  // not range-separable: decided after the join
         uint8_t* dst = dsts ? dsts[g] : nullptr;
         uint64_t cap = dsts ? caps[g] : ab;
         if (!dsts) {
@@ -982,7 +994,7 @@ int hg_multi_compact_host(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
     }
     const uint64_t total = OB[nrange], nrec = RB[nrange];
     if (out_len) *out_len = total;
-    if (result) *result = hg_merge_result{nrec, HG_OK, 0, 0};
+    if (result) *result = split_result(O, nrec);
     if (total > cap) return HG_ERR_CAPACITY;
     const uint64_t nb = h_blocks ? (nrec + block_stride - 1) / block_stride : 0;
     std::vector<uint64_t> bpos(nb + 1, 0);
@@ -1099,7 +1111,7 @@ int hg_multi_compact_dev(hg_ctx* const* ctxs, uint32_t nctx, uint32_t ntables,
         out_recs[g] = O[g].n;
         nrec += O[g].n;
     }
-    if (result) *result = hg_merge_result{nrec, HG_OK, 0, 0};
+    if (result) *result = split_result(O, nrec);
     return HG_OK;
 }
 

@@ -170,6 +170,8 @@ Knob g_knobs[] = {
     {"HG_MERGE_KWAY", 0, false},         // 1: the one-pass k-way merge (3..KW_MAX runs)
     {"HG_MERGE_SERIAL", 0, false},       // 1: the reference loop (rank path), 2: the round-2 loop
     {"HG_MERGE_TEST_EPOCH_FAIL", 0, false},  // test hook: epoch k reports a failure
+    {"HG_MERGE_TEST_LB_EXPIRE", 0, false},   // test hook: the first merge's final-round tile k
+                                             // acts as if its look-back wait ran over budget
     {"HG_RANK_NOPACK", 0, false},        // 1: rank path with plain ranks at any size
     {"HG_DEBUG_POISON", 0, false},       // 1: new device buffers filled with 0xA5 (diagnostics)
 };
@@ -314,6 +316,20 @@ int hg_ctx_synchronize(hg_ctx* c) {
     return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }
 
+// A stream being captured into a graph: calls on it must not lean on the
+// host's record of which control half a previous call left clean (a replay
+// always reuses the half captured, and the clearing kernels of the other half
+// run only at replay), so they capture their own memset and mark both halves
+// unknown.  Entry points with host staging or syncs refuse to be captured.
+static bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return st != hipStreamCaptureStatusNone;
+}
+
 // The single-table decode's two control regions (hg_ctx::dctl) for a table
 // of len bytes; a new allocation holds nothing known to be zero.
 static int ensure_dctl(hg_ctx* c, uint64_t len) {
@@ -331,6 +347,33 @@ int hg_ctx_reserve(hg_ctx* c, uint64_t max_sst_bytes, uint64_t max_pairs) {
     int r = ensure(c, c->ws, need);
     if (r == HG_OK && max_sst_bytes) r = ensure_dctl(c, max_sst_bytes);
     if (r == HG_OK && max_pairs) r = ensure(c, c->recoff, max_pairs * sizeof(uint64_t));
+    if (r == HG_OK && max_pairs) {  // the encode's group-sum halves
+        uint64_t first = 0, ng = 0;
+        hgk_encode_group_sums(max_pairs, &first, &ng);
+        const uint64_t gneed = 2 * ((ng * 8 + 255) & ~(uint64_t)255);
+        if (c->egs.bytes < gneed) {
+            c->egs_clean[0] = c->egs_clean[1] = 0;
+            r = ensure(c, c->egs, gneed);
+        }
+    }
+    if (r == HG_OK && max_sst_bytes) {  // a one-table batched decode's control + staging
+        const uint64_t ctot = (hgk_decode_ctl_bytes(max_sst_bytes) + 255) & ~255ull;
+        const uint64_t sbh = (hgk_decode_multi_stage_bytes(1) + 255) & ~(uint64_t)255;
+        if (c->bctl.bytes < 2 * ctot) {
+            c->bctl_off[0].clear();
+            c->bctl_off[1].clear();
+            r = ensure(c, c->bctl, 2 * ctot);
+        }
+        if (r == HG_OK && c->bstage_d.bytes < 2 * sbh) {
+            c->bstage_shadow[0].clear();
+            c->bstage_shadow[1].clear();
+            r = ensure(c, c->bstage_d, 2 * sbh);
+        }
+        if (r == HG_OK && ensure_pin(c->bstage, hgk_decode_multi_stage_bytes(1)) != HG_OK)
+            r = HG_HIP_FAIL;
+        if (r == HG_OK && ensure(c, c->bws, (hgk_decode_workspace_bytes(max_sst_bytes) + 255) & ~255ull) != HG_OK)
+            r = HG_HIP_FAIL;
+    }
     return r;
 }
 
@@ -354,12 +397,13 @@ int hg_decode_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* 
     const uint64_t half = c->dctl.bytes / 2 & ~(uint64_t)255;
     char* base = static_cast<char*>(c->dctl.p);
     const int cur = c->dctl_cur;
+    const bool cap_mode = capturing(c->stream);
     uint64_t zeroed = 0;
     r = hgk_decode_launch_ctl(d_sst, len, d_spans, cap, d_result, c->ws.p, base + cur * half,
-                              c->dctl_clean[cur], base + (1 - cur) * half, half, &zeroed,
-                              c->stream);
+                              cap_mode ? 0 : c->dctl_clean[cur], base + (1 - cur) * half, half,
+                              &zeroed, c->stream);
     c->dctl_clean[cur] = 0;  // this call's statuses
-    c->dctl_clean[1 - cur] = r == HG_OK ? zeroed : 0;
+    c->dctl_clean[1 - cur] = r == HG_OK && !cap_mode ? zeroed : 0;
     c->dctl_cur = 1 - cur;
     return r;
 }
@@ -501,6 +545,8 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
         if (lens[i] >= kMaxLen) return HG_ERR_TOO_LARGE;
     }
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    // pinned argument staging (re-read at a replay) and host-side shadows
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     if (hgk_knob("HG_DECODE_BATCH", 0) != 1)
         return batch_one_launch(c, ntables, d_tables, lens, d_spans, caps, d_results, 0, nullptr);
     int fan = (int)hgk_knob("HG_DECODE_STREAMS", 4);
@@ -921,14 +967,16 @@ static int encode_dev_async_ex(hg_ctx* c, const uint8_t* d_arena, const hg_pair*
     const uint64_t half = c->egs.bytes / 2 & ~(uint64_t)255;
     char* base = static_cast<char*>(c->egs.p);
     const int cur = c->egs_cur;
+    const bool cap_mode = capturing(c->stream);
     uint64_t zeroed = 0;
     r = hgk_encode_launch_ctl(d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride, d_blocks,
                               d_result, reinterpret_cast<unsigned long long*>(c->ws.p),
-                              reinterpret_cast<uint64_t*>(base + cur * half), c->egs_clean[cur],
+                              reinterpret_cast<uint64_t*>(base + cur * half),
+                              cap_mode ? 0 : c->egs_clean[cur],
                               reinterpret_cast<uint64_t*>(base + (1 - cur) * half), half / 8,
                               &zeroed, c->stream);
     c->egs_clean[cur] = 0;
-    c->egs_clean[1 - cur] = r == HG_OK ? zeroed : 0;
+    c->egs_clean[1 - cur] = r == HG_OK && !cap_mode ? zeroed : 0;
     c->egs_cur = 1 - cur;
     return r;
 }
@@ -1126,6 +1174,7 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;  // pinned argument staging
     if (!c->mstage_ev && hipEventCreateWithFlags(&c->mstage_ev, hipEventDisableTiming) != hipSuccess)
         return HG_HIP_FAIL;
     if (ntables == 0) {  // min_by_key over no candidates: the reference panics (:213)

@@ -121,7 +121,9 @@ typedef struct hg_encode_result {
  * (every table strictly increasing); for input that is not, 1 the serial
  * loop on the device (hg_merge_dev_async, or many disorder points), 2 epochs
  * of the parallel merge cut at the tables' disorder points (the synchronous
- * entry points; index = the number of epochs). */
+ * entry points; index = the number of epochs), 3 the parallel merge redone
+ * after a look-back wait ran over its budget (a stalled grid; synchronous
+ * entry points; index = the merges run after the first, >= 1). */
 typedef struct hg_merge_result {
     uint64_t n_out;  /* merged records (tombstones included) */
     int32_t kind;
@@ -179,7 +181,17 @@ int hg_ctx_use_own_stream(hg_ctx* ctx);
 void* hg_ctx_stream(hg_ctx* ctx);
 int hg_ctx_synchronize(hg_ctx* ctx);
 /* Pre-size the device workspace so later calls never allocate
- * (keeps them graph-capturable and out of timed regions). */
+ * (keeps them graph-capturable and out of timed regions): the single-table
+ * decode and encode for tables of up to max_sst_bytes and max_pairs records,
+ * and a one-table batched decode.
+ *
+ * Graph capture: hg_decode_dev_async, hg_decode_range_dev_async,
+ * hg_encode_dev_async, hg_keyindex_build_dev_async and hg_lookup_dev_async
+ * may be captured on a stream (hg_ctx_set_stream) and replayed any number of
+ * times; under capture each clears its own control words (no state carried
+ * between calls).  hg_decode_batch_dev_async and hg_merge_dev_async stage
+ * their arguments through pinned host memory and return HG_ERR_INVALID_ARG
+ * on a capturing stream; the synchronous entry points cannot be captured. */
 int hg_ctx_reserve(hg_ctx* ctx, uint64_t max_sst_bytes, uint64_t max_pairs);
 
 /* ---- decode ----------------------------------------------------------

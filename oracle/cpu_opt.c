@@ -10,7 +10,7 @@
  * (a wrong guess is redone from the exact entry), as the GPU engine does.
  * Results are checked against hgo_decode / hgo_encode by the tests.
  */
-#define _POSIX_C_SOURCE 199309L
+#define _POSIX_C_SOURCE 200112L
 #include <pthread.h>
 #include <stdlib.h>
 #include <string.h>
@@ -81,29 +81,114 @@ static uint64_t guess_entry(const uint8_t* b, uint64_t len, uint64_t b0) {
     return len;
 }
 
+/* Every multi-threaded entry below spawns its workers first and starts the
+ * clock when all of them stand at a barrier (a service keeps a thread pool:
+ * thread creation is not codec work), then runs its phases between barriers
+ * with thread 0 (the caller) doing the short serial steps. */
 typedef struct {
     const uint8_t* b;
-    uint64_t len, lo, hi, guess, cnt, exit, err_pos;
+    uint64_t len, lo, hi, guess, cnt, exit, err_pos, dst;
     hg_span* out;
-    uint64_t cap;
-    int kind;
+    hg_span* spans;
+    uint64_t cap, total_cap;
+    int kind, place;
 } range_job;
 
-static void* range_worker(void* arg) {
+typedef struct {
+    pthread_barrier_t bar;
+    uint32_t nthreads;
+    void* jobs;
+    void (*phase[3])(void* job); /* run by every thread, a barrier after each */
+    void (*serial[3])(void* pool); /* thread 0 between phase i and i + 1 (nullable) */
+    size_t job_bytes;
+    double t0;
+} pool_run;
+
+typedef struct {
+    pool_run* p;
+    uint32_t t;
+} pool_arg;
+
+static void pool_body(pool_run* p, uint32_t t) {
+    pthread_barrier_wait(&p->bar);
+    if (t == 0) p->t0 = now_s();
+    pthread_barrier_wait(&p->bar);
+    for (int i = 0; i < 3 && p->phase[i]; ++i) {
+        p->phase[i]((char*)p->jobs + p->job_bytes * t);
+        pthread_barrier_wait(&p->bar);
+        if (t == 0 && p->serial[i]) p->serial[i](p);
+        pthread_barrier_wait(&p->bar);
+    }
+}
+
+static void* pool_thread(void* arg) {
+    pool_arg* a = (pool_arg*)arg;
+    pool_body(a->p, a->t);
+    return NULL;
+}
+
+/* Runs p over p->nthreads threads; returns seconds from the release of the
+ * start barrier to the end of the last phase. */
+static double pool_go(pool_run* p) {
+    pthread_t th[256];
+    pool_arg args[256];
+    pthread_barrier_init(&p->bar, NULL, p->nthreads);
+    for (uint32_t t = 1; t < p->nthreads; ++t) {
+        args[t].p = p;
+        args[t].t = t;
+        pthread_create(&th[t], NULL, pool_thread, &args[t]);
+    }
+    pool_body(p, 0);
+    const double t1 = now_s();
+    for (uint32_t t = 1; t < p->nthreads; ++t) pthread_join(th[t], NULL);
+    pthread_barrier_destroy(&p->bar);
+    return t1 - p->t0;
+}
+
+static void range_walk(void* arg) {
     range_job* j = (range_job*)arg;
     j->guess = j->lo ? guess_entry(j->b, j->len, j->lo) : 0;
     j->kind = walk_range(j->b, j->len, j->guess, j->hi, j->out, j->cap, &j->cnt, &j->exit,
                          &j->err_pos);
-    return NULL;
+}
+
+/* thread 0: the entry handoff in order (a range entered off its guess is
+ * walked again from the exact entry), then every range's output offset */
+static uint64_t g_dec_total, g_dec_bad;
+static void range_handoff(void* pool) {
+    pool_run* p = (pool_run*)pool;
+    range_job* jobs = (range_job*)p->jobs;
+    uint64_t total = 0, bad = 0;
+    for (uint32_t t = 0; t < p->nthreads; ++t) {
+        range_job* j = &jobs[t];
+        j->place = 0;
+        if (bad) continue;
+        if (t && j->guess != jobs[t - 1].exit) {
+            j->guess = jobs[t - 1].exit;
+            j->kind = walk_range(j->b, j->len, j->guess, j->hi, j->out, j->cap, &j->cnt, &j->exit,
+                                 &j->err_pos);
+        }
+        j->dst = total;
+        j->place = 1;
+        total += j->cnt;
+        if (j->kind != HG_OK) bad = 1;
+    }
+    g_dec_total = total;
+    g_dec_bad = bad;
+}
+
+static void range_place(void* arg) {
+    range_job* j = (range_job*)arg;
+    if (!j->place || j->dst >= j->total_cap) return;
+    const uint64_t m = j->dst + j->cnt <= j->total_cap ? j->cnt : j->total_cap - j->dst;
+    if (m) memcpy(j->spans + j->dst, j->out, m * sizeof(hg_span));
 }
 
 uint64_t hgo_mt_decode(const uint8_t* bytes, uint64_t len, hg_span* spans, uint64_t cap,
                        hg_span* scratch, uint32_t nthreads, double* seconds) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
-    range_job jobs[256];
-    pthread_t th[256];
-    const double t0 = now_s();
+    static range_job jobs[256];
     for (uint32_t t = 0; t < nthreads; ++t) {
         range_job* j = &jobs[t];
         j->b = bytes;
@@ -114,26 +199,20 @@ uint64_t hgo_mt_decode(const uint8_t* bytes, uint64_t len, hg_span* spans, uint6
          * len/16 + 2*nthreads + 2 spans, regions never overlap */
         j->out = scratch + j->lo / 16 + 2 * (uint64_t)t;
         j->cap = (j->hi - j->lo) / 16 + 2;
-        if (t) pthread_create(&th[t], NULL, range_worker, j);
+        j->spans = spans;
+        j->total_cap = cap;
     }
-    range_worker(&jobs[0]);
-    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
-    /* entry handoff in order; spans into place */
-    uint64_t total = 0, bad = 0;
-    for (uint32_t t = 0; t < nthreads; ++t) {
-        range_job* j = &jobs[t];
-        if (t && j->guess != jobs[t - 1].exit) { /* redo from the exact entry */
-            j->guess = jobs[t - 1].exit;
-            j->kind = walk_range(bytes, len, j->guess, j->hi, j->out, j->cap, &j->cnt, &j->exit,
-                                 &j->err_pos);
-        }
-        const uint64_t m = total + j->cnt <= cap ? j->cnt : (total < cap ? cap - total : 0);
-        if (m) memmove(spans + total, j->out, m * sizeof(hg_span));
-        total += j->cnt;
-        if (j->kind != HG_OK) { bad = 1; break; }
-    }
-    if (seconds) *seconds = now_s() - t0;
-    return bad ? UINT64_MAX : total;
+    pool_run p;
+    memset(&p, 0, sizeof p);
+    p.nthreads = nthreads;
+    p.jobs = jobs;
+    p.job_bytes = sizeof(range_job);
+    p.phase[0] = range_walk;
+    p.serial[0] = range_handoff;
+    p.phase[1] = range_place;
+    const double secs = pool_go(&p);
+    if (seconds) *seconds = secs;
+    return g_dec_bad ? UINT64_MAX : g_dec_total;
 }
 
 typedef struct {
@@ -143,15 +222,26 @@ typedef struct {
     uint8_t* out;
 } enc_job;
 
-static void* enc_size_worker(void* arg) {
+static void enc_size_worker(void* arg) {
     enc_job* j = (enc_job*)arg;
     uint64_t s = 0;
     for (uint64_t i = j->lo; i < j->hi; ++i) s += 16 + (uint64_t)j->pairs[i].klen + j->pairs[i].vlen;
     j->bytes = s;
-    return NULL;
 }
 
-static void* enc_copy_worker(void* arg) {
+static uint64_t g_enc_total;
+static void enc_bases(void* pool) {
+    pool_run* p = (pool_run*)pool;
+    enc_job* jobs = (enc_job*)p->jobs;
+    uint64_t base = 0;
+    for (uint32_t t = 0; t < p->nthreads; ++t) {
+        jobs[t].base = base;
+        base += jobs[t].bytes;
+    }
+    g_enc_total = base;
+}
+
+static void enc_copy_worker(void* arg) {
     enc_job* j = (enc_job*)arg;
     uint8_t* o = j->out + j->base;
     for (uint64_t i = j->lo; i < j->hi; ++i) {
@@ -163,36 +253,31 @@ static void* enc_copy_worker(void* arg) {
         if (v) memcpy(o + 16 + k, j->arena + p->val_off, v);
         o += 16 + k + v;
     }
-    return NULL;
 }
 
 uint64_t hgo_mt_encode(const uint8_t* arena, const hg_pair* pairs, uint64_t n, uint8_t* out,
                        uint32_t nthreads, double* seconds) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
-    enc_job jobs[256];
-    pthread_t th[256];
-    const double t0 = now_s();
+    static enc_job jobs[256];
     for (uint32_t t = 0; t < nthreads; ++t) {
         jobs[t].arena = arena;
         jobs[t].pairs = pairs;
         jobs[t].out = out;
         jobs[t].lo = n / nthreads * t;
         jobs[t].hi = t + 1 == nthreads ? n : n / nthreads * (t + 1);
-        if (t) pthread_create(&th[t], NULL, enc_size_worker, &jobs[t]);
     }
-    enc_size_worker(&jobs[0]);
-    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
-    uint64_t base = 0;
-    for (uint32_t t = 0; t < nthreads; ++t) {
-        jobs[t].base = base;
-        base += jobs[t].bytes;
-    }
-    for (uint32_t t = 1; t < nthreads; ++t) pthread_create(&th[t], NULL, enc_copy_worker, &jobs[t]);
-    enc_copy_worker(&jobs[0]);
-    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
-    if (seconds) *seconds = now_s() - t0;
-    return base;
+    pool_run p;
+    memset(&p, 0, sizeof p);
+    p.nthreads = nthreads;
+    p.jobs = jobs;
+    p.job_bytes = sizeof(enc_job);
+    p.phase[0] = enc_size_worker;
+    p.serial[0] = enc_bases;
+    p.phase[1] = enc_copy_worker;
+    const double secs = pool_go(&p);
+    if (seconds) *seconds = secs;
+    return g_enc_total;
 }
 
 /* CPU roofline (BASELINE.md CPU-roof): n bytes copied by nthreads threads,
@@ -203,19 +288,16 @@ typedef struct {
     uint64_t n;
 } cpy_job;
 
-static void* cpy_worker(void* arg) {
+static void cpy_worker(void* arg) {
     cpy_job* j = (cpy_job*)arg;
     memcpy(j->dst, j->src, j->n);
-    return NULL;
 }
 
 void hgo_mt_memcpy(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t nthreads,
                    double* seconds) {
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
-    cpy_job jobs[256];
-    pthread_t th[256];
-    const double t0 = now_s();
+    static cpy_job jobs[256];
     const uint64_t per = (n / nthreads + 63) & ~63ull;
     for (uint32_t t = 0; t < nthreads; ++t) {
         const uint64_t lo = per * t < n ? per * t : n;
@@ -223,9 +305,13 @@ void hgo_mt_memcpy(uint8_t* dst, const uint8_t* src, uint64_t n, uint32_t nthrea
         jobs[t].dst = dst + lo;
         jobs[t].src = src + lo;
         jobs[t].n = hi - lo;
-        if (t) pthread_create(&th[t], NULL, cpy_worker, &jobs[t]);
     }
-    cpy_worker(&jobs[0]);
-    for (uint32_t t = 1; t < nthreads; ++t) pthread_join(th[t], NULL);
-    if (seconds) *seconds = now_s() - t0;
+    pool_run p;
+    memset(&p, 0, sizeof p);
+    p.nthreads = nthreads;
+    p.jobs = jobs;
+    p.job_bytes = sizeof(cpy_job);
+    p.phase[0] = cpy_worker;
+    const double secs = pool_go(&p);
+    if (seconds) *seconds = secs;
 }
