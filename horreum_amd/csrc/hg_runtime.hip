@@ -316,11 +316,12 @@ int hg_ctx_synchronize(hg_ctx* c) {
     return hipStreamSynchronize(c->stream) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }
 
-// A stream being captured into a graph: calls on it must not lean on the
-// host's record of which control half a previous call left clean (a replay
-// always reuses the half captured, and the clearing kernels of the other half
-// run only at replay), so they capture their own memset and mark both halves
-// unknown.  Entry points with host staging or syncs refuse to be captured.
+// A stream being captured into a graph: every stream-ordered entry point
+// refuses it (HG_ERR_INVALID_ARG, nothing enqueued).  A context carries state
+// from call to call -- which control half the previous call's kernels left
+// clear, argument staging halves, pinned argument copies -- that a graph
+// replay would not follow, and a captured single-table decode faulted the
+// GPU on its first replay (round 6); capture is not supported.
 static bool capturing(hipStream_t s) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(s, &st) != hipSuccess) {
@@ -387,6 +388,7 @@ int hg_decode_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* 
     if (!c || !d_result || (len && !d_sst) || (cap && !d_spans)) return HG_ERR_INVALID_ARG;
     if (len >= kMaxLen) return HG_ERR_TOO_LARGE;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     if (len == 0)  // empty file: zero records (src/format.rs:54 loop never runs)
         return hipMemsetAsync(d_result, 0, sizeof(hg_decode_result), c->stream) == hipSuccess
                    ? HG_OK
@@ -397,13 +399,12 @@ int hg_decode_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, hg_span* 
     const uint64_t half = c->dctl.bytes / 2 & ~(uint64_t)255;
     char* base = static_cast<char*>(c->dctl.p);
     const int cur = c->dctl_cur;
-    const bool cap_mode = capturing(c->stream);
     uint64_t zeroed = 0;
     r = hgk_decode_launch_ctl(d_sst, len, d_spans, cap, d_result, c->ws.p, base + cur * half,
-                              cap_mode ? 0 : c->dctl_clean[cur], base + (1 - cur) * half, half,
-                              &zeroed, c->stream);
+                              c->dctl_clean[cur], base + (1 - cur) * half, half, &zeroed,
+                              c->stream);
     c->dctl_clean[cur] = 0;  // this call's statuses
-    c->dctl_clean[1 - cur] = r == HG_OK && !cap_mode ? zeroed : 0;
+    c->dctl_clean[1 - cur] = r == HG_OK ? zeroed : 0;
     c->dctl_cur = 1 - cur;
     return r;
 }
@@ -545,7 +546,6 @@ int hg_decode_batch_dev_async(hg_ctx* c, uint32_t ntables, const uint8_t* const*
         if (lens[i] >= kMaxLen) return HG_ERR_TOO_LARGE;
     }
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
-    // pinned argument staging (re-read at a replay) and host-side shadows
     if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     if (hgk_knob("HG_DECODE_BATCH", 0) != 1)
         return batch_one_launch(c, ntables, d_tables, lens, d_spans, caps, d_results, 0, nullptr);
@@ -858,6 +858,7 @@ int hg_decode_range_dev_async(hg_ctx* c, const uint8_t* d_sst, uint64_t len, uin
     if (stop > len) stop = len;
     if (begin > entry || begin > len || entry > len) return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     const uint64_t span = stop > begin ? stop - begin : 0;
     int r = ensure(c, c->ws, hgk_decode_workspace_bytes(span ? span : 1));
     if (r != HG_OK) return r;
@@ -941,6 +942,7 @@ static int encode_dev_async_ex(hg_ctx* c, const uint8_t* d_arena, const hg_pair*
     if (!c || !d_result || (n && !d_pairs) || (cap && !d_out)) return HG_ERR_INVALID_ARG;
     if (d_blocks && block_stride == 0) return HG_ERR_INVALID_ARG;  // slice::chunks(0) panics
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     if (n == 0)
         return hipMemsetAsync(d_result, 0, sizeof(hg_encode_result), c->stream) == hipSuccess
                    ? HG_OK
@@ -967,16 +969,14 @@ static int encode_dev_async_ex(hg_ctx* c, const uint8_t* d_arena, const hg_pair*
     const uint64_t half = c->egs.bytes / 2 & ~(uint64_t)255;
     char* base = static_cast<char*>(c->egs.p);
     const int cur = c->egs_cur;
-    const bool cap_mode = capturing(c->stream);
     uint64_t zeroed = 0;
     r = hgk_encode_launch_ctl(d_arena, d_pairs, n, d_out, cap, d_rec_off, block_stride, d_blocks,
                               d_result, reinterpret_cast<unsigned long long*>(c->ws.p),
-                              reinterpret_cast<uint64_t*>(base + cur * half),
-                              cap_mode ? 0 : c->egs_clean[cur],
+                              reinterpret_cast<uint64_t*>(base + cur * half), c->egs_clean[cur],
                               reinterpret_cast<uint64_t*>(base + (1 - cur) * half), half / 8,
                               &zeroed, c->stream);
     c->egs_clean[cur] = 0;
-    c->egs_clean[1 - cur] = r == HG_OK && !cap_mode ? zeroed : 0;
+    c->egs_clean[1 - cur] = r == HG_OK ? zeroed : 0;
     c->egs_cur = 1 - cur;
     return r;
 }
@@ -1174,7 +1174,7 @@ int merge_async(hg_ctx* c, uint32_t ntables, const uint8_t* d_arena, uint64_t ar
     if (!c || !d_result || (ntables && (!table_off || !d_spans || !counts)) || (cap && !d_out))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
-    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;  // pinned argument staging
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     if (!c->mstage_ev && hipEventCreateWithFlags(&c->mstage_ev, hipEventDisableTiming) != hipSuccess)
         return HG_HIP_FAIL;
     if (ntables == 0) {  // min_by_key over no candidates: the reference panics (:213)
@@ -1558,6 +1558,7 @@ int hg_keyindex_build_dev_async(hg_ctx* c, const uint8_t* d_table, uint64_t len,
                                 const hg_span* d_spans, uint64_t n, void* d_index) {
     if (!c || (n && (!d_table || !d_spans || !d_index))) return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     return hgk_keyindex_launch(d_table, len, d_spans, n, d_index, c->stream);
 }
 
@@ -1568,6 +1569,7 @@ int hg_lookup_dev_async(hg_ctx* c, const uint8_t* d_table, const hg_span* d_span
     if (!c || (nq && (!d_queries || !d_results)) || (n && nq && (!d_table || !d_spans || !d_index)))
         return HG_ERR_INVALID_ARG;
     if (set_dev(c) != HG_OK) return HG_HIP_FAIL;
+    if (capturing(c->stream)) return HG_ERR_INVALID_ARG;
     return hgk_lookup_launch(d_table, d_spans, d_index, n, block_stride, d_keys, d_queries, nq,
                              d_results, c->stream);
 }

@@ -181,17 +181,14 @@ int hg_ctx_use_own_stream(hg_ctx* ctx);
 void* hg_ctx_stream(hg_ctx* ctx);
 int hg_ctx_synchronize(hg_ctx* ctx);
 /* Pre-size the device workspace so later calls never allocate
- * (keeps them graph-capturable and out of timed regions): the single-table
+ * (keeps allocation out of timed regions): the single-table
  * decode and encode for tables of up to max_sst_bytes and max_pairs records,
  * and a one-table batched decode.
  *
- * Graph capture: hg_decode_dev_async, hg_decode_range_dev_async,
- * hg_encode_dev_async, hg_keyindex_build_dev_async and hg_lookup_dev_async
- * may be captured on a stream (hg_ctx_set_stream) and replayed any number of
- * times; under capture each clears its own control words (no state carried
- * between calls).  hg_decode_batch_dev_async and hg_merge_dev_async stage
- * their arguments through pinned host memory and return HG_ERR_INVALID_ARG
- * on a capturing stream; the synchronous entry points cannot be captured. */
+ * Graph capture is not supported: a context carries state from call to call
+ * (which control words the previous call's kernels left clear, argument
+ * staging), so every stream-ordered entry point returns HG_ERR_INVALID_ARG
+ * on a stream that is being captured and enqueues nothing. */
 int hg_ctx_reserve(hg_ctx* ctx, uint64_t max_sst_bytes, uint64_t max_pairs);
 
 /* ---- decode ----------------------------------------------------------

@@ -162,3 +162,39 @@ def test_cfg5_full_share_property(engine):
     want = rows.index_select(0, want_rows).view(-1)
     assert got.numel() == want.numel()
     assert torch.equal(got, want)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("nctx", [1, 4])
+def test_cfg4_all_256_tables_one_device(engine, nctx):
+    """BASELINE config 4 at its FULL table count on one device: 256 tables x
+    64 MiB (16 GiB; 16 B keys, values uniform in 8 B..4 KiB, 5 % tombstones)
+    from host memory through hg_multi_decode_host (SSTableManager::new
+    opening a directory, src/sstable/manager.rs:47-55) with `nctx` contexts
+    sharing the GPU -- table i on context i % nctx, batched decode chains per
+    group under the device byte budget.  Every span of every table against
+    the oracle (src/format.rs:50-77).  (the largest batched decode
+    tested had been 32 tables, and round 5's staging bug depended on the
+    table count.)"""
+    import torch
+    from horreum_amd import synth
+    from horreum_amd.multi import MultiEngine
+    hosts = []
+    for t in range(256):
+        v = synth.mixed_table_vlens(64 << 20, 8, 4096, 0.05, seed=4 + t)
+        keys = np.arange(v.size, dtype=np.uint64) * 7 + t
+        buf, _ = synth.keyed_table(keys, v, seed=4 + t, device=engine.device)
+        hosts.append(buf.cpu().numpy())
+        del buf
+    torch.cuda.empty_cache()
+    assert sum(h.size for h in hosts) > 16 * 10**9
+    m = MultiEngine([engine.device.index] * nctx)
+    try:
+        outs = m.decode_tables(hosts)
+    finally:
+        m.close()
+    assert len(outs) == 256
+    for i, (h, o) in enumerate(zip(hosts, outs)):
+        want, wn, wk, _, _ = oracle.decode(h)
+        assert (o.n, o.kind, wk) == (wn, 0, 0), i
+        assert np.array_equal(o.spans, want), i

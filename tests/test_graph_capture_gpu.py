@@ -1,11 +1,9 @@
 """the single-table decode and the encode keep per-context
-state between calls (which control half the previous call left clean).  A
-call captured into a HIP graph must not lean on it: every replay reuses the
-half captured.  Each entry point captured once and replayed several times,
-with eager calls on the same context in between (they flip the halves), every
-result against the oracle (src/format.rs:23-77).  Also: the entry points
-that stage arguments through pinned memory refuse a capturing stream, and
-hg_ctx_reserve leaves nothing for the first calls to allocate."""
+state between calls (which control half the previous call's kernels left
+clear), which a HIP-graph replay would not follow.  Capture is therefore
+refused by every stream-ordered entry point (HG_ERR_INVALID_ARG, nothing
+enqueued).  ADVICE r5 (medium): after hg_ctx_reserve the first encode and a
+one-table batched decode allocate nothing."""
 import ctypes
 
 import numpy as np
@@ -22,136 +20,69 @@ def _table(n, seed):
     return arena, pairs, oracle.encode(arena, pairs)[0]
 
 
-def _check_decode(eng, spans, res, want):
-    ws, wn, wk, _, _ = want
-    r = res[:24].cpu().numpy()
-    assert int(r[:8].view("<u8")[0]) == wn and int(r[8:12].view("<i4")[0]) == wk == 0
-    assert np.array_equal(eng.spans_to_numpy(spans, wn), ws)
-
-
-def test_decode_capture_replay(knobs):
+def test_every_stream_ordered_entry_point_refuses_capture():
+    """Graph capture is not supported (a context carries state between calls
+    that a replay would not follow; round 6 saw a captured decode fault on
+    its first replay): on a capturing stream every stream-ordered entry point
+    returns HG_ERR_INVALID_ARG and enqueues nothing -- the capture holds only
+    the caller's own work, and the context works normally afterwards."""
     import torch
     from horreum_amd.engine import Engine
-    _, _, table = _table(60_000, 901)  # ~20 MB: many pre-pass batches, look-back across them
+    arena, pairs, table = _table(2_000, 903)
     want = oracle.decode(table)
     eng = Engine(0)
     try:
-        eng.reserve(table.size, 0)
         d = eng.to_device(table)
+        da, dp = eng.to_device(arena), eng.to_device(pairs.view(np.uint8))
         cap = table.size // 16
-        spans, res = eng.empty(cap * 16), eng.empty(64)
-        s = torch.cuda.Stream()
-        # an eager warm-up call on the capture stream
-        with torch.cuda.stream(s):
-            eng.set_stream(s)
-            eng.decode_dev_async(d, table.size, spans, cap, res)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
-            eng.set_stream(torch.cuda.current_stream())
-            eng.decode_dev_async(d, table.size, spans, cap, res)
-        eng.set_stream(s)
-        for i in range(4):
-            spans.fill_(0xEE)
-            res.fill_(0xEE)
-            g.replay()
-            torch.cuda.synchronize()
-            _check_decode(eng, spans, res, want)
-            if i % 2 == 0:  # an eager call between replays flips the halves
-                spans.fill_(0xEE)
-                with torch.cuda.stream(s):
-                    eng.decode_dev_async(d, table.size, spans, cap, res)
-                torch.cuda.synchronize()
-                _check_decode(eng, spans, res, want)
-        del g
-    finally:
-        eng.close()
-
-
-def test_encode_capture_replay():
-    import torch
-    from horreum_amd.engine import Engine
-    arena, pairs, want = _table(80_000, 902)
-    _, _, wblocks, _ = oracle.encode(arena, pairs, block_stride=7)
-    eng = Engine(0)
-    try:
-        n = pairs.size
-        eng.reserve(0, n)
-        da = eng.to_device(arena)
-        dp = eng.to_device(pairs.view(np.uint8))
-        out = eng.empty(want.size)
-        nb = (n + 6) // 7
-        blocks = eng.empty(nb * 24)
-        res = eng.empty(64)
-        s = torch.cuda.Stream()
-        with torch.cuda.stream(s):
-            eng.set_stream(s)
-            eng.encode_dev_async(da, dp, n, out, want.size, None, 7, blocks, res)
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
-            eng.set_stream(torch.cuda.current_stream())
-            eng.encode_dev_async(da, dp, n, out, want.size, None, 7, blocks, res)
-        eng.set_stream(s)
-        for i in range(4):
-            out.fill_(0)
-            blocks.fill_(0)
-            g.replay()
-            torch.cuda.synchronize()
-            r = res[:16].cpu().numpy()
-            assert int(r[:8].view("<u8")[0]) == want.size and int(r[8:12].view("<i4")[0]) == 0
-            assert np.array_equal(out.cpu().numpy(), want), i
-            assert np.array_equal(blocks.cpu().numpy().view("<u8").reshape(-1, 3),
-                                  wblocks.view("<u8").reshape(-1, 3)), i
-            if i % 2 == 0:
-                out.fill_(0)
-                with torch.cuda.stream(s):
-                    eng.encode_dev_async(da, dp, n, out, want.size, None, 7, blocks, res)
-                torch.cuda.synchronize()
-                assert np.array_equal(out.cpu().numpy(), want), i
-        del g
-    finally:
-        eng.close()
-
-
-def test_staged_entry_points_refuse_capture():
-    """hg_decode_batch_dev_async and hg_merge_dev_async stage their
-    arguments through pinned host memory (re-read at a replay): they return
-    HG_ERR_INVALID_ARG on a capturing stream and enqueue nothing."""
-    import torch
-    from horreum_amd.engine import Engine
-    _, _, table = _table(2_000, 903)
-    eng = Engine(0)
-    try:
-        d = eng.to_device(table)
-        spans, res = eng.empty(table.size), eng.empty(64)
+        spans, res, out = eng.empty(table.size), eng.empty(128), eng.empty(table.size)
+        idx = eng.empty(64)
         lib = eng.lib
+        vp = ctypes.c_void_p
         tp = (ctypes.c_void_p * 1)(d.data_ptr())
         ln = (ctypes.c_uint64 * 1)(table.size)
         sp = (ctypes.c_void_p * 1)(spans.data_ptr())
-        cp = (ctypes.c_uint64 * 1)(table.size // 16)
+        cp = (ctypes.c_uint64 * 1)(cap)
+        toff = (ctypes.c_uint64 * 1)(0)
+        cnt = (ctypes.c_uint64 * 1)(10)
         s = torch.cuda.Stream()
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        rcs = {}
         with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
             eng.set_stream(torch.cuda.current_stream())
-            rc_b = lib.hg_decode_batch_dev_async(eng.ctx, 1, ctypes.cast(tp, ctypes.c_void_p),
-                                                 ctypes.cast(ln, ctypes.c_void_p),
-                                                 ctypes.cast(sp, ctypes.c_void_p),
-                                                 ctypes.cast(cp, ctypes.c_void_p),
-                                                 ctypes.c_void_p(res.data_ptr()))
-            toff = (ctypes.c_uint64 * 1)(0)
-            cnt = (ctypes.c_uint64 * 1)(10)
-            rc_m = lib.hg_merge_dev_async(eng.ctx, 1, ctypes.c_void_p(d.data_ptr()), table.size,
-                                          ctypes.cast(toff, ctypes.c_void_p),
-                                          ctypes.cast(sp, ctypes.c_void_p),
-                                          ctypes.cast(cnt, ctypes.c_void_p),
-                                          ctypes.c_void_p(spans.data_ptr()), 10,
-                                          ctypes.c_void_p(res.data_ptr()))
-            res.zero_()  # something to capture
-        eng.set_stream(None)
-        assert (rc_b, rc_m) == (-1, -1)
+            ctx = eng.ctx
+            rcs["decode"] = lib.hg_decode_dev_async(ctx, vp(d.data_ptr()), table.size,
+                                                    vp(spans.data_ptr()), cap, vp(res.data_ptr()))
+            rcs["range"] = lib.hg_decode_range_dev_async(ctx, vp(d.data_ptr()), table.size, 0,
+                                                         table.size, 0, vp(spans.data_ptr()), cap,
+                                                         vp(res.data_ptr()))
+            rcs["encode"] = lib.hg_encode_dev_async(ctx, vp(da.data_ptr()), vp(dp.data_ptr()),
+                                                    pairs.size, vp(out.data_ptr()), table.size,
+                                                    None, 0, None, vp(res.data_ptr()))
+            rcs["batch"] = lib.hg_decode_batch_dev_async(ctx, 1, ctypes.cast(tp, vp),
+                                                         ctypes.cast(ln, vp), ctypes.cast(sp, vp),
+                                                         ctypes.cast(cp, vp), vp(res.data_ptr()))
+            rcs["merge"] = lib.hg_merge_dev_async(ctx, 1, vp(d.data_ptr()), table.size,
+                                                  ctypes.cast(toff, vp), ctypes.cast(sp, vp),
+                                                  ctypes.cast(cnt, vp), vp(out.data_ptr()), 10,
+                                                  vp(res.data_ptr()))
+            rcs["keyindex"] = lib.hg_keyindex_build_dev_async(ctx, vp(d.data_ptr()), table.size,
+                                                              vp(spans.data_ptr()), 1,
+                                                              vp(idx.data_ptr()))
+            rcs["lookup"] = lib.hg_lookup_dev_async(ctx, vp(d.data_ptr()), vp(spans.data_ptr()),
+                                                    vp(idx.data_ptr()), 1, 0, vp(d.data_ptr()),
+                                                    vp(idx.data_ptr()), 1, vp(res.data_ptr()))
+            res.zero_()  # the caller's own work: all the graph holds
+        eng.set_stream(torch.cuda.current_stream())
+        assert rcs == {k: -1 for k in rcs}, rcs
+        g.replay()
+        torch.cuda.synchronize()
         del g
+        # the context is usable after the refused capture
+        out_d = eng.decode_dev(d, table.size)
+        assert (out_d.n, out_d.kind) == (want[1], 0)
+        assert np.array_equal(eng.spans_to_numpy(out_d.spans, out_d.n), want[0])
     finally:
         eng.close()
 

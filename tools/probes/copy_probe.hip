@@ -48,6 +48,54 @@ __global__ __launch_bounds__(256) void copy_tile(const u32x4* __restrict__ src, 
     }
 }
 
+// each workgroup copies one contiguous chunk (no grid stride), U loads in
+// flight per lane, TH threads per workgroup
+template <int U, int TH, bool NT>
+__global__ __launch_bounds__(TH) void copy_chunk(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                 uint64_t n16, uint64_t per) {
+    const uint64_t b = (uint64_t)blockIdx.x * per;
+    const uint64_t e = b + per < n16 ? b + per : n16;
+    for (uint64_t i = b + threadIdx.x; i < e; i += (uint64_t)TH * U) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + (uint64_t)u * TH;
+            if (j < e) v[u] = NT ? __builtin_nontemporal_load(src + j) : src[j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + (uint64_t)u * TH;
+            if (j < e) {
+                if (NT) __builtin_nontemporal_store(v[u], dst + j);
+                else dst[j] = v[u];
+            }
+        }
+    }
+}
+
+// loads nontemporal, stores default (or the reverse): which side the policy helps
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void copy_mixed(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                  uint64_t n16) {
+    const uint64_t stride = (uint64_t)gridDim.x * 256 * U;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; i < n16; i += stride) {
+        u32x4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + (uint64_t)u * 256;
+            if (j < n16) v[u] = NTL ? __builtin_nontemporal_load(src + j) : src[j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t j = i + (uint64_t)u * 256;
+            if (j < n16) {
+                if (NTS) __builtin_nontemporal_store(v[u], dst + j);
+                else dst[j] = v[u];
+            }
+        }
+    }
+}
+
 template <typename F>
 static float time_it(F f) {
     hipEvent_t a, b;
@@ -96,6 +144,24 @@ int main() {
         rep("tile 19x1KiB default", time_it([&] { copy_tile<19, false><<<(uint32_t)nb19, 256>>>(src, dst, n16); }));
         const uint64_t nb76 = (n16 + 256 * 76 - 1) / (256 * 76);
         rep("tile 76x1KiB nt", time_it([&] { copy_tile<76, true><<<(uint32_t)nb76, 256>>>(src, dst, n16); }));
+    }
+    for (int g : {256, 512, 1024, 2048}) {  // contiguous chunk per workgroup
+        char nm[64];
+        const uint64_t per = (n16 + g - 1) / g;
+#define C(U, TH, NT)                                                                          \
+        snprintf(nm, sizeof nm, "chunk %d U=%d th=%d nt=%d", g, U, TH, NT);                  \
+        rep(nm, time_it([&] { copy_chunk<U, TH, NT><<<g, TH>>>(src, dst, n16, per); }));
+        C(4, 256, true) C(8, 256, true) C(16, 256, true) C(4, 512, true) C(8, 512, true)
+        C(4, 1024, true) C(8, 1024, false)
+#undef C
+    }
+    for (int g : {4096, 8192}) {
+        char nm[64];
+#define M(U, L, S)                                                                            \
+        snprintf(nm, sizeof nm, "grid %d U=%d ntl=%d nts=%d", g, U, L, S);                     \
+        rep(nm, time_it([&] { copy_mixed<U, L, S><<<g, 256>>>(src, dst, n16); }));
+        M(8, true, false) M(8, false, true) M(16, true, true)
+#undef M
     }
     CHECK(hipFree(src));
     CHECK(hipFree(dst));

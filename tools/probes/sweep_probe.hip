@@ -106,6 +106,150 @@ __global__ __launch_bounds__(256) void glds_sweep_kernel(const uint8_t* src, uin
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Round 6: the same stream cut into CH-byte chunks (CH = 4 or 8 KiB) in a
+// ring of NBUF chunks (NBUF * CH = 32 KiB: the pre-pass's two piece buffers),
+// NBUF - 1 chunks in flight while one is read: more bytes in flight per
+// workgroup than two whole-piece buffers at the same LDS.
+template <int NBUF, int CH>
+__global__ __launch_bounds__(256) void ring_sweep_kernel(const uint8_t* src, uint32_t ppb,
+                                                         unsigned long long* out) {
+    extern __shared__ u32x4 buf[];  // NBUF * CH bytes
+    constexpr uint32_t WPC = CH / 1024 / 4;  // DMA instructions per wave per chunk (1 KiB each)
+    const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
+    const uint64_t base = (uint64_t)blockIdx.x * ppb * PIECE;
+    const uint32_t nch = ppb * (PIECE / CH);
+    auto issue = [&](uint32_t k) {
+        const uint8_t* s = src + base + (uint64_t)k * CH;
+        uint8_t* d = reinterpret_cast<uint8_t*>(buf) + (k % NBUF) * CH;
+#pragma unroll
+        for (uint32_t q = 0; q < WPC; ++q) {
+            const uint32_t g0 = q * 256 + wid * 64;
+            __builtin_amdgcn_global_load_lds(static_cast<const void*>(s + (uint64_t)(g0 + lane) * 16),
+                                             (__attribute__((address_space(3))) void*)(d + g0 * 16), 16, 0, 2);
+        }
+    };
+    for (uint32_t k = 0; k + 1 < NBUF && k < nch; ++k) issue(k);
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < nch; ++k) {
+        if (k + NBUF - 1 < nch) {
+            issue(k + NBUF - 1);
+            if (WPC * (NBUF - 1) == 7) __asm__ volatile("s_waitcnt vmcnt(7)" ::: "memory");
+            else if (WPC * (NBUF - 1) == 6) __asm__ volatile("s_waitcnt vmcnt(6)" ::: "memory");
+            else if (WPC * (NBUF - 1) == 4) __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else if (WPC * (NBUF - 1) == 3) __asm__ volatile("s_waitcnt vmcnt(3)" ::: "memory");
+            else __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const u32x4 a = buf[(k % NBUF) * (CH / 16) + (tid * 7 + k) % (CH / 16)];
+        acc ^= a.x ^ a.w;
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+// Round 6: the pre-pass geometry (two 16 KiB piece buffers, 40 KB, 4 per CU)
+// plus an L2 warm-up of piece k + PFD: waves 0 and 1 issue one 4-byte
+// default-policy LDS-DMA per 128-byte line of it into a 512-byte LDS sink (no
+// VGPR holds the data), so the lines are on their way to L2 before the
+// piece's own DMA asks for them.
+template <int PFD>
+__global__ __launch_bounds__(256) void glds_pf_sweep_kernel(const uint8_t* src, uint32_t ppb,
+                                                            unsigned long long* out) {
+    extern __shared__ u32x4 buf[];  // 2 * PIECE + 512 sink
+    const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
+    const uint64_t base = (uint64_t)blockIdx.x * ppb * PIECE;
+    uint8_t* sink = reinterpret_cast<uint8_t*>(buf) + 2 * PIECE;
+    auto issue = [&](uint32_t k) {
+        const uint8_t* s = src + base + (uint64_t)k * PIECE;
+        uint8_t* d = reinterpret_cast<uint8_t*>(buf) + (k % 2) * PIECE;
+#pragma unroll
+        for (uint32_t q = 0; q < GPT; ++q) {
+            const uint32_t g0 = q * 256 + wid * 64;
+            __builtin_amdgcn_global_load_lds(static_cast<const void*>(s + (uint64_t)(g0 + lane) * 16),
+                                             (__attribute__((address_space(3))) void*)(d + g0 * 16), 16, 0, 2);
+        }
+    };
+    auto warm = [&](uint32_t k) {  // waves 0, 1: 128 lines of 128 B
+        if (wid < 2) {
+            const uint8_t* s = src + base + (uint64_t)k * PIECE + (uint64_t)(tid * 128);
+            __builtin_amdgcn_global_load_lds(static_cast<const void*>(s),
+                                             (__attribute__((address_space(3))) void*)(sink + wid * 256), 4, 0, 0);
+        }
+    };
+    issue(0);
+    for (uint32_t k = 1; k < PFD && k < ppb; ++k) warm(k);
+    uint32_t acc = 0;
+    for (uint32_t k = 0; k < ppb; ++k) {
+        if (k + 1 < ppb) {
+            issue(k + 1);
+            const bool pf = k + PFD < ppb;
+            if (pf) warm(k + PFD);
+            if (pf && wid < 2) __asm__ volatile("s_waitcnt vmcnt(5)" ::: "memory");
+            else __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory");
+        } else {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const u32x4 a = buf[(k % 2) * (PIECE / 16) + (tid * 7 + k) % (PIECE / 16)];
+        acc ^= a.x ^ a.w;
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+template <int PFD>
+void run_pf(const uint8_t* d, uint64_t len, uint32_t ppb, unsigned long long* out, const char* name) {
+    const uint32_t grid = (uint32_t)(len / PIECE) / ppb;
+    const size_t lds = 40960;
+    CHECK(hipFuncSetAttribute((const void*)glds_pf_sweep_kernel<PFD>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int occ = 0;
+    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, glds_pf_sweep_kernel<PFD>, 256, lds));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    float best = 1e9f;
+    for (int r = 0; r < 8; ++r) {
+        CHECK(hipEventRecord(e0));
+        glds_pf_sweep_kernel<PFD><<<grid, 256, lds>>>(d, ppb, out);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0 && ms < best) best = ms;
+    }
+    printf("%-26s ppb=%3u grid=%6u occ/CU=%2d  %.4f ms  %.0f GB/s\n", name, ppb, grid, occ, best,
+           (double)grid * ppb * PIECE / best / 1e6);
+}
+
+template <int NBUF, int CH>
+void run_ring(const uint8_t* d, uint64_t len, uint32_t ppb, unsigned long long* out, const char* name,
+              size_t pad) {
+    const uint32_t grid = (uint32_t)(len / PIECE) / ppb;
+    const size_t lds = (size_t)NBUF * CH + pad;
+    CHECK(hipFuncSetAttribute((const void*)ring_sweep_kernel<NBUF, CH>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int occ = 0;
+    CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, ring_sweep_kernel<NBUF, CH>, 256, lds));
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    float best = 1e9f;
+    for (int r = 0; r < 8; ++r) {
+        CHECK(hipEventRecord(e0));
+        ring_sweep_kernel<NBUF, CH><<<grid, 256, lds>>>(d, ppb, out);
+        CHECK(hipEventRecord(e1));
+        CHECK(hipEventSynchronize(e1));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, e0, e1));
+        if (r > 0 && ms < best) best = ms;
+    }
+    printf("%-26s ppb=%3u grid=%6u occ/CU=%2d  %.4f ms  %.0f GB/s\n", name, ppb, grid, occ, best,
+           (double)grid * ppb * PIECE / best / 1e6);
+}
+
 template <int NBUF, int AUX, int ROT = 0>
 void run_glds(const uint8_t* d, uint64_t len, uint32_t ppb, unsigned long long* out, const char* name,
               size_t pad = 0) {
@@ -193,6 +337,17 @@ int main() {
             if (r > 0 && ms < best) best = ms;
         }
         printf("flat grid-stride           grid=%6d  %.4f ms  %.0f GB/s\n", g, best, len / best / 1e6);
+    }
+    if (getenv("SWEEP_RING")) {  // round 6: chunk rings at the pre-pass's 40 KB / 4 per CU
+        for (int rep = 0; rep < 2; ++rep) {
+            run_glds<2, 2>(d, len, 64, out, "glds x2 nt 40KB", 40960 - 2 * PIECE);
+            run_ring<4, 8192>(d, len, 64, out, "ring 4x8KiB 40KB", 40960 - 4 * 8192);
+            run_ring<8, 4096>(d, len, 64, out, "ring 8x4KiB 40KB", 40960 - 8 * 4096);
+            run_ring<3, 8192>(d, len, 64, out, "ring 3x8KiB 40KB", 40960 - 3 * 8192);
+            run_pf<2>(d, len, 64, out, "glds x2 + L2 warm k+2");
+            run_pf<3>(d, len, 64, out, "glds x2 + L2 warm k+3");
+        }
+        return 0;
     }
     if (getenv("SWEEP_ROT")) {  // the pre-pass geometry (64 pieces, 40 KB), lockstep vs rotated
         for (int rep = 0; rep < 3; ++rep) {

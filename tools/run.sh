@@ -14,6 +14,8 @@
 #   merge       tools/merge_epochs.py (sorted / epochs / rank-path timings)
 #   compact     tools/compact_leg.py (the bench's cfg 5 scaled leg alone)
 #   cfg4diag    tools/spec_diag.py on cfg 4's tables at the batched geometry
+#   two         tools/two_share.sh base (two share-leg compactions at once)
+#   probes      tools/probes/copy_probe and sweep_probe (SWEEP_RING=1)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 T=${TAG:-run}
 fail() { echo "== $1 failed"; tail -${2:-20} "$3"; exit 1; }
@@ -67,6 +69,14 @@ for step in "$@"; do
       CFG4_TABLES=${CFG4_TABLES:-32} HG_DECODE_BP=64 HG_DECODE_SBP=64 timeout -k 10 400 \
         python3 tools/spec_diag.py cfg4 > gpurun_out/${T}_cfg4diag.log 2>&1 || fail cfg4diag 5 gpurun_out/${T}_cfg4diag.log
       grep -v amdgpu.ids gpurun_out/${T}_cfg4diag.log ;;
+    two)  # two processes compacting the cfg 5 share at once on one GPU
+      timeout -k 10 600 bash tools/two_share.sh base > gpurun_out/${T}_two.log 2>&1 || fail two 20 gpurun_out/${T}_two.log
+      cat gpurun_out/${T}_two.log ;;
+    probes)  # copy ceiling (encode) and the pre-pass stream geometry
+      timeout -k 10 300 tools/probes/copy_probe > gpurun_out/${T}_copy_probe.log 2>&1 || fail probes 5 gpurun_out/${T}_copy_probe.log
+      SWEEP_RING=1 timeout -k 10 300 tools/probes/sweep_probe > gpurun_out/${T}_sweep_ring.log 2>&1 ||
+        fail probes 5 gpurun_out/${T}_sweep_ring.log
+      cat gpurun_out/${T}_copy_probe.log gpurun_out/${T}_sweep_ring.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

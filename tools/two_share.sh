@@ -11,7 +11,7 @@ for n in "$@"; do
   B=$!
   wait $A; ra=$?; wait $B; rb=$?
   for x in a b; do
-    echo "== $n $x: $(grep '^{' gpurun_out/two_${n}_$x.log | tail -1 | python3 -c 'import json,sys; l=json.loads(sys.stdin.read()); print(l["ms"], l["times_ms"], l["status"], l.get("parity_bytes_ok"))')"
+    echo "== $n $x: $(grep '^{' gpurun_out/two_${n}_$x.log | tail -1 | python3 -c 'import json,sys; l=json.loads(sys.stdin.read()); print(l["ms"], l["times_ms"], l["status"], l.get("parity_bytes_ok"), l.get("merge_paths"))')"
   done
   [ $ra -eq 0 ] && [ $rb -eq 0 ] || exit 1
 done
