@@ -136,6 +136,19 @@ void* hgk_ctx_decode_ctl(hg_ctx* c) {
     const uint64_t half = c->dctl.bytes / 2 & ~(uint64_t)255;
     return static_cast<char*>(c->dctl.p) + (1 - c->dctl_cur) * half;
 }
+// Diagnostics: device bytes the context's work buffers hold (tests check
+// that hg_ctx_reserve leaves nothing for the first calls to grow).
+uint64_t hgk_ctx_device_bytes(hg_ctx* c) {
+    if (!c) return 0;
+    uint64_t t = 0;
+    for (const DevBuf* b : {&c->ws, &c->dctl, &c->bctl, &c->egs, &c->recoff, &c->results, &c->d_in, &c->d_out,
+                            &c->d_aux, &c->d_blk, &c->mws, &c->mres, &c->mspans, &c->mpairs, &c->lk_index,
+                            &c->lk_keys, &c->lk_res, &c->bws, &c->bstage_d, &c->x_res, &c->x_aux, &c->x_arena,
+                            &c->x_spans})
+        t += b->bytes;
+    for (int i = 0; i < c->naux; ++i) t += c->aux_ws[i].bytes;
+    return t;
+}
 int hgk_debug_d2h(void* dst, const void* src, uint64_t n) {
     return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) == hipSuccess ? HG_OK : HG_HIP_FAIL;
 }

@@ -89,8 +89,8 @@ def test_every_stream_ordered_entry_point_refuses_capture():
 
 def test_reserve_then_first_calls_do_not_grow():
     """after hg_ctx_reserve the first encode (its group
-    sums) and a one-table batched decode allocate nothing: the device memory
-    the allocator reports does not move across them."""
+    sums) and a one-table batched decode grow none of the context's work
+    buffers (hgk_ctx_device_bytes, a diagnostics export)."""
     import torch
     from horreum_amd.engine import Engine
     arena, pairs, table = _table(40_000, 904)
@@ -101,14 +101,14 @@ def test_reserve_then_first_calls_do_not_grow():
         da, dp = eng.to_device(arena), eng.to_device(pairs.view(np.uint8))
         out, spans, res = eng.empty(table.size), eng.empty(table.size), eng.empty(128)
         eng.reserve(table.size, n)
-        torch.cuda.synchronize()
-        free0 = torch.cuda.mem_get_info()[0]
+        held = eng.lib.hgk_ctx_device_bytes
+        held.restype, held.argtypes = ctypes.c_uint64, [ctypes.c_void_p]
+        b0 = held(eng.ctx)
         eng.encode_dev_async(da, dp, n, out, table.size, None, 0, None, res)
         eng.decode_batch_dev_async([d], [table.size], [spans], [table.size // 16], res[64:])
         eng.decode_dev_async(d, table.size, spans, table.size // 16, res[64:])
         torch.cuda.synchronize()
-        free1 = torch.cuda.mem_get_info()[0]
-        assert free1 == free0, (free0, free1)
+        assert held(eng.ctx) == b0, (b0, held(eng.ctx))  # no work buffer grew
         assert np.array_equal(out.cpu().numpy(), table)
     finally:
         eng.close()

@@ -96,6 +96,50 @@ __global__ __launch_bounds__(256) void copy_mixed(const u32x4* __restrict__ src,
     }
 }
 
+// Round 6: the read side by LDS-DMA (global_load_lds, the decode pre-pass's
+// 7.1 TB/s read form) into NBUF 16 KiB LDS buffers, NBUF - 1 in flight, the
+// write side by 16-byte nontemporal stores from LDS; each workgroup copies a
+// contiguous span of PPB pieces.
+template <int NBUF>
+__global__ __launch_bounds__(256) void copy_glds(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                 uint32_t ppb) {
+    extern __shared__ u32x4 lbuf[];
+    constexpr uint32_t PIECE = 16384;
+    const uint32_t tid = threadIdx.x, wid = tid >> 6, lane = tid & 63u;
+    const uint64_t base = (uint64_t)blockIdx.x * ppb * PIECE;
+    auto issue = [&](uint32_t k) {
+        const uint8_t* s = src + base + (uint64_t)k * PIECE;
+        uint8_t* d = reinterpret_cast<uint8_t*>(lbuf) + (k % NBUF) * PIECE;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            const uint32_t g0 = q * 256 + wid * 64;
+            __builtin_amdgcn_global_load_lds(static_cast<const void*>(s + (uint64_t)(g0 + lane) * 16),
+                                             (__attribute__((address_space(3))) void*)(d + g0 * 16), 16, 0, 2);
+        }
+    };
+    for (uint32_t k = 0; k + 1 < NBUF && k < ppb; ++k) issue(k);
+    for (uint32_t k = 0; k < ppb; ++k) {
+        if (k + NBUF - 1 < ppb) {
+            issue(k + NBUF - 1);
+            // stores of earlier pieces are older than these DMAs: counted waits
+            // cover them too (conservative)
+            if (NBUF == 2) __asm__ volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else __asm__ volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+            __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        const u32x4* l = lbuf + (k % NBUF) * (PIECE / 16);
+        u32x4* o = reinterpret_cast<u32x4*>(dst + base + (uint64_t)k * PIECE);
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) v[q] = l[q * 256 + tid];
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) __builtin_nontemporal_store(v[q], o + q * 256 + tid);
+        __asm__ volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+}
+
 template <typename F>
 static float time_it(F f) {
     hipEvent_t a, b;
@@ -144,6 +188,27 @@ int main() {
         rep("tile 19x1KiB default", time_it([&] { copy_tile<19, false><<<(uint32_t)nb19, 256>>>(src, dst, n16); }));
         const uint64_t nb76 = (n16 + 256 * 76 - 1) / (256 * 76);
         rep("tile 76x1KiB nt", time_it([&] { copy_tile<76, true><<<(uint32_t)nb76, 256>>>(src, dst, n16); }));
+    }
+    if (getenv("COPY_GLDS")) {
+        const uint32_t npieces = (uint32_t)(bytes / 16384);
+        for (uint32_t ppb : {16u, 32u, 64u, 128u}) {
+            char nm[64];
+            const uint32_t g = npieces / ppb;
+            CHECK(hipFuncSetAttribute((const void*)copy_glds<2>, hipFuncAttributeMaxDynamicSharedMemorySize, 40960));
+            CHECK(hipFuncSetAttribute((const void*)copy_glds<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 49152));
+            snprintf(nm, sizeof nm, "glds copy x2 ppb=%u grid %u", ppb, g);
+            rep(nm, time_it([&] { copy_glds<2><<<g, 256, 40960>>>((const uint8_t*)src, (uint8_t*)dst, ppb); }));
+            snprintf(nm, sizeof nm, "glds copy x3 ppb=%u grid %u", ppb, g);
+            rep(nm, time_it([&] { copy_glds<3><<<g, 256, 49152>>>((const uint8_t*)src, (uint8_t*)dst, ppb); }));
+        }
+        for (int g : {4096, 8192, 16384}) {
+            char nm[64];
+            snprintf(nm, sizeof nm, "grid %d U=8 nt=1", g);
+            rep(nm, time_it([&] { copy_grid<8, true><<<g, 256>>>(src, dst, n16); }));
+        }
+        CHECK(hipFree(src));
+        CHECK(hipFree(dst));
+        return 0;
     }
     for (int g : {256, 512, 1024, 2048}) {  // contiguous chunk per workgroup
         char nm[64];
