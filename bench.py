@@ -204,15 +204,15 @@ def host_cores():
     return max(1, min(share, aff)), nproc, aff
 
 
-def cpu_all_cores(host_sample, seconds=2.0):
+def cpu_all_cores(host_sample, seconds=1.0):
     """The optimised multi-threaded CPU codec (oracle/cpu_opt.c: byte ranges
     with guessed entries handed over in order, spans placed in parallel, not
     owned copies; sizes / prefix / copy for encode; workers started at a
-    barrier, as a pool would hold them) on EVERY core this process may run
-    on (its CPU affinity, capped at the codec's 256 threads), and beside it
-    on the job's OMP_NUM_THREADS share: cfg 2 decode of the same sample,
-    cfg 3 encode of a 1 M-pair sample, and a memcpy of the sample (the
-    CPU's streaming ceiling)."""
+    barrier, as a pool would hold them) at several thread counts up to EVERY
+    core this process may run on (its CPU affinity, capped at the codec's 256
+    threads), the job's OMP_NUM_THREADS share among them: cfg 2 decode of the
+    same sample, cfg 3 encode of a 1 M-pair sample, and a memcpy of the
+    sample (the CPU's streaming ceiling); the best of each is the figure."""
     from horreum_amd import synth
     from oracle import oracle
     share, nproc, aff = host_cores()
@@ -247,23 +247,25 @@ def cpu_all_cores(host_sample, seconds=2.0):
                 "encode_cfg3_1M_GiB_s": round(rate(enc, 304_000_000), 3),
                 "memcpy_GiB_s": round(rate(lambda: oracle.mt_memcpy(cp, host_sample, threads),
                                            host_sample.size), 3)}
-    whole = measure(min(aff, 256))
+    # thread counts: the job's share, powers of two up to every core of the
+    # affinity (the memory system, not the core count, bounds this byte work:
+    # more threads are not always faster), the codec's 256-thread cap
+    counts = sorted({c for c in (share, 32, 64, 128, min(aff, 256)) if 1 <= c <= min(aff, 256)})
+    runs = [measure(c) for c in counts]
     ok = bool(np.array_equal(spans[:1000], oracle.decode(host_sample[:132000])[0])
               and np.array_equal(cp[:4096], host_sample[:4096]))
-    job = measure(share) if share != whole["threads"] else None
     del cp
-    out_d = {"cores": whole["threads"], "nproc": nproc, "affinity": aff, "kind": "port (tuned)",
-             "decode_cfg2_GiB_s": whole["decode_cfg2_GiB_s"],
-             "encode_cfg3_1M_GiB_s": whole["encode_cfg3_1M_GiB_s"],
-             "memcpy_GiB_s": whole["memcpy_GiB_s"],
-             "sample": f"decode: the same {host_sample.size} B cfg 2 sample; encode: 1 M pairs of "
-                       f"32 B / 256 B; hgo_mt_decode / hgo_mt_encode, >= {seconds} s each, on "
-                       f"every core of the process's affinity",
-             "parity_spot": ok}
-    if job is not None:
-        out_d["job_share"] = dict(job, note="the OMP_NUM_THREADS share the GPU box gives one "
-                                            "GPU's job")
-    return out_d
+    best = max(runs, key=lambda r: r["decode_cfg2_GiB_s"])
+    return {"cores": best["threads"], "nproc": nproc, "affinity": aff, "kind": "port (tuned)",
+            "decode_cfg2_GiB_s": best["decode_cfg2_GiB_s"],
+            "encode_cfg3_1M_GiB_s": max(r["encode_cfg3_1M_GiB_s"] for r in runs),
+            "memcpy_GiB_s": max(r["memcpy_GiB_s"] for r in runs),
+            "by_threads": runs,
+            "sample": f"decode: the same {host_sample.size} B cfg 2 sample; encode: 1 M pairs of "
+                      f"32 B / 256 B; hgo_mt_decode / hgo_mt_encode, >= {seconds} s each, at "
+                      f"{counts} threads (every core of the process's affinity the largest); the "
+                      f"best of each is reported",
+            "parity_spot": ok}
 
 
 def cpu_extras(host_sample, seconds=1.0):
