@@ -719,47 +719,6 @@ __device__ uint32_t stride_guess(const uint8_t* data, uint64_t rem, uint32_t cle
     return found;
 }
 
-// stride_guess over the first `lim` bytes of piece 0 only (the prefix the
-// pre-pass DMAs ahead of the piece, HG_SPEC_PREFIX): candidates whose third
-// repeat lies past lim but inside the piece cannot be checked, so if one of
-// them comes before the first candidate found the result is NEED_FULL (the
-// caller guesses on the whole piece) -- the answer is always stride_guess's.
-constexpr uint32_t NEED_FULL = 0xFFFFFFFEu;
-__device__ uint32_t stride_guess_prefix(const uint8_t* data, uint64_t rem, uint32_t clen, uint32_t hz,
-                                        uint32_t lim) {
-    const uint32_t lane = threadIdx.x & 63u;
-    const bool any_valid = rem >= 16;
-    const uint64_t plim64 = any_valid ? rem - 16 : 0;
-    const uint32_t plim = plim64 < 0xFFFFFFFFull ? (uint32_t)plim64 : 0xFFFFFFFFu;
-    uint32_t c = filter_bits(data, lane, hz, clen, plim, any_valid);
-    uint32_t found = NO_GUESS, cut = NO_GUESS;
-    while (c) {
-        const uint32_t b = __ffs(c) - 1;
-        c &= c - 1;
-        const uint32_t p = lane * 16 + b;
-        uint64_t kl, vl;
-        lds_header(data, p, kl, vl);
-        if ((kl >> 32) | (vl >> 32)) continue;
-        const uint64_t R = 16 + kl + vl;
-        if (R > rem - p || p + 3 * R >= clen) continue;
-        if (p + 3 * R >= lim) {  // checkable on the whole piece only
-            cut = p;
-            break;
-        }
-        const uint32_t r = (uint32_t)R;
-        if (hdr_eq(data, p + r, kl, vl) && hdr_eq(data, p + 2 * r, kl, vl) &&
-            hdr_eq(data, p + 3 * r, kl, vl)) {
-            found = p;
-            break;
-        }
-    }
-    for (int d = 32; d >= 1; d >>= 1) {
-        found = min(found, (uint32_t)__shfl_xor((int)found, d, 64));
-        cut = min(cut, (uint32_t)__shfl_xor((int)cut, d, 64));
-    }
-    return cut < found ? NEED_FULL : found;
-}
-
 // ---- general engine -------------------------------------------------------------
 // Header filter, strong candidates, "backed" marks, lane guess and the lane's
 // speculative walk (see the file comment).  All threads call it.
@@ -2042,7 +2001,7 @@ struct SpecSmem {
     uint32_t hcode;           // SpecBatch.pad: how the batch went (SB_*)
     // lane-walk mode (lw_batch): per-wave chunk masks and guess / chain
     // scratch, quarter summaries of the last two stitching rounds
-    alignas(16) uint16_t lw_zm[NW][LW_ZM_WORDS];  // (also the pre-pass's prefix buffer, HG_SPEC_PREFIX)
+    alignas(8) uint16_t lw_zm[NW][LW_ZM_WORDS];
     uint32_t lw_sg[THREADS];
     uint8_t lw_tg[THREADS];
     uint64_t lw_wx[2][NW];
@@ -3290,18 +3249,6 @@ __device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb,
 #error "HG_LW_FUSE needs HG_SPEC_GLDS (the second buffer)"
 #endif
 constexpr uint32_t SPEC_ALT_BYTES = HG_LW_FUSE ? PIECE + 512 : PIECE + 64;  // a piece + halo and zeros
-// HG_SPEC_PREFIX: a batch that guesses its entry (b > 0) has wave 0 DMA its
-// first SPEC_PRE_BYTES and its pieces' halos (by LDS-DMA, not plain loads)
-// AHEAD of piece 0, and guesses from that prefix while pieces 0 and 1 are
-// still landing: the guess no longer sits between piece 0's arrival and the
-// DMA of piece 2 (round 4's timeline: piece 0 took ~13 us of every
-// workgroup's ~150, the stream running dry meanwhile), and no plain halo load
-// makes the compiler wait for piece 1's DMA at piece 0.
-#ifndef HG_SPEC_PREFIX
-#define HG_SPEC_PREFIX 0
-#endif
-constexpr uint32_t SPEC_PRE_BYTES = 2048 + 64;  // the guess's window (64 lanes x 16 B + 3 records) + slack
-constexpr uint32_t SPEC_PRE_LIM = 2048;
 
 __device__ __forceinline__ bool spec_dma(const DecodeArgs& a, uint32_t p, uint8_t* dst) {
     const uint64_t base = (uint64_t)p * PIECE;
@@ -3335,35 +3282,16 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     __shared__ uint64_t spec_alt[SPEC_ALT_BYTES / 8];
     uint8_t* const buf0 = reinterpret_cast<uint8_t*>(s.data64);
     uint8_t* const buf1 = reinterpret_cast<uint8_t*>(spec_alt);
-#if HG_SPEC_PREFIX
-    // the prefix and the halos ahead of piece 0 (wave 0; uniform decision):
-    // the batch's first SPEC_PRE_BYTES into the lane-walk mask rows (unused
-    // until a lane walk, which starts after the guess), the halos into s.halo
-    uint8_t* const pre = reinterpret_cast<uint8_t*>(&s.lw_zm[0][0]);
-    const bool use_pre = b > 0 && (uint64_t)p0 * PIECE + SPEC_PRE_BYTES <= a.rlen &&
-                         (uint64_t)(p0 + np) * PIECE + 16 <= a.rlen;
-    if (use_pre && tid < 64) {
-        const uint32_t lane = tid;
-        if (lane < np) dma16(static_cast<const void*>(a.sst + (uint64_t)(p0 + lane + 1) * PIECE), reinterpret_cast<uint8_t*>(s.halo));
-        const uint8_t* src = a.sst + (uint64_t)p0 * PIECE;
-        dma16(static_cast<const void*>(src + lane * 16), pre);
-        dma16(static_cast<const void*>(src + 1024 + lane * 16), pre + 1024);
-        if (lane < 4) dma16(static_cast<const void*>(src + 2048 + lane * 16), pre + 2048);
-    }
-#else
-    constexpr bool use_pre = false;
-#endif
     bool dma_cur = spec_dma(a, p0, buf0);
 #else
     uint4 v[GPT];
     load_piece(a, p0, v);
-    constexpr bool use_pre = false;
 #endif
     uint4 h = make_uint4(0, 0, 0, 0);
     // (the halos by DMA behind piece 0's, so that piece 0's halo store no
     // longer waits for the next piece's DMA, measured no faster: cfg 2
     // 0.2037 vs 0.1999 ms, same box, profiles/r4_ab_first_piece.log)
-    if (!use_pre && tid < np) h = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
+    if (tid < np) h = load16(a, (uint64_t)(p0 + tid + 1) * PIECE);
     uint64_t X = 0, X0 = 0, total = 0;
     bool ok = true, hop = false;
     int bad = 0;
@@ -3399,13 +3327,6 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         data = cur;
         raw_barrier();  // (A) every wave is done with the other buffer (piece i - 1)
         const bool dma_next = i + 1 < np && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
-#if HG_SPEC_PREFIX
-        if (i == 0 && use_pre && tid < 64) {  // wave 0: the guess from the prefix, pieces 0 / 1 in flight
-            lw_wait_vm(dma_next ? 2 * GPT : GPT);  // (the halos and the prefix are older than piece 0's DMA)
-            const uint32_t f = stride_guess_prefix(pre, rem, clen, a.hz, SPEC_PRE_LIM);
-            if (tid == 0) s.guess = f;
-        }
-#endif
         lw_wait_vm(dma_next ? GPT : 0);  // (and every store before the DMA)
         flush_prefixes();
 #ifdef HG_SPEC_TIMELINE
@@ -3417,7 +3338,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
                 *reinterpret_cast<uint4*>(cur + (q * THREADS + tid) * 16) =
                     load16(a, base + (q * THREADS + tid) * 16);
         }
-        if (i == 0 && !use_pre && tid < np) s.halo[tid] = h;
+        if (i == 0 && tid < np) s.halo[tid] = h;
         if (tid < 4)  // thread 0 reads back its own halo write when i == 0
             *reinterpret_cast<uint4*>(cur + PIECE + tid * 16) = tid == 0 ? s.halo[i] : make_uint4(0, 0, 0, 0);
         raw_barrier();     // (B)
@@ -3433,16 +3354,11 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         if (i == 0 && b == 0) {
             X = X0 = a.entry;  // the first batch's entry is known exactly
         } else if (i == 0) {
-            // (HG_SPEC_PREFIX: s.guess holds the prefix's guess, published by
-            // barrier (B); a NEED_FULL one is redone on the whole piece)
-            if (!use_pre || uni(s.guess) == NEED_FULL) {
-                if (use_pre) __syncthreads();  // every thread has read s.guess
-                if (tid < 64) {
-                    const uint32_t f = stride_guess(data, rem, clen, a.hz);
-                    if (tid == 0) s.guess = f;
-                }
-                __syncthreads();
+            if (tid < 64) {
+                const uint32_t f = stride_guess(data, rem, clen, a.hz);
+                if (tid == 0) s.guess = f;
             }
+            __syncthreads();
             const uint32_t f = uni(s.guess);
 #ifdef HG_SPEC_TIMELINE
             if (tid == 0) tl[4] = __builtin_amdgcn_s_memrealtime();
