@@ -3249,6 +3249,18 @@ __device__ __forceinline__ void spec_publish(const DecodeArgs& a, SpecBatch* sb,
 #error "HG_LW_FUSE needs HG_SPEC_GLDS (the second buffer)"
 #endif
 constexpr uint32_t SPEC_ALT_BYTES = HG_LW_FUSE ? PIECE + 512 : PIECE + 64;  // a piece + halo and zeros
+// HG_SPEC_STWAIT: the wait for piece i's DMA lets the stores the wave issued
+// after the previous wait (thread 0's piece record) stay in flight: they sit
+// between piece i's DMA and piece i + 1's in the wave's in-order vmcnt queue,
+// so a plain vmcnt(GPT) also waited for their write acknowledgement every
+// piece.  Same box, 3 rounds each (profiles/r6_ab_store_wait.log): cfg 2
+// 0.2025 / 0.1971 / 0.1987 -> 0.2005 / 0.1953 / 0.1974 ms, small and medium
+// records ~1 % faster.  Not in compaction mode (KPRE): counting its prefix
+// stores out too took that kernel from 114 to 122 VGPRs and the cfg 5 legs
+// 9.0 -> 10.4 ms and 1.22 -> 1.45 ms.
+#ifndef HG_SPEC_STWAIT
+#define HG_SPEC_STWAIT 1
+#endif
 
 __device__ __forceinline__ bool spec_dma(const DecodeArgs& a, uint32_t p, uint8_t* dst) {
     const uint64_t base = (uint64_t)p * PIECE;
@@ -3302,6 +3314,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
     // issued (one per 16-byte store; a wave issues one when its first lane
     // does), for the counted waits of the LDS-DMA staging.
     const uint32_t w64 = tid & ~63u;  // the wave's first thread
+    uint32_t nst = 0;  // store instructions the wave issued since its last wait (lower bound)
     auto flush_prefixes = [&]() -> uint32_t {
         if (!KPRE || !pf_n) return 0u;
         hg_span* slot = a.scratch + (size_t)pf_piece * MAX_REC_PIECE;
@@ -3327,8 +3340,9 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
         data = cur;
         raw_barrier();  // (A) every wave is done with the other buffer (piece i - 1)
         const bool dma_next = i + 1 < np && spec_dma(a, p + 1, (i & 1) ? buf0 : buf1);
-        lw_wait_vm(dma_next ? GPT : 0);  // (and every store before the DMA)
-        flush_prefixes();
+        // (and every store before the DMA, unless HG_SPEC_STWAIT counts them out)
+        lw_wait_vm(dma_next ? GPT + (HG_SPEC_STWAIT && !KPRE ? nst : 0u) : 0);
+        nst = flush_prefixes();  // (a lower bound of the wave's store instructions)
 #ifdef HG_SPEC_TIMELINE
         if (i == 0 && tid == 0) tl[3] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -3391,6 +3405,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
             o.pad = 0;
             sp[p] = o;
         }
+        if (HG_SPEC_STWAIT && !KPRE && w64 == 0) ++nst;  // thread 0's piece record: wave 0 only
         if (KPRE && ps.kind == PK_STRIDE) {  // compaction mode: key prefixes from LDS
             const uint32_t xr = (uint32_t)(X - base), R = (uint32_t)ps.R;
 #pragma unroll

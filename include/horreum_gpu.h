@@ -162,7 +162,9 @@ const char* hg_last_hip_error(void);
  * The library reads no environment variables; these are its only run-time
  * switches, process-wide, all defaulting to the measured best (the list and
  * their meaning: DESIGN.md section 7).  value < 0 clears a knob.  Returns
- * HG_ERR_INVALID_ARG for an unknown name.  hg_get_knob: -1 when unset. */
+ * HG_ERR_INVALID_ARG for an unknown name.  hg_get_knob: -1 when unset.
+ * A call reads a knob when it needs it (some calls more than once), so set
+ * knobs while no call is in flight on any thread. */
 int hg_set_knob(const char* name, int64_t value);
 int hg_get_knob(const char* name, int64_t* value);
 
