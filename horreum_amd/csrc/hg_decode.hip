@@ -2474,10 +2474,11 @@ __device__ __forceinline__ void lw_chunk_masks(const uint8_t* buf, uint16_t* zm)
 #endif
 __device__ __forceinline__ void lw_masks4(const uint16_t* zm, uint32_t seg0, uint32_t clen,
                                           uint64_t rem, uint64_t& cm0, uint64_t& nextbit,
-                                          uint64_t& zb) {
+                                          uint64_t& zb, uint64_t* nb_raw = nullptr) {
     cm0 = 0;
     nextbit = 0;
     zb = 0;
+    if (nb_raw) *nb_raw = 0;
     if (seg0 >= clen || rem < 16) return;
     const uint32_t gi = seg0 / 16;  // zero-byte bits of bytes seg0 .. seg0 + 79: d0, d1, d2 (16)
     const uint2 z = *reinterpret_cast<const uint2*>(&zm[gi]);
@@ -2503,14 +2504,16 @@ __device__ __forceinline__ void lw_masks4(const uint16_t* zm, uint32_t seg0, uin
     }
     const uint32_t q = seg0 + SEG;
     nextbit = (q < clen && (uint64_t)q <= plim) ? c64 : 0ull;
+    // (past the chunk's last position: the halo's mask bits, for run ends)
+    if (nb_raw) *nb_raw = (uint64_t)q <= plim ? c64 : 0ull;
     cm0 = c;
 }
 
 __device__ __forceinline__ void lw_masks(const uint16_t* zm, uint32_t seg0, uint32_t clen,
                                          uint64_t rem, uint32_t hz, uint64_t& cm0,
-                                         uint64_t& nextbit, uint64_t& zb) {
+                                         uint64_t& nextbit, uint64_t& zb, uint64_t* nb_raw = nullptr) {
     if (HG_LW_LEAN) {
-        lw_masks4(zm, seg0, clen, rem, cm0, nextbit, zb);
+        lw_masks4(zm, seg0, clen, rem, cm0, nextbit, zb, nb_raw);
         return;
     }
     cm0 = 0;
@@ -2771,16 +2774,124 @@ __device__ __forceinline__ bool lw_chunk_serial(const DecodeArgs& a, const uint8
     return __shfl(ok, 0, 64) != 0;
 }
 
+// Round 6: a chunk entered at an exact X is first tried
+// by per-chunk discovery with no walks and no relaxation.  Take every
+// candidate that ENDS a run of header candidates (the masks' filter: a
+// short header also passes 1-3 bytes to its left) at or after X as a record
+// start, read each one's header (independent LDS reads, no chain), and
+// verify the whole set at once: inside a lane each candidate's successor
+// must be the lane's next candidate; a lane's first candidate must be the
+// largest successor of all earlier lanes' last candidates (one DPP max-scan)
+// -- lane je's first must be X -- and the chunk's largest successor must
+// reach its end.  By induction from X the verified set is exactly the
+// record chain (a record start that is not a run end, a false run end, an
+// unreadable record or more than 4 starts in a lane fail the check).  Then a
+// DPP sum-scan places the spans.  A failing chunk takes the lane walks
+// below, which are exact on any input.  Same contract as lw_chunk.
+// Same box, 3 rounds (profiles/r6_ab_lw_verify.log; every run bit-exact
+// against the oracle): small records 0.1366 -> 0.1264 ms, medium 0.1806 ->
+// 0.1637, zero-valued small 0.1465 -> 0.1511 (its chunks skip the try, the
+// gate costs ~3 %), the stride and hop shapes unchanged.  Variants measured
+// on the way: every run end taken (no spacing filter) fails on 2/3 of the
+// small-record chunks (a tiny record's value read 8 bytes in also ends a
+// run): small 0.147; always trying on every chunk: zero-valued small 0.179;
+// a per-stream back-off instead of the zero-byte gate: streams are only 16
+// chunks long, small 0.135.
+#ifndef HG_LW_VERIFY
+#define HG_LW_VERIFY 1
+#endif
+__device__ __forceinline__ bool lw_chunk_verify(const uint8_t* data, uint64_t cb, uint32_t xw,
+                                                uint32_t je, uint32_t seg0, uint32_t clen,
+                                                uint32_t lim, uint64_t cm0, uint64_t nb,
+                                                hg_span* out, uint32_t& count, uint64_t& exit,
+                                                uint32_t& nstores) {
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t re = cm0 & ~((cm0 >> 1) | (nb << 63));  // run ends of this lane's segment
+    if (lane < je) re = 0;
+    else if (lane == je) re &= ~0ull << (xw - seg0);  // starts at or after X (xw - seg0 < 64)
+    // Records are >= 16 bytes apart, so of run ends closer than that at most
+    // one is a start: keep them greedily in position order (the earlier one
+    // -- a tiny record's value / next header read 8 bytes in also ends a
+    // run).  Within the lane, then again from the previous lane's last kept
+    // run end (its first pass; a cascade over a whole lane of run ends
+    // spaced < 16 apart is left to the verification).
+    auto greedy = [&](int32_t last, int32_t& lastk) -> uint64_t {
+        uint64_t kept = 0, t = re;
+        while (t) {
+            const int32_t q = __ffsll((long long)t) - 1;
+            t &= t - 1;
+            if (q - last >= 16) {
+                kept |= 1ull << q;
+                last = q;
+            }
+        }
+        lastk = last;
+        return kept;
+    };
+    int32_t l1 = -64;
+    (void)greedy(-64, l1);
+    const int32_t prevl = __builtin_amdgcn_update_dpp(-1000, l1, 0x138, 0xf, 0xf, false) - 64;
+    int32_t l2 = 0;
+    uint64_t r = greedy(lane == je ? -64 : prevl, l2);  // (lane je: the entry X is exact)
+    const uint32_t n = (uint32_t)__popcll(r);
+    bool ok = n <= 4;
+    const uint32_t lim16 = lim - 16;
+    uint32_t first = 0, nx = 0, p01 = 0, p23 = 0;
+#pragma unroll
+    for (uint32_t it = 0; it < 4; ++it) {
+        if (!r) break;
+        const uint32_t p = seg0 + (uint32_t)(__ffsll((long long)r) - 1);
+        r &= r - 1;
+        uint32_t k0, v0;  // (the mask bit says: readable, high words zero)
+        lds_kv32(data, p, k0, v0);
+        const uint32_t room = lim16 - p;
+        if (k0 > room || v0 > room - k0) ok = false;  // unreadable: the walks report it exactly
+        if (it == 0) first = p;
+        else if (nx != p) ok = false;
+        nx = p + 16 + k0 + v0;
+        if (it == 0) p01 = p;
+        if (it == 1) p01 |= p << 16;
+        if (it == 2) p23 = p;
+        if (it == 3) p23 |= p << 16;
+    }
+    const uint32_t m = dpp_max_incl(n ? nx : 0u);
+    // the previous lanes' largest successor (gfx9 wave_shr:1, lane 0 gets 0)
+    const uint32_t before = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xf, 0xf, false);
+    if (lane == je) ok = ok && n && first == xw;
+    else if (n) ok = ok && before == first;
+    if (__ballot(!ok)) return false;
+    const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
+    if (E < clen) return false;  // a record starts in the chunk after the last run end
+    const uint32_t incl = dpp_sum_incl(n);
+    count = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    exit = cb + E;
+    nstores = 0;
+    if (out) {
+        const uint32_t cmax = (uint32_t)__builtin_amdgcn_readlane((int)dpp_max_incl(n), 63);
+        const uint32_t pre = incl - n;
+        for (uint32_t i = 0; i < cmax; ++i) {  // one store instruction per step
+            if (i < n) {
+                const uint32_t v = i < 2 ? p01 : p23;
+                lw_store_span(out, pre + i, data, cb, (i & 1) ? (v >> 16) : (v & 0xFFFFu));
+            }
+        }
+        nstores = cmax;
+    }
+    return true;
+}
+
 // The staged chunk at cb (records start in [cb, cb + clen)) entered at X
 // (exact; LW_GUESS: at its first lane guess whose walk lands on another
 // lane's guess): spans to out[0, count) (nullptr: none), entry = the entry
 // used, exit = the first start at or after cb + clen, nstores = span store
 // instructions issued.  Wave-level; every lane returns the same values.
+// vs: reserved for a stream-level verification state (unused).
+template <bool VER>
 __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const uint8_t* data,
                                          const uint16_t* zm, uint32_t* sg, uint8_t* tg,
                                          uint64_t cb, uint32_t clen, uint64_t X, hg_span* out,
                                          uint64_t& entry, uint32_t& count, uint64_t& exit,
-                                         uint32_t& nstores) {
+                                         uint32_t& nstores, uint32_t& vs) {
     const uint32_t lane = threadIdx.x & 63u;
     const bool guess = X == LW_GUESS;
     nstores = 0;
@@ -2793,9 +2904,21 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     const uint32_t seg0 = lane * SEG, segend = min(seg0 + SEG, clen);
     const uint32_t je = guess ? 0u : (uint32_t)((X - cb) / SEG);
     const bool in_chunk = seg0 < clen && lane >= je;
-    uint64_t cm0, nb, zb;
-    lw_masks(zm, seg0, clen, rem, a.hz, cm0, nb, zb);
+    uint64_t cm0, nb, zb, nbr = 0;
+    lw_masks(zm, seg0, clen, rem, a.hz, cm0, nb, zb, &nbr);
     const uint32_t lim = (uint32_t)min(rem, (uint64_t)1 << 31);
+    // (a chunk whose bytes are mostly zero -- zero-byte values -- is full of
+    // false run ends: the verification would fail, so it is not tried when a
+    // quarter of its lanes hold >= 40 zero bytes of their 64)
+    if (VER && HG_LW_VERIFY && HG_LW_LEAN && !guess &&
+        __popcll(__ballot(in_chunk && __popcll(zb) >= 40)) < 16 &&
+        lw_chunk_verify(data, cb, (uint32_t)(X - cb), je, seg0, clen, lim, cm0, nbr, out, count, exit,
+                        nstores)) {
+        entry = X;
+        LW_STAMP(4);
+        return true;
+    }
+    (void)vs;
     uint32_t g = NO_GUESS;
     LWalk w;
     w.dead = true;
@@ -2978,6 +3101,7 @@ __device__ __forceinline__ bool lw_chunk_walk(const DecodeArgs& a, const uint8_t
 // through the wave's two LDS chunk buffers: piece records into sp[], spans
 // into the pieces' scratch slots.  Wave-level; returns ok with the entry
 // used, the exit and the records.
+template <bool VER>
 __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint8_t* bufs,
                                           uint16_t* zm, uint32_t* sg, uint8_t* tg, uint32_t pb,
                                           uint32_t pe, uint64_t X, SpecPiece* sp, uint64_t& entry,
@@ -3000,6 +3124,7 @@ __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint
     total = 0;
     entry = X;
     bool ser = false;  // HG_LW_SER: the last chunk's records were few, walk this one by one lane
+    uint32_t vs = 0;   // HG_LW_VERIFY back-off (lw_chunk)
     for (uint64_t k = k0; k < k1; ++k) {
         uint8_t* const cur = bufs + ((k - k0) & 1u) * LW_CBUF;
         uint8_t* const nxt = bufs + ((k - k0 + 1) & 1u) * LW_CBUF;
@@ -3015,7 +3140,7 @@ __device__ __forceinline__ bool lw_stream(SpecSmem& s, const DecodeArgs& a, uint
         uint64_t en = 0, ex = 0;
         uint32_t cnt = 0, nst = 0;
         const bool okc = walk1 ? lw_chunk_walk(a, cur, zm, cb, clen, x, out, en, cnt, ex, nst)
-                               : lw_chunk(s, a, cur, zm, sg, tg, cb, clen, x, out, en, cnt, ex, nst);
+                               : lw_chunk<VER>(s, a, cur, zm, sg, tg, cb, clen, x, out, en, cnt, ex, nst, vs);
         if (!okc) {
             ok = false;
             break;
@@ -3075,6 +3200,9 @@ __device__ __forceinline__ void spec_stage(SpecSmem& s, const uint4 (&v)[GPT], u
 // predecessor's exit is streamed again from it).  On success X0 = entry, X =
 // exit, total = records.  All threads call it (the pieces staged by the
 // caller are not used: every chunk is fetched again, L2-warm).
+// VER: the per-chunk verification (HG_LW_VERIFY) is compiled in -- not in
+// compaction mode, whose kernel it pushed from 114 VGPRs into scratch spills.
+template <bool VER = true>
 __device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const DecodeArgs& a,
                                          uint32_t p0, uint32_t np, SpecPiece* sp, uint64_t& X0,
                                          uint64_t& X, uint64_t& total, uint32_t& why) {
@@ -3101,7 +3229,7 @@ __device__ __forceinline__ bool lw_batch(SpecSmem& s, uint64_t* alt, const Decod
     uint64_t x = 0;
     uint32_t flast = 0;
     for (uint32_t att = 0;; ++att) {  // one call site of lw_stream (first pass and re-streams)
-        if (run) okw = lw_stream(s, a, bufs, zm, sg, tg, pb, pe, xin, sp, en, ex, tot, nlead);
+        if (run) okw = lw_stream<VER>(s, a, bufs, zm, sg, tg, pb, pe, xin, sp, en, ex, tot, nlead);
         run = false;
         const uint32_t f = att & 1u;
         flast = f;
@@ -3445,7 +3573,7 @@ __device__ void spec_body(const DecodeArgs& a, SpecBatch* sb, SpecPiece* sp, uin
 #if HG_LW_FUSE
     if (HG_LW && !ok && hop && __builtin_amdgcn_readfirstlane(s.hcode) == SB_HOP_SMALL) {
         uint32_t why = 0;
-        const bool lok = lw_batch(s, spec_alt, a, p0, np, sp, X0, X, total, why);
+        const bool lok = lw_batch<!KPRE>(s, spec_alt, a, p0, np, sp, X0, X, total, why);
         if (tid == 0) spec_publish(a, sb, b, X0, X, total, lok, lok ? SB_LW : (SB_LW_DEAD | (why << 8)));
         return;
     }
