@@ -859,3 +859,27 @@ def test_stride_batch_tails(engine, where):
         host = np.concatenate([host[:cut], suffix])
         break
     assert_same(engine, host)
+
+
+@pytest.mark.parametrize("shape", [
+    ("tiny", 3_000_000, (0, 3), (0, 3)),      # 16-21 B records: up to 4 starts per 64-byte lane
+    ("empty_mix", 2_500_000, (0, 2), (0, 40)),  # many klen 0 / vlen 0 records (run ends 8 apart)
+    ("small_wide", 1_000_000, (0, 200), (0, 64)),
+])
+def test_lane_walk_chunk_verification_shapes(engine, shape):
+    """Round 6's per-chunk discovery (lw_chunk_verify: run-end candidates
+    kept >= 16 bytes apart, verified at once by DPP scans, the lane walks for
+    chunks that fail it) on shapes that stress it: records of 16-21 bytes
+    (four starts in one lane), empty keys and tombstones (false run ends 8
+    bytes into a record), wider keys; bit-exact vs the oracle whole, cut
+    mid-record, and with a corrupt length planted in the middle (the verified
+    set fails, the exact walk reports the error the oracle reports)."""
+    _, n, kr, vr = shape
+    data = _shape_table(n, kr, vr, seed=11)
+    assert_same(engine, data)
+    assert_same(engine, data[: data.size - 7])
+    bad = data.copy()
+    want = oracle.decode(bad)[0]
+    mid = int(want["off"][want.size // 2])
+    bad[mid + 8: mid + 16] = np.frombuffer(np.uint64(1 << 40).tobytes(), np.uint8)  # vlen past the file
+    assert_same(engine, bad)
