@@ -2797,6 +2797,9 @@ __device__ __forceinline__ bool lw_chunk_serial(const DecodeArgs& a, const uint8
 // run): small 0.147; always trying on every chunk: zero-valued small 0.179;
 // a per-stream back-off instead of the zero-byte gate: streams are only 16
 // chunks long, small 0.135.
+#ifndef HG_LW_VSTORE
+#define HG_LW_VSTORE 1
+#endif
 #ifndef HG_LW_VERIFY
 #define HG_LW_VERIFY 1
 #endif
@@ -2836,6 +2839,13 @@ __device__ __forceinline__ bool lw_chunk_verify(const uint8_t* data, uint64_t cb
     const uint32_t n = (uint32_t)__popcll(r);
     bool ok = n <= 4;
     const uint32_t lim16 = lim - 16;
+    // HG_LW_VSTORE: each candidate's span is stored as soon as its header is
+    // read (placed by the candidates' prefix count); a chunk that fails the
+    // check is stored again, exactly, by the walks (after these stores have
+    // completed), and candidates beyond its true count land inside the
+    // piece's scratch slot (<= 256 per chunk) where nothing reads them.
+    const uint32_t incl = dpp_sum_incl(n);
+    const uint32_t pre = incl - n;
     uint32_t first = 0, nx = 0, p01 = 0, p23 = 0;
 #pragma unroll
     for (uint32_t it = 0; it < 4; ++it) {
@@ -2849,26 +2859,32 @@ __device__ __forceinline__ bool lw_chunk_verify(const uint8_t* data, uint64_t cb
         if (it == 0) first = p;
         else if (nx != p) ok = false;
         nx = p + 16 + k0 + v0;
-        if (it == 0) p01 = p;
-        if (it == 1) p01 |= p << 16;
-        if (it == 2) p23 = p;
-        if (it == 3) p23 |= p << 16;
+        if (HG_LW_VSTORE) {
+            if (out) write_span(out, pre + it, cb + p, k0, v0);
+        } else {
+            if (it == 0) p01 = p;
+            if (it == 1) p01 |= p << 16;
+            if (it == 2) p23 = p;
+            if (it == 3) p23 |= p << 16;
+        }
     }
     const uint32_t m = dpp_max_incl(n ? nx : 0u);
     // the previous lanes' largest successor (gfx9 wave_shr:1, lane 0 gets 0)
     const uint32_t before = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)m, 0x138, 0xf, 0xf, false);
     if (lane == je) ok = ok && n && first == xw;
     else if (n) ok = ok && before == first;
-    if (__ballot(!ok)) return false;
     const uint32_t E = (uint32_t)__builtin_amdgcn_readlane((int)m, 63);
-    if (E < clen) return false;  // a record starts in the chunk after the last run end
-    const uint32_t incl = dpp_sum_incl(n);
+    if (__ballot(!ok) || E < clen) {  // (E < clen: a record starts after the last run end)
+        if (HG_LW_VSTORE && out) lw_wait_vm(0);  // the walks' stores land after these
+        return false;
+    }
     count = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     exit = cb + E;
     nstores = 0;
-    if (out) {
+    if (out && HG_LW_VSTORE) {
+        nstores = (uint32_t)__builtin_amdgcn_readlane((int)dpp_max_incl(n), 63);
+    } else if (out) {
         const uint32_t cmax = (uint32_t)__builtin_amdgcn_readlane((int)dpp_max_incl(n), 63);
-        const uint32_t pre = incl - n;
         for (uint32_t i = 0; i < cmax; ++i) {  // one store instruction per step
             if (i < n) {
                 const uint32_t v = i < 2 ? p01 : p23;
