@@ -117,7 +117,7 @@ def barrier(world, device=None):
 
 
 DECODE_KERNELS = ("decode_spec_kernel", "decode_kernel")
-PMC_TAG = "r5"  # the round whose profiles/<tag>_pmc_*.json the legs cite
+PMC_TAG = "r6"  # the round whose profiles/<tag>_pmc_*.json the legs cite
 
 
 def load_traffic(kernels):
