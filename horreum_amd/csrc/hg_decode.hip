@@ -2333,13 +2333,17 @@ constexpr uint32_t LW_ENTRY_RETRIES = 4;        // guessed entries tried after o
 constexpr uint32_t LW_TRIES = HG_LW_TRIES;      // candidates a lane examines for its guess
 constexpr uint32_t LW_PROF = 8;
 constexpr uint64_t LW_GUESS = ~0ull;            // "enter at the first linked lane guess"
-// Diagnostics (a.sdiag != null, tools/lw_diag.py): lane 0 of wave 0 charges the
-// cycles since the last stamp to phase k (0 waiting for a chunk + its masks,
+// Diagnostics (a build with -DHG_LW_DIAG=1 and a.sdiag != null,
+// tools/lw_diag.py): lane 0 of wave 0 charges the cycles since the last
+// stamp to phase k (0 waiting for a chunk + its masks,
 // 1 guesses + walks, 2 chain marks, 3 relaxation, 4 span stores, 5 stitching,
 // 6 lead-in chunks, 7 relaxation rounds run).
+#ifndef HG_LW_DIAG
+#define HG_LW_DIAG 0  // 1: the lane-walk phase clock (a.sdiag) is compiled in
+#endif
 #define LW_STAMP(k)                                                   \
     do {                                                              \
-        if (a.sdiag && threadIdx.x == 0) {                            \
+        if (HG_LW_DIAG && a.sdiag && threadIdx.x == 0) {              \
             const uint64_t now_ = __builtin_amdgcn_s_memtime();       \
             s.lw_prof[k] += (uint32_t)(now_ - s.lw_last);             \
             s.lw_last = now_;                                         \
@@ -2982,7 +2986,7 @@ __device__ __forceinline__ bool lw_chunk(SpecSmem& s, const DecodeArgs& a, const
     uint32_t st = act ? 0u : 3u;  // 0 walking from g, 1 passed through, 2 waiting, 3 not on the path
     bool conv = false;
     for (uint32_t r = 0; r < LW_WROUNDS; ++r) {
-        if (a.sdiag && threadIdx.x == 0) ++s.lw_prof[7];
+        if (HG_LW_DIAG && a.sdiag && threadIdx.x == 0) ++s.lw_prof[7];
         const uint32_t m = dpp_max_incl(ev);
         // the previous lane's inclusive max: a DPP wave shift (gfx9 wave_shr:1,
         // lane 0 gets 0) instead of __shfl_up's LDS permute round trip

@@ -126,7 +126,30 @@ __device__ __forceinline__ uint32_t zmask4(uint32_t x) { return zflags(x) & 0xFu
 __device__ __forceinline__ uint32_t zbyte_flags(uint32_t x) {
     return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
 }
+#ifndef HG_ZADD64
+#define HG_ZADD64 0  // A/B r6 (profiles/r6_ab_zmask_diag.log): mixed, within noise -- off
+#endif
+// zbyte_flags of two dwords with one 64-bit add (v_lshl_add_u64): the
+// masked bytes are <= 0x7F, so no carry crosses a byte and the 64-bit sum is
+// the two 32-bit ones.
+__device__ __forceinline__ void zbyte_flags2(uint32_t x, uint32_t y, uint32_t& fx, uint32_t& fy) {
+    const uint64_t w = ((uint64_t)y << 32) | x;
+    const uint64_t t = (w & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full;
+    // ~(t | x) & 0x80808080 as one v_bitop3 (truth table bit (t<<2 | x<<1 | c): only 0,0,1)
+    fx = __builtin_amdgcn_bitop3_b32((uint32_t)t, x, 0x80808080u, 0x02);
+    fy = __builtin_amdgcn_bitop3_b32((uint32_t)(t >> 32), y, 0x80808080u, 0x02);
+}
 __device__ __forceinline__ uint32_t zmask16(uint4 v) {
+    if (HG_ZDOT && HG_ZADD64) {
+        uint32_t fx, fy, fz, fw;
+        zbyte_flags2(v.x, v.y, fx, fy);
+        zbyte_flags2(v.z, v.w, fz, fw);
+        const uint32_t lo = __builtin_amdgcn_udot4(
+            fy, 0x80402010u, __builtin_amdgcn_udot4(fx, 0x08040201u, 0u, false), false);
+        const uint32_t hi = __builtin_amdgcn_udot4(
+            fw, 0x80402010u, __builtin_amdgcn_udot4(fz, 0x08040201u, 0u, false), false);
+        return (lo >> 7) | (hi << 1);
+    }
     if (HG_ZDOT) {
         const uint32_t lo = __builtin_amdgcn_udot4(
             zbyte_flags(v.y), 0x80402010u,

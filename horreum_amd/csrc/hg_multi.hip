@@ -31,6 +31,7 @@
 
 #include "hg_internal.hpp"
 #include "hg_knobs.hpp"
+#include "hg_knobs.hpp"
 
 using namespace hgi;
 
@@ -600,7 +601,9 @@ namespace {
 // (a device-to-device copy, or a peer copy over xGMI: a copy, not a collective).
 int copy_dev(hg_ctx* c, void* dst, int src_dev, const void* src, size_t n) {
     if (!n) return HG_OK;
-    const hipError_t e = src_dev == c->device
+    // (HG_MULTI_TEST_PEER_COPY: the peer-copy call on one device too, so a
+    // one-GPU box runs the branch the cross-GPU split takes)
+    const hipError_t e = src_dev == c->device && hgk_knob("HG_MULTI_TEST_PEER_COPY", 0) != 1
                              ? hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, c->stream)
                              : hipMemcpyPeerAsync(dst, c->device, src, src_dev, n, c->stream);
     return e == hipSuccess ? HG_OK : HG_HIP_FAIL;

@@ -186,6 +186,8 @@ Knob g_knobs[] = {
     {"HG_MERGE_TEST_LB_EXPIRE", 0, false},   // test hook: the first merge's final-round tile k
                                              // acts as if its look-back wait ran over budget
     {"HG_RANK_NOPACK", 0, false},        // 1: rank path with plain ranks at any size
+    {"HG_MULTI_TEST_PEER_COPY", 0, false},  // test hook: 1: same-device context copies also
+                                             // take the peer-copy call (the cross-GPU branch)
     {"HG_DEBUG_POISON", 0, false},       // 1: new device buffers filled with 0xA5 (diagnostics)
 };
 std::mutex g_knob_mu;

@@ -297,6 +297,22 @@ def test_compact_dev_capacity_reports_slice_sizes(engine, multi2):
     assert np.array_equal(got, single.data) and sum(orc) == single.n
 
 
+@pytest.mark.parametrize("k,n_universe,frac,seed", [(6, 20000, 0.3, 51), (8, 12000, 0.5, 52)])
+def test_compact_dev_peer_copy_call_on_one_device(engine, multi3, knobs, k, n_universe, frac, seed):
+    """The cross-GPU split's copy branch (hipMemcpyPeerAsync, hg_multi.hip
+    copy_dev) run on one device (HG_MULTI_TEST_PEER_COPY=1: same-device
+    contexts take the peer-copy call too): slices byte-identical to the
+    single-context compaction, as with device-to-device copies."""
+    knobs("HG_MULTI_TEST_PEER_COPY", 1)
+    tables = sorted_tables(k, n_universe, frac, seed)
+    rc, got, nrec, res, single, ol = _compact_dev_case(engine, multi3, tables,
+                                                       [t % 3 for t in range(k)])
+    assert rc == 0 and single.status == 0
+    assert nrec == single.n == res.n_out
+    assert np.array_equal(got, single.data)
+    assert sum(1 for x in ol if x) >= 2
+
+
 # ---- contexts on distinct devices (skipped on a one-GPU box) -----------------------------
 @pytest.mark.skipif("not __import__('torch').cuda.device_count() >= 2",
                     reason="needs two GPUs: the peer-copy branch of the split")

@@ -5,7 +5,9 @@ batch, s_memtime cycles per phase as thread 0 of the workgroup sees them
 4 count scan, 5 span stores, 6 lead-in probe, 7 rounds run), for the
 decode_variants workloads named on the command line (default small medium).
 The instrumented launch goes through hgk_decode_launch_diag; its timing is
-not quoted anywhere."""
+not quoted anywhere.  The phase clock is compiled in only by
+`tools/build_variant.sh diag "-DHG_LW_DIAG=1"` (run with HG_LIBRARY pointing at
+build_exp/diag/libhorreum_gpu.so); the default build records nothing."""
 import ctypes
 import json
 import os
