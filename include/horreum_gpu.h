@@ -161,7 +161,7 @@ const char* hg_last_hip_error(void);
 /* Knobs: batch-geometry overrides, A/B switches and test hooks (ABI 6).
  * The library reads no environment variables; these are its only run-time
  * switches, process-wide, all defaulting to the measured best (the list and
- * their meaning: DESIGN.md section 7).  value < 0 clears a knob.  Returns
+ * their meaning: DESIGN.md section 1, "No environment reads").  value < 0 clears a knob.  Returns
  * HG_ERR_INVALID_ARG for an unknown name.  hg_get_knob: -1 when unset.
  * A call reads a knob when it needs it (some calls more than once), so set
  * knobs while no call is in flight on any thread. */
