@@ -632,9 +632,6 @@ typedef uint32_t m_u32x4 __attribute__((ext_vector_type(4)));
 #define HG_REC_GU 1  // cfg 5 leg: 1 595 us, 2 630 us (more spills)
 #endif
 constexpr uint32_t REC_GU = HG_REC_GU;
-#ifndef HG_FIN_TICKET
-#define HG_FIN_TICKET 1  // the last round's tile order from an atomic ticket (else blockIdx)
-#endif
 #ifndef HG_REC_WAVES
 #define HG_REC_WAVES 5
 #endif
@@ -675,11 +672,11 @@ __global__ __launch_bounds__(THREADS, MODE == 1 ? 6 : MODE == 2 ? HG_REC_WAVES :
     // tile's XCD) that wait ran out the spin budget and the merge went to a
     // redo, 4-125 s per compaction (profiles/r5_bench_n2_shared_gpu_rehearsal.json).
     __shared__ uint32_t fin_ticket;
-    if (FINAL && HG_FIN_TICKET) {
+    if (FINAL) {
         if (tid == 0) fin_ticket = atomicAdd(reinterpret_cast<unsigned int*>(f.st + 2 * (uint64_t)f.ntiles), 1u);
         __syncthreads();
     }
-    const uint32_t bx = FINAL && HG_FIN_TICKET ? fin_ticket : blockIdx.x;
+    const uint32_t bx = FINAL ? fin_ticket : blockIdx.x;
     const uint64_t t0 = (uint64_t)bx * TILE;
     if (t0 >= a.n) return;
     const bool fin_lds = FINAL && a.ntables <= FIN_LDS_TABLES;
