@@ -448,16 +448,21 @@ def test_batch_decode_guess_shapes(engine):
         assert np.array_equal(engine.spans_to_numpy(spans[i], min(n, caps[i])), ws), i
 
 
-def _shape_table(n, kr, vr, seed):
+def _shape_table(n, kr, vr, seed, zero_values=False):
     """decode_variants-style table built vectorised: n records, key lengths in
     [kr[0], kr[1]), value lengths in [vr[0], vr[1]) (5 % tombstones), random
-    payload bytes."""
+    payload bytes (zero_values: every value byte 0)."""
     rng = np.random.default_rng(seed)
     kl = rng.integers(*kr, n)
     vl = rng.integers(*vr, n)
     vl[rng.random(n) < 0.05] = 0
     offs = np.concatenate([[0], np.cumsum(16 + kl + vl)])
     buf = rng.integers(0, 256, int(offs[-1]), dtype=np.uint8)
+    if zero_values:  # value byte <=> inside [start + 16 + klen, next start)
+        d = np.zeros(buf.size + 1, np.int32)
+        np.add.at(d, offs[:-1] + 16 + kl, 1)
+        np.add.at(d, offs[1:], -1)
+        buf[np.cumsum(d[:-1]) > 0] = 0
     hdr = np.stack([kl, vl], axis=1).astype("<u8").view(np.uint8).reshape(n, 16)
     for i in range(16):
         buf[offs[:-1] + i] = hdr[:, i]
@@ -865,6 +870,11 @@ def test_stride_batch_tails(engine, where):
     ("tiny", 3_000_000, (0, 3), (0, 3)),      # 16-21 B records: up to 4 starts per 64-byte lane
     ("empty_mix", 2_500_000, (0, 2), (0, 40)),  # many klen 0 / vlen 0 records (run ends 8 apart)
     ("small_wide", 1_000_000, (0, 200), (0, 64)),
+    # zero-byte values: zero-heavy chunks (the gate), mixed with checked ones
+    ("zero_small", 1_500_000, (1, 24), (0, 64), True),
+    ("zero_small_empty_keys", 1_500_000, (0, 24), (0, 64), True),
+    ("zero_midlarge", 200_000, (16, 17), (400, 1200), True),
+    ("zero_tiny", 2_000_000, (1, 3), (0, 24), True),
 ])
 def test_lane_walk_chunk_verification_shapes(engine, shape):
     """Round 6's per-chunk discovery (lw_chunk_verify: run-end candidates
@@ -873,9 +883,11 @@ def test_lane_walk_chunk_verification_shapes(engine, shape):
     (four starts in one lane), empty keys and tombstones (false run ends 8
     bytes into a record), wider keys; bit-exact vs the oracle whole, cut
     mid-record, and with a corrupt length planted in the middle (the verified
-    set fails, the exact walk reports the error the oracle reports)."""
-    _, n, kr, vr = shape
-    data = _shape_table(n, kr, vr, seed=11)
+    set fails, the exact walk reports the error the oracle reports).  Zero-
+    valued shapes: their zero-heavy chunks skip the check (the gate) and
+    take the walks, the other chunks the check."""
+    n, kr, vr = shape[1:4]
+    data = _shape_table(n, kr, vr, seed=11, zero_values=len(shape) > 4 and shape[4])
     assert_same(engine, data)
     assert_same(engine, data[: data.size - 7])
     bad = data.copy()
