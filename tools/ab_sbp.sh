@@ -1,3 +1,6 @@
+#!/bin/bash
+# Pre-pass batch size A/B (knob HG_DECODE_SBP via the environment, forwarded by
+# tools/decode_variants.py) on the lane-walk shapes: default, 8 and 32 pieces.
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out && export TMPDIR=/tmp
 for r in 1 2; do for v in 0 8 32; do
   if [ $v = 0 ]; then unset HG_DECODE_SBP; else export HG_DECODE_SBP=$v; fi
